@@ -1,0 +1,184 @@
+/*
+ * mininf_amd.h -- C ABI of the MI355X (gfx950) ELBO hot path.
+ *
+ * The reference (tillahoffmann/mininf) is pure Python on PyTorch and has no FFI of its own; its
+ * "operator API" for the ELBO path is three Python seams:
+ *   1. the tracer plugin point  -- mininf/core.py:128-140 (TracerMixin.sample), dispatched from
+ *      mininf/core.py:325-328 (sample);
+ *   2. the Distribution protocol consumed at mininf/core.py:233-241 (log_prob) and
+ *      mininf/nn.py:124-145, 217, 226 (rsample / entropy);
+ *   3. the loss module mininf/nn.py:212-228 (EvidenceLowerBoundLoss.forward).
+ * Every entry point below replaces the arithmetic behind one of those seams; the comment above each
+ * one names the reference line(s) and the torch.distributions code it stands in for.
+ *
+ * Conventions (all entry points):
+ *   - return 0 on success, a negative MI_E* code for an invalid argument, or a positive hipError_t;
+ *   - never throw across the ABI, never allocate device memory (workspaces are caller-provided and
+ *     sized by the matching *_workspace_bytes query), never synchronise the host;
+ *   - asynchronous on the given stream (`stream` is a hipStream_t; NULL = the null stream);
+ *   - tensors are device pointers plus int64 element strides over a logical [K, N] space
+ *     (K = Monte-Carlo particles, N = flattened elements of one site); a stride of 0 broadcasts;
+ *   - floating-point data is IEEE fp32 (the reference's default dtype); accumulation is fp32
+ *     within a wavefront and fp64 across wavefronts.
+ */
+#ifndef MININF_AMD_H
+#define MININF_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_ABI_VERSION 1
+
+#define MI_MAX_SITES 4
+#define MI_MAX_OPERANDS 6
+#define MI_MAX_SLOTS 4
+
+/* error codes (negative) */
+#define MI_EINVAL (-1)      /* malformed descriptor or size */
+#define MI_EWORKSPACE (-2)  /* workspace too small */
+#define MI_EUNSUPPORTED (-3)
+
+/* site families (torch.distributions formulas they restate are cited in sites.hip) */
+enum mi_family {
+  MI_NORMAL = 0,            /* roles: loc, scale, value          torch/distributions/normal.py:88-103 */
+  MI_BERNOULLI_LOGITS = 1,  /* roles: logits, -, value            torch/distributions/bernoulli.py:121-125 */
+  MI_BERNOULLI_PROBS = 2,   /* roles: probs, -, value (clamped)   bernoulli.py:104-106, utils.py:101-137 */
+  MI_BETA = 3               /* roles: concentration1, concentration0, value  beta.py:88-92, dirichlet.py:90-97 */
+};
+
+/* what to do with d(site total)/d(operand) */
+enum mi_grad_mode {
+  MI_GRAD_NONE = 0,
+  MI_GRAD_DENSE = 1,     /* write g0 * dT_k/dx[k,i] to `grad` (same logical [K,N] space) */
+  MI_GRAD_PARTICLE = 2   /* operand is one scalar per particle: reduce dT_k/dx[k] into slot `slot` */
+};
+
+/* flag bits reported per site */
+#define MI_FLAG_SUPPORT 1u  /* a (non-masked) value lies outside the family's support */
+#define MI_FLAG_PARAM 2u    /* a parameter violates its constraint (e.g. scale <= 0) */
+
+typedef struct mi_operand {
+  const float* data;
+  int64_t stride_k;
+  int64_t stride_i;
+  int32_t grad_mode;     /* enum mi_grad_mode */
+  int32_t slot;          /* MI_GRAD_PARTICLE: reduction slot in [0, num_slots) */
+  float* grad;           /* MI_GRAD_DENSE: output */
+  int64_t grad_stride_k;
+  int64_t grad_stride_i;
+} mi_operand;
+
+typedef struct mi_site {
+  int32_t family;        /* enum mi_family */
+  int32_t operand[3];    /* role -> operand index, or -1 to use constant[role] */
+  float constant[3];
+  int32_t pad0;
+  const uint8_t* mask;   /* NULL = all observed; else bool bytes, masked-out elements contribute 0 */
+  int64_t mask_stride_k;
+  int64_t mask_stride_i;
+  double scale;          /* minibatch scale: declared batch numel / observed numel (core.py:267-271) */
+} mi_site;
+
+/* A group of sites evaluated over one shared [K, N] element space in a single pass, so that an
+ * operand read by several sites (e.g. a latent z that is the value of one site and the loc of
+ * another) is loaded once and its gradient accumulated in registers. */
+typedef struct mi_group {
+  int64_t K;
+  int64_t N;
+  int32_t num_sites;
+  int32_t num_operands;
+  int32_t num_slots;
+  int32_t compute_grads; /* 0: forward values only */
+  float grad_scale;      /* g0: upstream dL/dT_k assumed for MI_GRAD_DENSE outputs */
+  int32_t pad0;
+  mi_site sites[MI_MAX_SITES];
+  mi_operand operands[MI_MAX_OPERANDS];
+} mi_group;
+
+/* Library identification: returns MI_ABI_VERSION and writes the offload target ("gfx950"). */
+int mi_abi_version(char* target, size_t target_bytes);
+
+/* ---- site log-probability accumulation (replaces core.py:211-273 + torch log_prob) ------------ */
+
+/* Workspace needed by mi_group_forward for this descriptor. */
+int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);
+
+/* Evaluate all sites of `group` for every particle:
+ *   total[k]              = sum_s scale_s * sum_i mask_si * log p_s(value_ki | params_ki)  (fp32)
+ *   site_lp[s*K + k]      = scale_s * sum_i mask_si * log p_s(...)  (fp64; may be NULL)
+ *   slot_grad[j*K + k]    = dT_k / d x[k] for MI_GRAD_PARTICLE operands mapped to slot j (fp32)
+ *   operands[o].grad      = g0 * dT_k / d x[k,i] for MI_GRAD_DENSE operands
+ *   flags[s]              = OR of MI_FLAG_* found for site s (zeroed by this call)
+ * Replaces LogProbTracer.sample's dist.log_prob (core.py:241, masked branch core.py:231-239),
+ * LogProbTracer.total/contribution (core.py:247-273) and the autograd backward of the same ops. */
+int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,
+                     double* site_lp, float* slot_grad, uint32_t* flags, void* stream);
+
+/* Backward rescale of a speculative dense gradient: row k of x is multiplied by g[k] / g0; thread
+ * blocks whose rows all have g[k] == g0 return immediately (the common ELBO case). */
+int mi_scale_rows(float* x, int64_t stride_k, int64_t stride_i, int64_t K, int64_t N,
+                  const float* g, float g0, void* stream);
+
+/* Categorical site: logits[k, i, c] (already normalised, categorical.py:74-78), value int64[i]:
+ *   total[k] += scale * sum_i mask_i * logits[k, i, value_i]       (categorical.py:150-156)
+ * and, when dlogits != NULL, dlogits[k,i,c] = g0 * scale * mask_i * [c == value_i] (dense). */
+int mi_categorical_forward(const float* logits, int64_t stride_k, int64_t stride_i,
+                           int64_t stride_c, int64_t K, int64_t N, int64_t C,
+                           const int64_t* value, int64_t value_stride_k, int64_t value_stride_i,
+                           const uint8_t* mask, int64_t mask_stride_i, double scale, float g0,
+                           float* dlogits, void* workspace, size_t workspace_bytes, float* total,
+                           uint32_t* flags, void* stream);
+int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
+
+/* ---- guide reparameterised sampling (replaces nn.py:133-145 -> Normal/Beta.rsample) ------------ */
+
+/* Counter-based Philox-4x32-10 normals: eps[k, i] is a function of (seed, step, stream_id,
+ * particle_offset + k, i) only, so the union of draws is independent of how particles are sharded
+ * across GPUs. z[k, i] = loc[i] + eps[k, i] * scale[i] (normal.py:83-86). If `eps` is non-NULL it is
+ * used instead of the generator (parity mode: injected host noise, row-major [K, N]). */
+int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
+                      int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                      int64_t particle_offset, const float* eps, float* z, void* stream);
+
+/* Backward of mi_normal_rsample: dloc[i] = sum_k dz[k,i], dscale[i] = sum_k dz[k,i] * eps[k,i]
+ * with eps regenerated from the counter (or read from `eps`). */
+int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
+int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
+                               int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                               uint32_t stream_id, int64_t particle_offset, const float* eps,
+                               void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
+                               void* stream);
+
+/* Beta(concentration1, concentration0) draws x[k, i] = G1 / (G1 + G0) with Marsaglia-Tsang gamma
+ * variates from the same counter-based generator (beta.py:85-86, dirichlet.py:23-36, 85-88). With
+ * `x_in` non-NULL the draws are copied from it instead (parity mode). */
+int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t c0_stride,
+                    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                    int64_t particle_offset, const float* x_in, float* x, void* stream);
+
+/* Implicit reparameterisation gradient of the Beta draws (dirichlet.py:17-20 ->
+ * torch._dirichlet_grad, ATen/native/Distributions.h dirichlet_grad_one), reduced over particles:
+ *   dc1[i] = sum_k dx[k,i] * dgrad(x, c1, c1+c0) * (1 - x)
+ *   dc0[i] = -sum_k dx[k,i] * dgrad(1 - x, c0, c1+c0) * x */
+int mi_beta_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
+int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
+                             const float* x, const float* c1, int64_t c1_stride, const float* c0,
+                             int64_t c0_stride, int64_t K, int64_t N, void* workspace,
+                             size_t workspace_bytes, float* dc1, float* dc0, void* stream);
+
+/* Raw generator output for tests: out[k, i] = standard normal eps of mi_normal_rsample. */
+int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                     int64_t particle_offset, float* out, void* stream);
+/* Raw Philox-4x32-10 blocks for known-answer tests: out[4*j .. 4*j+3] = philox(ctr[j], key). */
+int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t key1, uint32_t* out,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MININF_AMD_H */

@@ -1,0 +1,145 @@
+"""
+ctypes binding of ``libmininf_amd.so`` -- the C ABI declared in ``include/mininf_amd.h``.
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (``hipcc --offload-arch=gfx950``)
+and loaded from this package directory. There is deliberately no fallback: if the library is missing
+or a launch fails, :func:`lib` / :func:`check` raise, so a GPU run can never silently fall back to
+PyTorch or CPU arithmetic.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+
+LIB_NAME = "libmininf_amd.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+MAX_SITES = 4
+MAX_OPERANDS = 6
+MAX_SLOTS = 4
+
+NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
+GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
+FLAG_SUPPORT, FLAG_PARAM = 1, 2
+
+c_i64 = ctypes.c_int64
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_vp = ctypes.c_void_p
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [
+        ("data", c_vp), ("stride_k", c_i64), ("stride_i", c_i64),
+        ("grad_mode", ctypes.c_int32), ("slot", ctypes.c_int32),
+        ("grad", c_vp), ("grad_stride_k", c_i64), ("grad_stride_i", c_i64),
+    ]
+
+
+class Site(ctypes.Structure):
+    _fields_ = [
+        ("family", ctypes.c_int32), ("operand", ctypes.c_int32 * 3),
+        ("constant", ctypes.c_float * 3), ("pad0", ctypes.c_int32),
+        ("mask", c_vp), ("mask_stride_k", c_i64), ("mask_stride_i", c_i64),
+        ("scale", ctypes.c_double),
+    ]
+
+
+class Group(ctypes.Structure):
+    _fields_ = [
+        ("K", c_i64), ("N", c_i64),
+        ("num_sites", ctypes.c_int32), ("num_operands", ctypes.c_int32),
+        ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
+        ("grad_scale", ctypes.c_float), ("pad0", ctypes.c_int32),
+        ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
+    ]
+
+
+# name -> (restype, argtypes). Mirrors include/mininf_amd.h one to one.
+_SIGNATURES = {
+    "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "mi_group_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Group),
+                                                ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_group_forward": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp]),
+    "mi_scale_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_float,
+                                     c_vp]),
+    "mi_categorical_workspace_bytes": (ctypes.c_int, [c_i64, c_i64,
+                                                      ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_categorical_forward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                              c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_double,
+                                              ctypes.c_float, c_vp, c_vp, ctypes.c_size_t, c_vp,
+                                              c_vp, c_vp]),
+    "mi_normal_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                         c_vp]),
+    "mi_normal_rsample_backward_workspace_bytes": (ctypes.c_int, [
+        c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_normal_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64,
+                                                  ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                                  ctypes.c_size_t, c_vp, c_vp, c_vp]),
+    "mi_beta_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp]),
+    "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
+        c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                                c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp, c_vp,
+                                                c_vp]),
+    "mi_philox_normal": (ctypes.c_int, [c_i64, c_i64, ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_uint32, c_i64, c_vp, c_vp]),
+    "mi_philox4x32": (ctypes.c_int, [c_vp, c_i64, ctypes.c_uint32, ctypes.c_uint32, c_vp, c_vp]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """
+    Load (once) and return the HIP library. Raises if it has not been built.
+    """
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} is missing; build it with `python -c 'import "
+                              "__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950).")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (restype, argtypes) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        _LIB = handle
+    return _LIB
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        kind = {-1: "invalid argument", -2: "workspace too small", -3: "unsupported"}.get(
+            code, f"hipError_t {code}")
+        raise NativeError(f"{what} failed: {kind}")
+
+
+def stream_handle(device: torch.device) -> int:
+    """
+    hipStream_t of torch's current stream on ``device`` (kernels are ordered with torch's own).
+    """
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(tensor: Optional[torch.Tensor]) -> Optional[int]:
+    return None if tensor is None else tensor.data_ptr()
+
+
+def require_device(tensor: torch.Tensor, what: str) -> None:
+    if tensor.device.type != "cuda":
+        raise NativeError(f"{what} must live on a ROCm device for the MI355X ELBO engine, got "
+                          f"{tensor.device}. Move the data and the guide to 'cuda' (HIP).")

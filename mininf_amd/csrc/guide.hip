@@ -1,0 +1,493 @@
+// Reparameterised guide sampling and its backward, for the mean-field Normal and Beta guide factors.
+//
+// Replaces FactorizedDistribution.rsample (mininf/nn.py:133-145) for those families, i.e.
+// torch Normal.rsample (torch/distributions/normal.py:83-86: loc + eps * scale) and Beta.rsample
+// (beta.py:85-86 -> dirichlet.py:23-36, 85-88: normalised gamma draws), plus the gradients autograd
+// would compute through them (Normal: d/dloc, d/dscale; Beta: the implicit reparameterisation
+// gradient torch._dirichlet_grad, ATen/native/Distributions.h dirichlet_grad_one).
+//
+// Layout: draws are written row-major z[k, i] (particles x elements) so that the site kernels read
+// them with unit stride along elements. eps is never stored: the backward regenerates it from the
+// Philox counter (seed, step, stream, global particle, element quad).
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace mi {
+
+constexpr int kGuideThreads = 256;
+
+// -------------------------------------------------------------------------------------------------
+// Normal
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
+    const float* __restrict__ loc, int64_t loc_s, const float* __restrict__ scale, int64_t scale_s,
+    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff,
+    const float* __restrict__ eps_in, float* __restrict__ z, int64_t rows_per_block) {
+  const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  const int64_t i0 = quad * 4;
+  if (i0 >= N) return;
+  const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t k1 = min(K, k0 + rows_per_block);
+  float m[4], sd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = min(i0 + j, N - 1);
+    m[j] = loc[i * loc_s];
+    sd[j] = scale[i * scale_s];
+  }
+  const bool full = (i0 + 4 <= N) && ((N & 3) == 0);
+  for (int64_t k = k0; k < k1; ++k) {
+    float e[4];
+    if (eps_in != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
+    } else {
+      guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+    }
+    float out[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = fmaf(e[j], sd[j], m[j]);
+    if (full) {
+      *reinterpret_cast<float4*>(z + k * N + i0) = make_float4(out[0], out[1], out[2], out[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (i0 + j < N) z[k * N + i0 + j] = out[j];
+    }
+  }
+}
+
+// Partial sums over particle slices: part[(slice * 2 + {0: dloc, 1: dscale}) * N + i].
+__global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
+    const float* __restrict__ dz, int64_t dz_sk, int64_t dz_si, int64_t K, int64_t N,
+    uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in,
+    float* __restrict__ out_loc, float* __restrict__ out_scale, int64_t out_stride,
+    int64_t rows_per_block) {
+  const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  const int64_t i0 = quad * 4;
+  if (i0 >= N) return;
+  const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t k1 = min(K, k0 + rows_per_block);
+  const bool vec = (dz_si == 1) && (i0 + 4 <= N) && ((N & 3) == 0) && ((dz_sk & 3) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(dz) & 15) == 0);
+  float sl[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t k = k0; k < k1; ++k) {
+    float g[4];
+    if (vec) {
+      const float4 v = *reinterpret_cast<const float4*>(dz + k * dz_sk + i0);
+      g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = (i0 + j < N) ? dz[k * dz_sk + (i0 + j) * dz_si] : 0.0f;
+    }
+    float e[4];
+    if (eps_in != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
+    } else {
+      guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sl[j] += g[j];
+      ss[j] = fmaf(g[j], e[j], ss[j]);
+    }
+  }
+  const int64_t slice = blockIdx.y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (i0 + j < N) {
+      out_loc[slice * out_stride + i0 + j] = sl[j];
+      out_scale[slice * out_stride + i0 + j] = ss[j];
+    }
+  }
+}
+
+// Sum `slices` rows of a [slices, N] partial array (fixed order, fp64).
+__global__ __launch_bounds__(kGuideThreads) void k_sum_slices(const float* __restrict__ part,
+                                                              int64_t slices, int64_t N,
+                                                              float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (i >= N) return;
+  double acc = 0.0;
+  for (int64_t s = 0; s < slices; ++s) acc += (double)part[s * N + i];
+  out[i] = (float)acc;
+}
+
+// -------------------------------------------------------------------------------------------------
+// Beta via two Marsaglia-Tsang gamma variates (G. Marsaglia, W. W. Tsang, "A simple method for
+// generating gamma variables", ACM TOMS 26(3), 2000), with the alpha < 1 boost
+// G(alpha) = G(alpha + 1) * U^(1/alpha).
+// -------------------------------------------------------------------------------------------------
+struct Stream {
+  uint64_t seed, step;
+  uint32_t stream_id, sub;
+  uint64_t elem, particle;
+  uint32_t block = 0;
+  U4 bits{};
+  int used = 4;
+  MI_DEV uint32_t next() {
+    if (used == 4) {
+      U4 c{(uint32_t)elem, (uint32_t)particle, (uint32_t)step ^ (uint32_t)(step >> 32),
+           (stream_id << 8) | (sub << 6) | (block & 63u)};
+      bits = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      ++block;
+      used = 0;
+    }
+    const uint32_t out = used == 0 ? bits.x : used == 1 ? bits.y : used == 2 ? bits.z : bits.w;
+    ++used;
+    return out;
+  }
+  MI_DEV float uniform() { return u01(next()); }
+  MI_DEV float normal() {
+    float a, b;
+    box_muller(next(), next(), a, b);
+    return a;
+  }
+};
+
+MI_DEV float sample_gamma(float alpha, Stream& rng) {
+  float boost = 1.0f;
+  if (!(alpha > 0.0f)) return 0.0f;
+  if (alpha < 1.0f) {
+    boost = powf(rng.uniform(), 1.0f / alpha);
+    alpha += 1.0f;
+  }
+  const float d = alpha - 1.0f / 3.0f;
+  const float c = 1.0f / sqrtf(9.0f * d);
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    float x, y;
+    int tries = 0;
+    do {
+      x = rng.normal();
+      y = 1.0f + c * x;
+    } while (y <= 0.0f && ++tries < 16);
+    if (y <= 0.0f) continue;
+    const float v = y * y * y;
+    const float u = rng.uniform();
+    const float xx = x * x;
+    if (u < 1.0f - 0.0331f * xx * xx) return boost * d * v;
+    if (logf(u) < 0.5f * xx + d * (1.0f - v + logf(v))) return boost * d * v;
+  }
+  return boost * d;  // not reached in practice (acceptance > 95 % per attempt)
+}
+
+__global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
+    const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
+    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff,
+    const float* __restrict__ x_in, float* __restrict__ x) {
+  const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (t >= K * N) return;
+  const int64_t k = t / N, i = t - k * N;
+  if (x_in != nullptr) {
+    x[t] = x_in[t];
+    return;
+  }
+  Stream ra{seed, step, stream_id, 0u, (uint64_t)i, (uint64_t)(poff + k)};
+  Stream rb{seed, step, stream_id, 1u, (uint64_t)i, (uint64_t)(poff + k)};
+  const float g1 = sample_gamma(c1[i * c1_s], ra);
+  const float g0 = sample_gamma(c0[i * c0_s], rb);
+  const float s = g1 + g0;
+  x[t] = s > 0.0f ? g1 / s : (c1[i * c1_s] >= c0[i * c0_s] ? 1.0f : 0.0f);
+}
+
+// ---- Beta implicit reparameterisation gradient -----------------------------------------------
+// Restatement (fp64 throughout) of the piecewise approximation used by torch._dirichlet_grad
+// (torch/include/ATen/native/Distributions.h, dirichlet_grad_one and helpers): the derivative of the
+// Beta(alpha, total - alpha) draw x with respect to alpha, -(d/dalpha CDF) / pdf, divided by
+// (1 - x). Four regimes: x near 0 (Taylor series), x near 1 (series for the mirrored variable),
+// both shapes large (Rice saddle-point expansion), otherwise a fitted rational correction of the
+// analytic approximation x (psi(total) - psi(alpha)) / beta.
+MI_DEV double beta_grad_small_alpha(double x, double a, double b) {
+  const double factor = digamma(a) - digamma(a + b) - log(x);
+  double coeff = 1.0;
+  double series = coeff / a * (factor + 1.0 / a);
+  for (int n = 1; n <= 10; ++n) {
+    coeff *= (n - b) * x / n;
+    const double den = a + n;
+    series += coeff / den * (factor + 1.0 / den);
+  }
+  const double r = x * pow(1.0 - x, -b) * series;
+  return r != r ? 0.0 : r;
+}
+
+MI_DEV double beta_grad_small_beta(double x, double a, double b) {
+  const double factor = digamma(a + b) - digamma(b);
+  double coeff = 1.0, prod = 1.0, dprod = 0.0, series = factor / a;
+  for (int n = 1; n <= 8; ++n) {
+    coeff *= -x / n;
+    dprod = dprod * (b - n) + prod;
+    prod *= (b - n);
+    series += coeff / (a + n) * (dprod + factor * prod);
+  }
+  const double r = -pow(1.0 - x, 1.0 - b) * series;
+  return r != r ? 0.0 : r;
+}
+
+MI_DEV double beta_grad_mid(double x, double a, double b) {
+  const double t = a + b;
+  const double mean = a / t;
+  const double sd = sqrt(a * b / (t + 1.0)) / t;
+  if (mean - 0.1 * sd <= x && x <= mean + 0.1 * sd) {
+    const double b2 = b * b;
+    const double poly = 47 * x * b2 * b2 +
+        a * ((43 + 20 * (16 + 27 * b) * x) * b2 * b +
+             a * (3 * (59 + 180 * b - 90 * x) * b2 +
+                  a * ((453 + 1620 * b * (1 - x) - 455 * x) * b + a * (8 * (1 - x) * (135 * b - 11)))));
+    const double pre_num = (1 + 12 * a) * (1 + 12 * b) / (t * t);
+    const double pre_den = 12960 * a * a * a * b * b * (1 + 12 * t);
+    return pre_num / (1 - x) * poly / pre_den;
+  }
+  const double prefactor = -x / sqrt(2 * a * b / t);
+  const double stirling = (1 + 1 / (12 * a) + 1 / (288 * a * a)) *
+                          (1 + 1 / (12 * b) + 1 / (288 * b * b)) /
+                          (1 + 1 / (12 * t) + 1 / (288 * t * t));
+  const double axbx = a * (x - 1) + b * x;
+  const double term1 = (2 * a * a * (x - 1) + a * b * (x - 1) - x * b * b) /
+                       (sqrt(2 * a / b) * pow(t, 1.5) * axbx * axbx);
+  const double term2 = 0.5 * log(a / (t * x));
+  const double term3 = sqrt(8 * a * b / t) / (b * x + a * (x - 1));
+  const double term4 = pow(b * log(b / (t * (1 - x))) + a * log(a / (t * x)), -1.5);
+  return stirling * prefactor * (term1 + term2 * (term3 + (x < mean ? term4 : -term4)));
+}
+
+// Fitted coefficients of the rational correction (numerator [0] and denominator [1] as
+// polynomials in u = log x, a = log(alpha) - u, b = log(total) - a); values as published in
+// torch's Distributions.h.
+__constant__ double kBetaGradCoef[2][3][3][4] = {
+    {{{1.003668233, -0.01061107488, -0.0657888334, 0.01201642863},
+      {0.6336835991, -0.3557432599, 0.05486251648, -0.001465281033},
+      {-0.03276231906, 0.004474107445, 0.002429354597, -0.0001557569013}},
+     {{0.221950385, -0.3187676331, 0.01799915743, 0.01074823814},
+      {-0.2951249643, 0.06219954479, 0.01535556598, 0.001550077057},
+      {0.02155310298, 0.004170831599, 0.001292462449, 6.976601077e-05}},
+     {{-0.05980841433, 0.008441916499, 0.01085618172, 0.002319392565},
+      {0.02911413504, 0.01400243777, -0.002721828457, 0.000751041181},
+      {0.005900514878, -0.001936558688, -9.495446725e-06, 5.385558597e-05}}},
+    {{{1, -0.02924021934, -0.04438342661, 0.007285809825},
+      {0.6357567472, -0.3473456711, 0.05454656494, -0.002407477521},
+      {-0.03301322327, 0.004845219414, 0.00231480583, -0.0002307248149}},
+     {{0.5925320577, -0.1757678135, 0.01505928619, 0.000564515273},
+      {0.1014815858, -0.06589186703, 0.01272886114, -0.0007316646956},
+      {-0.007258481865, 0.001096195486, 0.0003934994223, -4.12701925e-05}},
+     {{0.06469649321, -0.0236701437, 0.002902096474, -5.896963079e-05},
+      {0.001925008108, -0.002869809258, 0.0008000589141, -6.063713228e-05},
+      {-0.0003477407336, 6.959756487e-05, 1.097287507e-05, -1.650964693e-06}}}};
+
+MI_DEV double dirichlet_grad(double x, double alpha, double total) {
+  const double beta = total - alpha;
+  const double boundary = total * x * (1.0 - x);
+  if (x <= 0.5 && boundary < 2.5) return beta_grad_small_alpha(x, alpha, beta);
+  if (x >= 0.5 && boundary < 0.75) return -beta_grad_small_beta(1.0 - x, beta, alpha);
+  if (alpha > 6.0 && beta > 6.0) return beta_grad_mid(x, alpha, beta);
+  const double u = log(x);
+  const double a = log(alpha) - u;
+  const double b = log(total) - a;
+  const double pu[3] = {1.0, u, u * u};
+  const double pa[3] = {1.0, a, a * a};
+  double num = 0.0, den = 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double w = pu[r] * pa[c];
+      const double* n = kBetaGradCoef[0][r][c];
+      const double* d = kBetaGradCoef[1][r][c];
+      num += w * (n[0] + b * (n[1] + b * (n[2] + b * n[3])));
+      den += w * (d[0] + b * (d[1] + b * (d[2] + b * d[3])));
+    }
+  }
+  const double analytic = x * (digamma(total) - digamma(alpha)) / beta;
+  return num / den * analytic;
+}
+
+__global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
+    const float* __restrict__ dx, int64_t dx_sk, int64_t dx_si, const float* __restrict__ x,
+    const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
+    int64_t K, int64_t N, float* __restrict__ out1, float* __restrict__ out0, int64_t out_stride,
+    int64_t rows_per_block) {
+  const int64_t i = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (i >= N) return;
+  const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t k1 = min(K, k0 + rows_per_block);
+  const float a = c1[i * c1_s], b = c0[i * c0_s];
+  const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
+  double s1 = 0.0, s0 = 0.0;
+  for (int64_t k = k0; k < k1; ++k) {
+    const float g = dx[k * dx_sk + i * dx_si];
+    if (g == 0.0f) continue;
+    const float xv = x[k * N + i];
+    const float xw = 1.0f - xv;
+    // _Dirichlet_backward: grad_j * (go_j - sum(x * go)) with go = (g, 0)
+    s1 += dirichlet_grad(xv, a, tot) * (double)g * (double)(1.0f - xv);
+    s0 -= dirichlet_grad(xw, b, tot) * (double)g * (double)xv;
+  }
+  out1[blockIdx.y * out_stride + i] = (float)s1;
+  out0[blockIdx.y * out_stride + i] = (float)s0;
+}
+
+// Raw generator access for tests.
+__global__ void k_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                                uint32_t stream_id, int64_t poff, float* __restrict__ out) {
+  const int64_t quad = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = blockIdx.y;
+  if (quad * 4 >= N) return;
+  float e[4];
+  guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (quad * 4 + j < N) out[k * N + quad * 4 + j] = e[j];
+}
+
+__global__ void k_philox_raw(const uint32_t* __restrict__ ctr, int64_t count, uint32_t k0,
+                             uint32_t k1, uint32_t* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  const U4 r = philox4x32_10(U4{ctr[4 * j], ctr[4 * j + 1], ctr[4 * j + 2], ctr[4 * j + 3]}, k0, k1);
+  out[4 * j] = r.x;
+  out[4 * j + 1] = r.y;
+  out[4 * j + 2] = r.z;
+  out[4 * j + 3] = r.w;
+}
+
+}  // namespace mi
+
+namespace {
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+// Particle slices for the particle-reducing backward kernels: enough blocks to fill the chip,
+// at least 16 particles per slice.
+int64_t bwd_slices(int64_t K, int64_t N, int64_t elems_per_block) {
+  const int64_t gx = ceil_div(N, elems_per_block);
+  int64_t slices = ceil_div(2048, gx);
+  slices = std::min<int64_t>(slices, ceil_div(K, 16));
+  return std::max<int64_t>(1, slices);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
+                      int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                      int64_t particle_offset, const float* eps, float* z, void* stream) {
+  if (loc == nullptr || scale == nullptr || z == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
+    return MI_EINVAL;
+  const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
+  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(K, ceil_div(2048, gx)));
+  const int64_t rows = ceil_div(K, gy);
+  hipLaunchKernelGGL(mi::k_normal_rsample, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
+                     scale, scale_stride, K, N, seed, step, stream_id, particle_offset, eps, z, rows);
+  return to_code(hipGetLastError());
+}
+
+int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
+  if (K < 1 || N < 1 || bytes == nullptr) return MI_EINVAL;
+  const int64_t slices = bwd_slices(K, N, 4 * mi::kGuideThreads);
+  *bytes = slices > 1 ? (size_t)slices * 2 * (size_t)N * sizeof(float) : 0;
+  return 0;
+}
+
+int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
+                               int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                               uint32_t stream_id, int64_t particle_offset, const float* eps,
+                               void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
+                               void* stream) {
+  if (dz == nullptr || dloc == nullptr || dscale == nullptr || K < 1 || N < 1) return MI_EINVAL;
+  size_t need = 0;
+  mi_normal_rsample_backward_workspace_bytes(K, N, &need);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t slices = bwd_slices(K, N, 4 * mi::kGuideThreads);
+  const int64_t rows = ceil_div(K, slices);
+  const int64_t gy = ceil_div(K, rows);
+  const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
+  float* out_loc = dloc;
+  float* out_scale = dscale;
+  if (gy > 1) {
+    out_loc = static_cast<float*>(workspace);
+    out_scale = out_loc + gy * N;
+  }
+  hipLaunchKernelGGL(mi::k_normal_rsample_bwd, dim3((unsigned)gx, (unsigned)gy),
+                     dim3(mi::kGuideThreads), 0, s, dz, dz_stride_k, dz_stride_i, K, N, seed, step,
+                     stream_id, particle_offset, eps, out_loc, out_scale, N, rows);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || gy == 1) return to_code(e);
+  const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, out_loc, gy, N, dloc);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, out_scale, gy, N, dscale);
+  return to_code(hipGetLastError());
+}
+
+int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t c0_stride,
+                    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                    int64_t particle_offset, const float* x_in, float* x, void* stream) {
+  if (c1 == nullptr || c0 == nullptr || x == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
+    return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_beta_rsample, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), c1, c1_stride,
+                     c0, c0_stride, K, N, seed, step, stream_id, particle_offset, x_in, x);
+  return to_code(hipGetLastError());
+}
+
+int mi_beta_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
+  if (K < 1 || N < 1 || bytes == nullptr) return MI_EINVAL;
+  const int64_t slices = bwd_slices(K, N, mi::kGuideThreads);
+  *bytes = slices > 1 ? (size_t)slices * 2 * (size_t)N * sizeof(float) : 0;
+  return 0;
+}
+
+int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
+                             const float* x, const float* c1, int64_t c1_stride, const float* c0,
+                             int64_t c0_stride, int64_t K, int64_t N, void* workspace,
+                             size_t workspace_bytes, float* dc1, float* dc0, void* stream) {
+  if (dx == nullptr || x == nullptr || c1 == nullptr || c0 == nullptr || dc1 == nullptr ||
+      dc0 == nullptr || K < 1 || N < 1)
+    return MI_EINVAL;
+  size_t need = 0;
+  mi_beta_rsample_backward_workspace_bytes(K, N, &need);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t slices = bwd_slices(K, N, mi::kGuideThreads);
+  const int64_t rows = ceil_div(K, slices);
+  const int64_t gy = ceil_div(K, rows);
+  float* o1 = dc1;
+  float* o0 = dc0;
+  if (gy > 1) {
+    o1 = static_cast<float*>(workspace);
+    o0 = o1 + gy * N;
+  }
+  hipLaunchKernelGGL(mi::k_beta_rsample_bwd,
+                     dim3((unsigned)ceil_div(N, mi::kGuideThreads), (unsigned)gy),
+                     dim3(mi::kGuideThreads), 0, s, dx, dx_stride_k, dx_stride_i, x, c1, c1_stride,
+                     c0, c0_stride, K, N, o1, o0, N, rows);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || gy == 1) return to_code(e);
+  const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o1, gy, N, dc1);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o0, gy, N, dc0);
+  return to_code(hipGetLastError());
+}
+
+int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                     int64_t particle_offset, float* out, void* stream) {
+  if (out == nullptr || K < 1 || N < 1 || K > 65535) return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_philox_normal, dim3((unsigned)ceil_div(N, 4 * 256), (unsigned)K),
+                     dim3(256), 0, static_cast<hipStream_t>(stream), K, N, seed, step, stream_id,
+                     particle_offset, out);
+  return to_code(hipGetLastError());
+}
+
+int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t key1, uint32_t* out,
+                  void* stream) {
+  if (ctr == nullptr || out == nullptr || count < 1) return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_philox_raw, dim3((unsigned)ceil_div(count, 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), ctr, count, key0, key1, out);
+  return to_code(hipGetLastError());
+}
+
+}  // extern "C"

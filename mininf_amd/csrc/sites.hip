@@ -1,0 +1,832 @@
+// Site log-probability accumulation over the particle x element space of a model trace.
+//
+// Replaces, for the Normal / Bernoulli / Beta / Categorical families, the per-site
+// `distribution.log_prob(value)` of the reference tracer (mininf/core.py:241, masked branch
+// core.py:231-239), the per-site sums and minibatch scaling of LogProbTracer.total/contribution
+// (core.py:247-273) and the autograd backward of those torch ops. Formulas restate
+// torch/distributions (file:line cited at each family below).
+//
+// Three launch shapes, chosen on the host from the operand strides (mi_group_forward):
+//   ROW   -- a dense operand is contiguous along elements (x[k, i], stride_i == 1): lanes run along
+//            i, each wave owns a 64*ELEMS element segment and walks particle rows; coalesced
+//            256-B loads/stores per wave instruction; per-row wave-shuffle reduction.
+//   COL   -- a dense operand is contiguous along particles (x[i, k] as produced by a vmapped
+//            `X @ theta`, stride_k == 1) or there is no dense operand: lanes run along k and loop
+//            over elements; per-lane accumulation, no cross-lane reduction per element.
+//   BCAST -- one site whose parameters are per-particle scalars and whose value is shared data
+//            x[i] (the biased-coin / C2 shape): the value chunk is staged once in LDS and read as
+//            a broadcast float4 while each lane owns P particles; the per-particle constant part of
+//            log p is hoisted out of the element loop, leaving one FMA per (particle, element).
+// All three write per-(segment, particle) partial sums (fp32) that k_finalize reduces in fp64 in a
+// fixed order, so results are deterministic run to run.
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace mi {
+
+// -------------------------------------------------------------------------------------------------
+// Per-element family math.  d[r] = d log p / d role_r.
+// -------------------------------------------------------------------------------------------------
+struct Elem {
+  float lp;
+  float d[3];
+  uint32_t param_bad;
+  uint32_t support_bad;
+};
+
+// Normal(loc, scale): -(v-loc)^2 / (2 scale^2) - log(scale) - log(sqrt(2 pi))
+// torch/distributions/normal.py:88-103; support real (constraints.py: `value == value`).
+MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
+  const float inv = 1.0f / scale;
+  const float z = (v - loc) * inv;
+  e.lp = -0.5f * z * z - logf(scale) - kHalfLog2Pi;
+  e.d[0] = z * inv;
+  e.d[1] = (z * z - 1.0f) * inv;
+  e.d[2] = -z * inv;
+  e.param_bad = !(scale > 0.0f) || (loc != loc);
+  e.support_bad = (v != v);
+}
+
+// Bernoulli(logits): -BCE_with_logits(l, v) = -(max(l, 0) - l v + log1p(exp(-|l|)))
+// torch/distributions/bernoulli.py:121-125; support boolean {0, 1} (constraints.py:317-325).
+MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
+  const float t = expf(-fabsf(l));
+  e.lp = -(fmaxf(l, 0.0f) - l * v + log1pf(t));
+  const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
+  e.d[0] = v - sig;
+  e.d[1] = 0.0f;
+  e.d[2] = l;
+  e.param_bad = (l != l);
+  e.support_bad = !(v == 0.0f || v == 1.0f);
+}
+
+// Bernoulli(probs): logits = log(p_c) - log1p(-p_c), p_c = clamp(p, eps, 1 - eps)
+// (bernoulli.py:104-106 -> utils.py probs_to_logits / clamp_probs); clamp passes the gradient
+// only inside [eps, 1 - eps].
+MI_DEV void bernoulli_probs_to_logits(float p, float& l, float& dl_dp) {
+  const float hi = 1.0f - kFloatEps;
+  const float pc = fminf(fmaxf(p, kFloatEps), hi);
+  l = logf(pc) - log1pf(-pc);
+  dl_dp = (p >= kFloatEps && p <= hi) ? (1.0f / pc + 1.0f / (1.0f - pc)) : 0.0f;
+}
+
+MI_DEV void eval_bernoulli_probs(float p, float v, Elem& e) {
+  float l, dl_dp;
+  bernoulli_probs_to_logits(p, l, dl_dp);
+  eval_bernoulli_logits(l, v, e);
+  e.d[0] *= dl_dp;
+  e.param_bad = !(p >= 0.0f && p <= 1.0f);
+}
+
+MI_DEV float xlogy(float x, float y) { return (y != y) ? y : (x == 0.0f ? 0.0f : x * logf(y)); }
+
+// Beta(c1, c0) = Dirichlet([c1, c0]) at [v, 1 - v]:
+//   xlogy(c1 - 1, v) + xlogy(c0 - 1, 1 - v) + lgamma(c1 + c0) - lgamma(c1) - lgamma(c0)
+// torch/distributions/beta.py:88-92 -> dirichlet.py:90-97; support [0, 1] (unit_interval).
+MI_DEV void eval_beta(float a, float b, float v, Elem& e) {
+  const float w = 1.0f - v;
+  e.lp = xlogy(a - 1.0f, v) + xlogy(b - 1.0f, w) + lgammaf(a + b) - lgammaf(a) - lgammaf(b);
+  const double psi_ab = digamma((double)a + (double)b);
+  e.d[0] = logf(v) + (float)(psi_ab - digamma((double)a));
+  e.d[1] = logf(w) + (float)(psi_ab - digamma((double)b));
+  e.d[2] = (a - 1.0f) / v - (b - 1.0f) / w;
+  e.param_bad = !(a > 0.0f) || !(b > 0.0f);
+  e.support_bad = !(v >= 0.0f && v <= 1.0f);
+}
+
+MI_DEV void eval_family(int family, float r0, float r1, float r2, Elem& e) {
+  switch (family) {
+    case MI_NORMAL: eval_normal(r0, r1, r2, e); break;
+    case MI_BERNOULLI_LOGITS: eval_bernoulli_logits(r0, r2, e); break;
+    case MI_BERNOULLI_PROBS: eval_bernoulli_probs(r0, r2, e); break;
+    default: eval_beta(r0, r1, r2, e); break;
+  }
+}
+
+// Uniform (scalar-branch) selection from compile-time-indexed register arrays; `idx` is always
+// wave-uniform (it comes from the kernel argument block), so no VALU select chains are emitted.
+template <int N>
+MI_DEV float pick(const float (&v)[N], int idx) {
+  float out = 0.0f;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (idx == j) out = v[j];
+  return out;
+}
+
+template <int N>
+MI_DEV void add_at(float (&v)[N], int idx, float x) {
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (idx == j) v[j] += x;
+}
+
+// One (particle k, element i) of a site group: loads every operand once, evaluates every site,
+// accumulates per-site log p and per-slot particle gradients, writes dense operand gradients.
+MI_DEV void group_element(const mi_group& G, int64_t k, int64_t i, float (&lp)[MI_MAX_SITES],
+                          float (&slot)[MI_MAX_SLOTS], uint32_t (&fl)[MI_MAX_SITES]) {
+  float ov[MI_MAX_OPERANDS];
+  float og[MI_MAX_OPERANDS];
+#pragma unroll
+  for (int o = 0; o < MI_MAX_OPERANDS; ++o) {
+    og[o] = 0.0f;
+    ov[o] = 0.0f;
+    if (o < G.num_operands) {
+      const mi_operand& op = G.operands[o];
+      ov[o] = op.data[k * op.stride_k + i * op.stride_i];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < MI_MAX_SITES; ++s) {
+    if (s < G.num_sites) {
+      const mi_site& st = G.sites[s];
+      float r[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) r[q] = st.operand[q] < 0 ? st.constant[q] : pick(ov, st.operand[q]);
+      bool observed = true;
+      if (st.mask != nullptr) observed = st.mask[k * st.mask_stride_k + i * st.mask_stride_i] != 0;
+      Elem e;
+      eval_family(st.family, r[0], r[1], r[2], e);
+      lp[s] += observed ? e.lp : 0.0f;
+      fl[s] |= (e.param_bad ? MI_FLAG_PARAM : 0u) | ((observed && e.support_bad) ? MI_FLAG_SUPPORT : 0u);
+      if (G.compute_grads) {
+        const float w = observed ? (float)st.scale : 0.0f;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int o = st.operand[q];
+          if (o >= 0) {
+            const int mode = G.operands[o].grad_mode;
+            if (mode == MI_GRAD_DENSE) add_at(og, o, w * e.d[q]);
+            else if (mode == MI_GRAD_PARTICLE) add_at(slot, G.operands[o].slot, w * e.d[q]);
+          }
+        }
+      }
+    }
+  }
+  if (G.compute_grads) {
+#pragma unroll
+    for (int o = 0; o < MI_MAX_OPERANDS; ++o) {
+      if (o < G.num_operands) {
+        const mi_operand& op = G.operands[o];
+        if (op.grad_mode == MI_GRAD_DENSE)
+          op.grad[k * op.grad_stride_k + i * op.grad_stride_i] = G.grad_scale * og[o];
+      }
+    }
+  }
+}
+
+// Partial sums layout: part[(v * nseg + seg) * K + k] for value v in
+// [0, num_sites) (per-site log p) followed by [num_sites, num_sites + num_slots) (slot grads).
+
+// -------------------------------------------------------------------------------------------------
+// ROW: lanes along elements.
+// -------------------------------------------------------------------------------------------------
+template <int ELEMS>
+__global__ __launch_bounds__(256) void k_group_row(const mi_group G, float* __restrict__ part,
+                                                   int64_t nseg, int64_t rows_per_block,
+                                                   uint32_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint32_t fl[MI_MAX_SITES] = {0u, 0u, 0u, 0u};
+  if (seg < nseg) {
+    const int64_t base = seg * (64 * ELEMS);
+    const int64_t k_begin = (int64_t)blockIdx.y * rows_per_block;
+    const int64_t k_end = min(G.K, k_begin + rows_per_block);
+    const int nv = G.num_sites + G.num_slots;
+    for (int64_t kb = k_begin; kb < k_end; kb += 64) {
+      float keep[MI_MAX_SITES + MI_MAX_SLOTS];
+#pragma unroll
+      for (int v = 0; v < MI_MAX_SITES + MI_MAX_SLOTS; ++v) keep[v] = 0.0f;
+      const int rows = (int)min((int64_t)64, k_end - kb);
+      for (int r = 0; r < rows; ++r) {
+        const int64_t k = kb + r;
+        float lp[MI_MAX_SITES] = {0.f, 0.f, 0.f, 0.f};
+        float slot[MI_MAX_SLOTS] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < ELEMS; ++e) {
+          const int64_t i = base + e * 64 + lane;
+          if (i < G.N) group_element(G, k, i, lp, slot, fl);
+        }
+#pragma unroll
+        for (int s = 0; s < MI_MAX_SITES; ++s) {
+          if (s < G.num_sites) {
+            const float t = wave_sum(lp[s]);
+            keep[s] = (lane == r) ? t : keep[s];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < MI_MAX_SLOTS; ++j) {
+          if (j < G.num_slots) {
+            const float t = wave_sum(slot[j]);
+            keep[MI_MAX_SITES + j] = (lane == r) ? t : keep[MI_MAX_SITES + j];
+          }
+        }
+      }
+      if (lane < rows) {
+#pragma unroll
+        for (int s = 0; s < MI_MAX_SITES; ++s)
+          if (s < G.num_sites) part[((int64_t)s * nseg + seg) * G.K + kb + lane] = keep[s];
+#pragma unroll
+        for (int j = 0; j < MI_MAX_SLOTS; ++j)
+          if (j < G.num_slots)
+            part[((int64_t)(G.num_sites + j) * nseg + seg) * G.K + kb + lane] = keep[MI_MAX_SITES + j];
+      }
+      (void)nv;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < MI_MAX_SITES; ++s)
+    if (s < G.num_sites) publish_flags(flags + s, fl[s]);
+}
+
+// -------------------------------------------------------------------------------------------------
+// COL: lanes along particles. `kw` lanes (power of two <= 64) cover consecutive particles, the
+// 64 / kw lane groups of a wave take interleaved elements.
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_group_col(const mi_group G, float* __restrict__ part,
+                                                   int64_t nseg, int64_t seg_len, int kw,
+                                                   uint32_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int kq = lane & (kw - 1);
+  const int isub = lane / kw;
+  const int istep = 64 / kw;
+  const int64_t k = (int64_t)blockIdx.y * kw + kq;
+  uint32_t fl[MI_MAX_SITES] = {0u, 0u, 0u, 0u};
+  float lp[MI_MAX_SITES] = {0.f, 0.f, 0.f, 0.f};
+  float slot[MI_MAX_SLOTS] = {0.f, 0.f, 0.f, 0.f};
+  if (seg < nseg && k < G.K) {
+    const int64_t i_begin = seg * seg_len;
+    const int64_t i_end = min(G.N, i_begin + seg_len);
+#pragma unroll 4
+    for (int64_t i = i_begin + isub; i < i_end; i += istep) group_element(G, k, i, lp, slot, fl);
+  }
+  if (kw < 64) {
+#pragma unroll
+    for (int s = 0; s < MI_MAX_SITES; ++s)
+      if (s < G.num_sites) lp[s] = wave_sum_strided(lp[s], kw);
+#pragma unroll
+    for (int j = 0; j < MI_MAX_SLOTS; ++j)
+      if (j < G.num_slots) slot[j] = wave_sum_strided(slot[j], kw);
+  }
+  if (seg < nseg && k < G.K && isub == 0) {
+#pragma unroll
+    for (int s = 0; s < MI_MAX_SITES; ++s)
+      if (s < G.num_sites) part[((int64_t)s * nseg + seg) * G.K + k] = lp[s];
+#pragma unroll
+    for (int j = 0; j < MI_MAX_SLOTS; ++j)
+      if (j < G.num_slots) part[((int64_t)(G.num_sites + j) * nseg + seg) * G.K + k] = slot[j];
+  }
+#pragma unroll
+  for (int s = 0; s < MI_MAX_SITES; ++s)
+    if (s < G.num_sites) publish_flags(flags + s, fl[s]);
+}
+
+// -------------------------------------------------------------------------------------------------
+// BCAST: one site, parameters are per-particle scalars (or constants), the value is shared data.
+// -------------------------------------------------------------------------------------------------
+constexpr int kBcastThreads = 256;
+constexpr int kBcastP = 4;          // particles per lane
+constexpr int kBcastChunk = 4096;   // elements staged per block
+
+MI_DEV float role_scalar(const mi_group& G, const mi_site& st, int q, int64_t k) {
+  const int o = st.operand[q];
+  if (o < 0) return st.constant[q];
+  const mi_operand& op = G.operands[o];
+  return op.data[k * op.stride_k];
+}
+
+MI_DEV float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[wave] = v;
+  __syncthreads();
+  float out = 0.0f;
+#pragma unroll
+  for (int w = 0; w < kBcastThreads / 64; ++w) out += scratch[w];
+  return out;
+}
+
+// FAMILY in {MI_BERNOULLI_LOGITS, MI_BERNOULLI_PROBS, MI_NORMAL, MI_BETA}
+template <int FAMILY, bool MASKED>
+__global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
+                                                              float* __restrict__ part,
+                                                              int64_t nchunk,
+                                                              uint32_t* __restrict__ flags) {
+  constexpr int NF = (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) ? 1 : 2;
+  __shared__ float4 feat[NF][kBcastChunk / 4];
+  __shared__ float scratch[kBcastThreads / 64];
+  __shared__ float sums[4];
+
+  const mi_site& st = G.sites[0];
+  const mi_operand& vop = G.operands[st.operand[2]];
+  const int64_t c = blockIdx.x;
+  const int64_t i0 = c * kBcastChunk;
+  const int64_t len = min((int64_t)kBcastChunk, G.N - i0);
+
+  // ---- stage: features of the value chunk, particle-independent sums, support flags ----------
+  float* f0 = reinterpret_cast<float*>(feat[0]);
+  float* f1 = reinterpret_cast<float*>(feat[NF - 1]);
+  float s_m = 0.0f, s_a = 0.0f, s_b = 0.0f, s_zero = 0.0f, s_one = 0.0f;
+  uint32_t fl = 0u;
+  for (int j = threadIdx.x; j < kBcastChunk; j += kBcastThreads) {
+    float v = 0.0f, m = 0.0f;
+    if (j < len) {
+      const int64_t i = i0 + j;
+      v = vop.data[i * vop.stride_i];
+      m = 1.0f;
+      if (MASKED) m = st.mask[i * st.mask_stride_i] != 0 ? 1.0f : 0.0f;
+    }
+    const bool obs = m != 0.0f;
+    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+      fl |= (obs && !(v == 0.0f || v == 1.0f)) ? MI_FLAG_SUPPORT : 0u;
+      const float f = obs ? v : 0.0f;
+      f0[j] = f;
+      s_a += f;
+    } else if (FAMILY == MI_NORMAL) {
+      fl |= (obs && v != v) ? MI_FLAG_SUPPORT : 0u;
+      f0[j] = obs ? v : 0.0f;
+      f1[j] = m;
+    } else {  // MI_BETA: log v and log(1 - v); exact 0 / 1 values are counted separately
+      fl |= (obs && !(v >= 0.0f && v <= 1.0f)) ? MI_FLAG_SUPPORT : 0u;
+      const bool zero = obs && v == 0.0f, one = obs && v == 1.0f;
+      const float la = (obs && !zero) ? logf(v) : 0.0f;
+      const float lb = (obs && !one) ? logf(1.0f - v) : 0.0f;
+      f0[j] = la;
+      f1[j] = lb;
+      s_a += la;
+      s_b += lb;
+      s_zero += zero ? 1.0f : 0.0f;
+      s_one += one ? 1.0f : 0.0f;
+    }
+    s_m += m;
+  }
+  s_m = block_sum(s_m, scratch);
+  s_a = block_sum(s_a, scratch);
+  if (FAMILY == MI_BETA) {
+    s_b = block_sum(s_b, scratch);
+    s_zero = block_sum(s_zero, scratch);
+    s_one = block_sum(s_one, scratch);
+  }
+  (void)sums;
+  __syncthreads();
+
+  // ---- per-particle element loop -------------------------------------------------------------
+  const int64_t kbase = (int64_t)blockIdx.y * (kBcastThreads * kBcastP) + threadIdx.x;
+  float pa[kBcastP], pb[kBcastP];
+  uint32_t pbad = 0u;
+#pragma unroll
+  for (int p = 0; p < kBcastP; ++p) {
+    const int64_t k = min(kbase + p * kBcastThreads, G.K - 1);
+    pa[p] = role_scalar(G, st, 0, k);
+    pb[p] = role_scalar(G, st, 1, k);
+  }
+  // Hoisted per-particle coefficients of the element loop.
+  float ca[kBcastP], cb[kBcastP];
+#pragma unroll
+  for (int p = 0; p < kBcastP; ++p) {
+    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+      float l = pa[p], dl = 1.0f;
+      if (FAMILY == MI_BERNOULLI_PROBS) {
+        pbad |= !(pa[p] >= 0.0f && pa[p] <= 1.0f);
+        bernoulli_probs_to_logits(pa[p], l, dl);
+      } else {
+        pbad |= (l != l);
+      }
+      ca[p] = l;
+      cb[p] = dl;
+    } else if (FAMILY == MI_NORMAL) {
+      pbad |= !(pb[p] > 0.0f) || (pa[p] != pa[p]);
+      ca[p] = pa[p];
+      cb[p] = 0.0f;
+    } else {
+      pbad |= !(pa[p] > 0.0f) || !(pb[p] > 0.0f);
+      ca[p] = pa[p] - 1.0f;
+      cb[p] = pb[p] - 1.0f;
+    }
+  }
+
+  double acc1[kBcastP], acc2[kBcastP];
+#pragma unroll
+  for (int p = 0; p < kBcastP; ++p) acc1[p] = acc2[p] = 0.0;
+  const int nq = (int)((len + 3) / 4);
+  for (int q0 = 0; q0 < nq; q0 += 16) {
+    float in1[kBcastP], in2[kBcastP];
+#pragma unroll
+    for (int p = 0; p < kBcastP; ++p) in1[p] = in2[p] = 0.0f;
+    const int q1 = min(nq, q0 + 16);
+    for (int q = q0; q < q1; ++q) {
+      const float4 x = feat[0][q];
+      if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+        // log p(x | l) = x l - softplus(l): one FMA per (particle, element)
+#pragma unroll
+        for (int p = 0; p < kBcastP; ++p) {
+          in1[p] = fmaf(x.x, ca[p], in1[p]);
+          in1[p] = fmaf(x.y, ca[p], in1[p]);
+          in1[p] = fmaf(x.z, ca[p], in1[p]);
+          in1[p] = fmaf(x.w, ca[p], in1[p]);
+        }
+      } else if (FAMILY == MI_NORMAL) {
+        const float4 m = feat[NF - 1][q];
+#pragma unroll
+        for (int p = 0; p < kBcastP; ++p) {
+          const float d0 = x.x - ca[p], d1 = x.y - ca[p], d2 = x.z - ca[p], d3 = x.w - ca[p];
+          if (MASKED) {
+            const float e0 = m.x * d0, e1 = m.y * d1, e2 = m.z * d2, e3 = m.w * d3;
+            in1[p] += (e0 + e1) + (e2 + e3);
+            in2[p] = fmaf(e0, d0, fmaf(e1, d1, fmaf(e2, d2, fmaf(e3, d3, in2[p]))));
+          } else {
+            in1[p] += (d0 + d1) + (d2 + d3);
+            in2[p] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, in2[p]))));
+          }
+        }
+      } else {
+        const float4 y = feat[NF - 1][q];
+#pragma unroll
+        for (int p = 0; p < kBcastP; ++p) {
+          in1[p] = fmaf(x.x, ca[p], fmaf(x.y, ca[p], fmaf(x.z, ca[p], fmaf(x.w, ca[p], in1[p]))));
+          in1[p] = fmaf(y.x, cb[p], fmaf(y.y, cb[p], fmaf(y.z, cb[p], fmaf(y.w, cb[p], in1[p]))));
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kBcastP; ++p) {
+      acc1[p] += (double)in1[p];
+      acc2[p] += (double)in2[p];
+    }
+  }
+
+  // ---- epilogue: constant parts, gradients, partial writes -------------------------------------
+  const int o_a = st.operand[0], o_b = st.operand[1];
+  const bool grads = G.compute_grads != 0;
+  const int slot_a = (grads && o_a >= 0 && G.operands[o_a].grad_mode == MI_GRAD_PARTICLE) ? G.operands[o_a].slot : -1;
+  const int slot_b = (grads && o_b >= 0 && G.operands[o_b].grad_mode == MI_GRAD_PARTICLE) ? G.operands[o_b].slot : -1;
+  const double M = s_m;
+  const float w = (float)st.scale;
+#pragma unroll
+  for (int p = 0; p < kBcastP; ++p) {
+    const int64_t k = kbase + p * kBcastThreads;
+    double lp = 0.0;
+    float ga = 0.0f, gb = 0.0f;
+    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+      const float l = ca[p];
+      const float t = expf(-fabsf(l));
+      const float softplus = fmaxf(l, 0.0f) + log1pf(t);
+      const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
+      lp = acc1[p] - M * (double)softplus;
+      ga = (float)(((double)s_a - M * (double)sig) * (double)cb[p]);
+    } else if (FAMILY == MI_NORMAL) {
+      const double sigma = pb[p];
+      const double inv2 = 1.0 / (sigma * sigma);
+      lp = -0.5 * acc2[p] * inv2 - M * ((double)logf(pb[p]) + (double)kHalfLog2Pi);
+      ga = (float)(acc1[p] * inv2);
+      gb = (float)(acc2[p] * inv2 / sigma - M / sigma);
+    } else {
+      const double a = pa[p], b = pb[p];
+      const double psi_ab = digamma(a + b);
+      double base = acc1[p] + M * ((double)lgammaf(pa[p] + pb[p]) - (double)lgammaf(pa[p]) - (double)lgammaf(pb[p]));
+      // xlogy semantics for exact 0 / 1 values (dirichlet.py:94)
+      if (s_zero > 0.0f && ca[p] != 0.0f) base += ca[p] > 0.0f ? -__builtin_inf() : __builtin_inf();
+      if (s_one > 0.0f && cb[p] != 0.0f) base += cb[p] > 0.0f ? -__builtin_inf() : __builtin_inf();
+      lp = base;
+      ga = (float)((double)s_a + M * (psi_ab - digamma(a)) - (s_zero > 0.0f ? __builtin_inf() : 0.0));
+      gb = (float)((double)s_b + M * (psi_ab - digamma(b)) - (s_one > 0.0f ? __builtin_inf() : 0.0));
+    }
+    if (k < G.K) {
+      part[((int64_t)0 * nchunk + c) * G.K + k] = (float)lp;
+      if (slot_a >= 0) part[((int64_t)(1 + slot_a) * nchunk + c) * G.K + k] = w * ga;
+      if (slot_b >= 0) part[((int64_t)(1 + slot_b) * nchunk + c) * G.K + k] = w * gb;
+    }
+  }
+  fl |= pbad ? MI_FLAG_PARAM : 0u;
+  publish_flags(flags, fl);
+}
+
+// -------------------------------------------------------------------------------------------------
+// Finalize: fixed-order fp64 reduction of partials over segments.
+// -------------------------------------------------------------------------------------------------
+struct FinalizeArgs {
+  int32_t num_sites;
+  int32_t num_slots;
+  double scale[MI_MAX_SITES];
+};
+
+__global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ part, int64_t nseg,
+                                                  int64_t K, const FinalizeArgs A,
+                                                  float* __restrict__ total,
+                                                  double* __restrict__ site_lp,
+                                                  float* __restrict__ slot_grad) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double t = 0.0;
+  for (int s = 0; s < A.num_sites; ++s) {
+    double acc = 0.0;
+    const float* p = part + (int64_t)s * nseg * K + k;
+    for (int64_t g = 0; g < nseg; ++g) acc += (double)p[g * K];
+    acc *= A.scale[s];
+    if (site_lp != nullptr) site_lp[(int64_t)s * K + k] = acc;
+    t += acc;
+  }
+  total[k] = (float)t;
+  for (int j = 0; j < A.num_slots; ++j) {
+    double acc = 0.0;
+    const float* p = part + (int64_t)(A.num_sites + j) * nseg * K + k;
+    for (int64_t g = 0; g < nseg; ++g) acc += (double)p[g * K];
+    slot_grad[(int64_t)j * K + k] = (float)acc;
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Backward rescale of speculative dense gradients.
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ x, int64_t sk, int64_t si,
+                                                    int64_t K, int64_t N,
+                                                    const float* __restrict__ g, float g0,
+                                                    int64_t rows_per_block) {
+  const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t k1 = min(K, k0 + rows_per_block);
+  bool all_same = true;
+  for (int64_t k = k0; k < k1; ++k) all_same &= (g[k] == g0);
+  if (all_same) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  for (int64_t k = k0; k < k1; ++k) {
+    const float f = g[k] / g0;
+    if (f != 1.0f) x[k * sk + i * si] *= f;
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Categorical (gather of normalised logits), lanes along elements.
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_categorical(
+    const float* __restrict__ logits, int64_t sk, int64_t si, int64_t sc, int64_t K, int64_t N,
+    int64_t C, const int64_t* __restrict__ value, int64_t vsk, int64_t vsi,
+    const uint8_t* __restrict__ mask, int64_t msi, float gscale, float* __restrict__ dlogits,
+    float* __restrict__ part, int64_t nseg, uint32_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t k = blockIdx.y;
+  uint32_t fl = 0u;
+  if (seg < nseg) {
+    float acc = 0.0f;
+    for (int e = 0; e < 16; ++e) {
+      const int64_t i = seg * 1024 + e * 64 + lane;
+      if (i < N) {
+        const bool obs = mask == nullptr || mask[i * msi] != 0;
+        const int64_t v = value[k * vsk + i * vsi];
+        const bool ok = v >= 0 && v < C;
+        fl |= (obs && !ok) ? MI_FLAG_SUPPORT : 0u;
+        if (obs && ok) {
+          const int64_t off = k * sk + i * si + v * sc;
+          acc += logits[off];
+          if (dlogits != nullptr) dlogits[off] = gscale;
+        }
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) part[seg * K + k] = acc;
+  }
+  publish_flags(flags, fl);
+}
+
+__global__ void k_categorical_finalize(const float* __restrict__ part, int64_t nseg, int64_t K,
+                                       double scale, float* __restrict__ total) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double acc = 0.0;
+  for (int64_t g = 0; g < nseg; ++g) acc += (double)part[g * K + k];
+  total[k] = (float)(acc * scale);
+}
+
+}  // namespace mi
+
+// =================================================================================================
+// Host side: launch-shape selection and the C ABI.
+// =================================================================================================
+namespace {
+
+enum Shape { kRow = 0, kCol = 1, kBcast = 2 };
+
+constexpr int kRowElems = 16;
+constexpr int64_t kTargetBlocks = 2048;
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+bool validate_group(const mi_group* g) {
+  if (g == nullptr || g->K < 1 || g->N < 1) return false;
+  if (g->num_sites < 1 || g->num_sites > MI_MAX_SITES) return false;
+  if (g->num_operands < 0 || g->num_operands > MI_MAX_OPERANDS) return false;
+  if (g->num_slots < 0 || g->num_slots > MI_MAX_SLOTS) return false;
+  for (int s = 0; s < g->num_sites; ++s) {
+    const mi_site& st = g->sites[s];
+    if (st.family < MI_NORMAL || st.family > MI_BETA) return false;
+    if (st.operand[2] < 0) return false;  // the value is always an operand
+    for (int q = 0; q < 3; ++q)
+      if (st.operand[q] >= g->num_operands) return false;
+  }
+  for (int o = 0; o < g->num_operands; ++o) {
+    const mi_operand& op = g->operands[o];
+    if (op.data == nullptr) return false;
+    if (op.grad_mode == MI_GRAD_DENSE && op.grad == nullptr) return false;
+    if (op.grad_mode == MI_GRAD_PARTICLE && (op.slot < 0 || op.slot >= g->num_slots)) return false;
+  }
+  return true;
+}
+
+bool is_dense(const mi_operand& op) { return op.stride_k != 0 && op.stride_i != 0; }
+
+bool bcast_eligible(const mi_group* g) {
+  if (g->num_sites != 1 || g->N < 1024 || g->K < 64) return false;
+  const mi_site& st = g->sites[0];
+  if (st.mask != nullptr && st.mask_stride_k != 0) return false;
+  const mi_operand& v = g->operands[st.operand[2]];
+  if (v.stride_k != 0 || v.stride_i == 0 || v.grad_mode != MI_GRAD_NONE) return false;
+  for (int q = 0; q < 2; ++q) {
+    const int o = st.operand[q];
+    if (o < 0) continue;
+    const mi_operand& op = g->operands[o];
+    if (op.stride_i != 0 || op.grad_mode == MI_GRAD_DENSE) return false;
+  }
+  return true;
+}
+
+struct Plan {
+  Shape shape;
+  int64_t nseg;
+  int64_t rows_per_block;  // ROW
+  int64_t seg_len;         // COL
+  int kw;                  // COL
+  dim3 grid;
+};
+
+Plan make_plan(const mi_group* g) {
+  Plan p{};
+  const int nv = g->num_sites + g->num_slots;
+  (void)nv;
+  if (bcast_eligible(g)) {
+    p.shape = kBcast;
+    p.nseg = ceil_div(g->N, mi::kBcastChunk);
+    p.grid = dim3((unsigned)p.nseg, (unsigned)ceil_div(g->K, mi::kBcastThreads * mi::kBcastP));
+    return p;
+  }
+  int dense = -1;
+  for (int o = 0; o < g->num_operands; ++o)
+    if (is_dense(g->operands[o])) { dense = o; break; }
+  const bool row = dense >= 0 && g->operands[dense].stride_i == 1 && g->operands[dense].stride_k != 1;
+  const bool row_fallback = dense >= 0 && g->operands[dense].stride_k != 1 && g->operands[dense].stride_i != 1 &&
+                            llabs(g->operands[dense].stride_i) < llabs(g->operands[dense].stride_k);
+  if (row || row_fallback) {
+    p.shape = kRow;
+    p.nseg = ceil_div(g->N, 64 * kRowElems);
+    const int64_t gx = ceil_div(p.nseg, 4);
+    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(kTargetBlocks, gx)));
+    p.rows_per_block = ceil_div(g->K, gy);
+    gy = ceil_div(g->K, p.rows_per_block);
+    p.grid = dim3((unsigned)gx, (unsigned)gy);
+    return p;
+  }
+  p.shape = kCol;
+  int kw = 1;
+  while (kw < 64 && kw < g->K) kw <<= 1;
+  p.kw = kw;
+  const int64_t gy = ceil_div(g->K, kw);
+  const int istep = 64 / kw;
+  const int64_t waves_per_tile = std::max<int64_t>(1, (kTargetBlocks * 4) / gy);
+  int64_t seg_len = ceil_div(g->N, waves_per_tile);
+  seg_len = std::max<int64_t>(seg_len, (int64_t)istep * 16);
+  seg_len = ceil_div(seg_len, istep) * istep;
+  p.seg_len = seg_len;
+  p.nseg = ceil_div(g->N, seg_len);
+  p.grid = dim3((unsigned)ceil_div(p.nseg, 4), (unsigned)gy);
+  return p;
+}
+
+size_t partial_bytes(const mi_group* g, const Plan& p) {
+  const int nv = g->num_sites + g->num_slots;
+  return (size_t)nv * (size_t)p.nseg * (size_t)g->K * sizeof(float);
+}
+
+int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+}  // namespace
+
+extern "C" {
+
+int mi_abi_version(char* target, size_t target_bytes) {
+  const char name[] = "gfx950";
+  if (target != nullptr && target_bytes > 0) {
+    size_t n = 0;
+    for (; n + 1 < target_bytes && name[n] != '\0'; ++n) target[n] = name[n];
+    target[n] = '\0';
+  }
+  return MI_ABI_VERSION;
+}
+
+int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
+  if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  *bytes = partial_bytes(group, p);
+  return 0;
+}
+
+int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,
+                     double* site_lp, float* slot_grad, uint32_t* flags, void* stream) {
+  if (!validate_group(group) || total == nullptr || flags == nullptr) return MI_EINVAL;
+  if (group->num_slots > 0 && slot_grad == nullptr) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  if (workspace_bytes < partial_bytes(group, p) || workspace == nullptr) return MI_EWORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
+  if (e != hipSuccess) return to_code(e);
+  const mi_group G = *group;
+  switch (p.shape) {
+    case kBcast: {
+      const bool masked = G.sites[0].mask != nullptr;
+      switch (G.sites[0].family) {
+#define MI_LAUNCH_BCAST(FAM)                                                                   \
+  case FAM:                                                                                    \
+    if (masked)                                                                                \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), 0, s, \
+                         G, part, p.nseg, flags);                                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), 0,   \
+                         s, G, part, p.nseg, flags);                                           \
+    break;
+        MI_LAUNCH_BCAST(MI_BERNOULLI_LOGITS)
+        MI_LAUNCH_BCAST(MI_BERNOULLI_PROBS)
+        MI_LAUNCH_BCAST(MI_NORMAL)
+        MI_LAUNCH_BCAST(MI_BETA)
+#undef MI_LAUNCH_BCAST
+        default: return MI_EUNSUPPORTED;
+      }
+      break;
+    }
+    case kRow:
+      hipLaunchKernelGGL((mi::k_group_row<kRowElems>), p.grid, dim3(256), 0, s, G, part, p.nseg,
+                         p.rows_per_block, flags);
+      break;
+    case kCol:
+      hipLaunchKernelGGL(mi::k_group_col, p.grid, dim3(256), 0, s, G, part, p.nseg, p.seg_len,
+                         p.kw, flags);
+      break;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return to_code(e);
+  mi::FinalizeArgs A{};
+  A.num_sites = G.num_sites;
+  A.num_slots = G.num_slots;
+  for (int i = 0; i < G.num_sites; ++i) A.scale[i] = G.sites[i].scale;
+  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, 256)), dim3(256), 0, s, part,
+                     p.nseg, G.K, A, total, site_lp, slot_grad);
+  return to_code(hipGetLastError());
+}
+
+int mi_scale_rows(float* x, int64_t stride_k, int64_t stride_i, int64_t K, int64_t N,
+                  const float* g, float g0, void* stream) {
+  if (x == nullptr || g == nullptr || K < 1 || N < 1 || g0 == 0.0f) return MI_EINVAL;
+  const int64_t rows = 64;
+  dim3 grid((unsigned)ceil_div(N, 256), (unsigned)ceil_div(K, rows));
+  hipLaunchKernelGGL(mi::k_scale_rows, grid, dim3(256), 0, static_cast<hipStream_t>(stream), x,
+                     stride_k, stride_i, K, N, g, g0, rows);
+  return to_code(hipGetLastError());
+}
+
+int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
+  if (K < 1 || N < 1 || bytes == nullptr) return MI_EINVAL;
+  *bytes = (size_t)ceil_div(N, 1024) * (size_t)K * sizeof(float);
+  return 0;
+}
+
+int mi_categorical_forward(const float* logits, int64_t stride_k, int64_t stride_i,
+                           int64_t stride_c, int64_t K, int64_t N, int64_t C,
+                           const int64_t* value, int64_t value_stride_k, int64_t value_stride_i,
+                           const uint8_t* mask, int64_t mask_stride_i, double scale, float g0,
+                           float* dlogits, void* workspace, size_t workspace_bytes, float* total,
+                           uint32_t* flags, void* stream) {
+  if (logits == nullptr || value == nullptr || total == nullptr || flags == nullptr || K < 1 ||
+      N < 1 || C < 1)
+    return MI_EINVAL;
+  size_t need = 0;
+  mi_categorical_workspace_bytes(K, N, &need);
+  if (workspace == nullptr || workspace_bytes < need) return MI_EWORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return to_code(e);
+  const int64_t nseg = ceil_div(N, 1024);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(mi::k_categorical, dim3((unsigned)ceil_div(nseg, 4), (unsigned)K), dim3(256),
+                     0, s, logits, stride_k, stride_i, stride_c, K, N, C, value, value_stride_k,
+                     value_stride_i, mask, mask_stride_i, (float)(g0 * scale), dlogits, part, nseg,
+                     flags);
+  e = hipGetLastError();
+  if (e != hipSuccess) return to_code(e);
+  hipLaunchKernelGGL(mi::k_categorical_finalize, dim3((unsigned)ceil_div(K, 256)), dim3(256), 0, s,
+                     part, nseg, K, scale, total);
+  return to_code(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,366 @@
+"""
+ELBO engine: turns a :class:`~mininf_amd.particles.ParticleTrace` into HIP site-kernel launches and
+wires them into autograd.
+
+Per step (one ``EvidenceLowerBoundLoss.forward``):
+
+1. sites that share their element space and a dense operand are grouped (at most 4 sites, 6
+   operands) so the operand is streamed from HBM once and its gradient written once;
+2. each group runs ``mi_group_forward`` (``include/mininf_amd.h``), which returns the per-particle
+   totals ``T_k`` and -- speculatively, because the ELBO is linear in ``T`` -- the gradients of all
+   operands, pre-multiplied by the upstream gradient the ELBO will send (``g0 = -1/K``);
+3. in backward, ``mi_scale_rows`` leaves those buffers untouched when the upstream really is
+   ``g0`` (every thread block exits after one comparison) and rescales them otherwise.
+
+Gradient modes per operand: DENSE (one value per particle and element: written in the operand's
+own layout), PARTICLE (one scalar per particle: reduced over elements inside the kernel).
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _native as nat
+from .particles import ParticleTrace, SiteRecord
+
+
+FAMILY_CODES = {
+    "normal": nat.NORMAL,
+    "bernoulli_logits": nat.BERNOULLI_LOGITS,
+    "bernoulli_probs": nat.BERNOULLI_PROBS,
+    "beta": nat.BETA,
+}
+
+
+def _collapse(t: torch.Tensor, K: int, shape: torch.Size) -> "_View":
+    """
+    Describe a [K, *R] tensor (R broadcastable to ``shape``) over the logical [K, N] element space
+    (N = numel(shape)). Per-particle scalars stay [K, 1] tensors with element stride 0 (their
+    gradient is reduced in the kernel); broadcast and collapsible dims stay views; anything else is
+    materialised by ``reshape``.
+    """
+    if t.dim() == 0:
+        t = t.expand(K)
+    R = tuple(t.shape[1:])
+    N = int(torch.Size(shape).numel())
+    if int(torch.Size(R).numel()) == 1:
+        base = t.reshape(K, 1)
+        return _View(base, base.stride(0), 0)
+    full = t.reshape((K,) + (1,) * (len(shape) - len(R)) + R).expand((K,) + tuple(shape))
+    flat = full.reshape(K, N)
+    return _View(flat, flat.stride(0), flat.stride(1) if N > 1 else 1)
+
+
+def _float(t: torch.Tensor, what: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise nat.NativeError(f"{what}: the HIP site kernels compute in float32 (the reference's "
+                              f"default dtype); got {t.dtype}.")
+    return t
+
+
+@dataclasses.dataclass
+class _View:
+    tensor: torch.Tensor   # the autograd input ([K, N] view, or [K, 1] for per-particle scalars)
+    sk: int                # element strides over the logical [K, N] space
+    si: int
+
+    @property
+    def key(self) -> Tuple:
+        t = self.tensor
+        return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), self.sk, self.si,
+                t.requires_grad)
+
+    @property
+    def dense(self) -> bool:
+        return self.sk != 0 and self.si != 0
+
+    @property
+    def per_particle(self) -> bool:
+        """One scalar per particle: the gradient is reduced over elements inside the kernel."""
+        return self.tensor.shape[1] == 1 and self.si == 0
+
+
+@dataclasses.dataclass
+class _Operand:
+    view: _View
+    mode: int
+    slot: int = -1
+
+
+class _GroupLauncher:
+    """
+    Owns the ctypes descriptor of one site group and launches ``mi_group_forward``.
+    """
+    def __init__(self, K: int, N: int, g0: float) -> None:
+        self.K, self.N, self.g0 = K, N, g0
+        self.operands: List[_Operand] = []
+        self.keys: Dict[Tuple, int] = {}
+        self.sites: List[Tuple[SiteRecord, List[int], Optional[torch.Tensor]]] = []
+        self.num_slots = 0
+
+    def try_add(self, site: SiteRecord, views: List[_View], mask: Optional[_View]) -> bool:
+        new = {v.key for v in views if v.key not in self.keys}
+        if len(self.sites) >= nat.MAX_SITES or len(self.operands) + len(new) > nat.MAX_OPERANDS:
+            return False
+        grad_on = torch.is_grad_enabled()
+        slots = len({v.key for v in views if v.key not in self.keys and v.per_particle
+                     and v.tensor.requires_grad and grad_on})
+        if self.num_slots + slots > nat.MAX_SLOTS:
+            return False
+        indices = []
+        for v in views:
+            if v.key not in self.keys:
+                mode, slot = nat.GRAD_NONE, -1
+                if v.tensor.requires_grad and grad_on:
+                    if v.per_particle:
+                        mode, slot = nat.GRAD_PARTICLE, self.num_slots
+                        self.num_slots += 1
+                    else:
+                        mode = nat.GRAD_DENSE
+                self.keys[v.key] = len(self.operands)
+                self.operands.append(_Operand(v, mode, slot))
+            indices.append(self.keys[v.key])
+        self.sites.append((site, indices, mask))
+        return True
+
+    def shares_dense_operand(self, views: List[_View]) -> bool:
+        return any(v.key in self.keys and v.dense for v in views)
+
+    def inputs(self) -> List[torch.Tensor]:
+        return [op.view.tensor for op in self.operands]
+
+    def run(self, compute_grads: bool):
+        device = self.operands[0].view.tensor.device
+        K, N = self.K, self.N
+        group = nat.Group()
+        group.K, group.N = K, N
+        group.num_sites = len(self.sites)
+        group.num_operands = len(self.operands)
+        group.num_slots = self.num_slots if compute_grads else 0
+        group.compute_grads = int(compute_grads)
+        group.grad_scale = self.g0
+        grads: List[Optional[torch.Tensor]] = []
+        for index, op in enumerate(self.operands):
+            desc = group.operands[index]
+            view = op.view
+            desc.data = view.tensor.data_ptr()
+            desc.stride_k, desc.stride_i = view.sk, view.si
+            grad = None
+            mode = op.mode if compute_grads else nat.GRAD_NONE
+            if mode == nat.GRAD_DENSE:
+                sk, si = view.sk, view.si
+                if (sk, si) in ((N, 1), (1, K)):
+                    grad = torch.empty_strided((K, N), (sk, si), dtype=torch.float32, device=device)
+                else:
+                    grad = torch.empty((K, N), dtype=torch.float32, device=device)
+                desc.grad = grad.data_ptr()
+                desc.grad_stride_k, desc.grad_stride_i = grad.stride()
+            desc.grad_mode = mode
+            desc.slot = op.slot if mode == nat.GRAD_PARTICLE else 0
+            grads.append(grad)
+        for index, (site, roles, mask) in enumerate(self.sites):
+            desc = group.sites[index]
+            desc.family = FAMILY_CODES[site.family]
+            if site.family.startswith("bernoulli"):
+                roles = [roles[0], -1, roles[1]]
+            for q in range(3):
+                desc.operand[q] = roles[q]
+                desc.constant[q] = 0.0
+            if mask is not None:
+                desc.mask = mask.tensor.data_ptr()
+                desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
+            desc.scale = site.scale
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
+                  "mi_group_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        total = torch.empty(K, dtype=torch.float32, device=device)
+        site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device)
+        slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
+        flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
+        nat.check(lib.mi_group_forward(ctypes.byref(group), workspace.data_ptr(), size.value,
+                                       total.data_ptr(), site_lp.data_ptr(), slot_grad.data_ptr(),
+                                       flags.data_ptr(), nat.stream_handle(device)),
+                  "mi_group_forward")
+        return total, site_lp, grads, slot_grad, flags
+
+
+class _SiteGroupFn(torch.autograd.Function):
+    """
+    Autograd node of one site group: forward returns T_k (fp32 [K]); backward returns the
+    speculative gradients (rescaled only if the upstream differs from g0).
+    """
+    @staticmethod
+    def forward(ctx, launcher: _GroupLauncher, holder: dict, *inputs):  # type: ignore[override]
+        need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
+        total, site_lp, grads, slot_grad, flags = launcher.run(need)
+        holder["flags"] = flags
+        holder["site_lp"] = site_lp
+        ctx.launcher = launcher
+        ctx.grads = grads
+        ctx.slot_grad = slot_grad
+        return total
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):  # type: ignore[override]
+        launcher: _GroupLauncher = ctx.launcher
+        grads, slot_grad = ctx.grads, ctx.slot_grad
+        if grads is None:  # a second backward through the same graph: recompute
+            _, _, grads, slot_grad, _ = launcher.run(True)
+        ctx.grads = None
+        g = g.contiguous()
+        device = g.device
+        out: List[Optional[torch.Tensor]] = []
+        for op, grad in zip(launcher.operands, grads):
+            if op.mode == nat.GRAD_DENSE:
+                sk, si = grad.stride()
+                nat.check(nat.lib().mi_scale_rows(grad.data_ptr(), sk, si, launcher.K, launcher.N,
+                                                  g.data_ptr(), launcher.g0,
+                                                  nat.stream_handle(device)), "mi_scale_rows")
+                out.append(grad)
+            elif op.mode == nat.GRAD_PARTICLE:
+                out.append((slot_grad[op.slot] * g).reshape(launcher.K, 1))
+            else:
+                out.append(None)
+        return (None, None, *out)
+
+
+class _CategoricalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, site: SiteRecord, holder: dict, g0: float, logits: torch.Tensor,
+                value: torch.Tensor, mask: Optional[torch.Tensor]):  # type: ignore[override]
+        K, N, C = logits.shape
+        device = logits.device
+        need = logits.requires_grad
+        dlogits = torch.zeros_like(logits) if need else None
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_categorical_workspace_bytes(K, N, ctypes.byref(size)),
+                  "mi_categorical_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        total = torch.empty(K, dtype=torch.float32, device=device)
+        flags = torch.empty(1, dtype=torch.int32, device=device)
+        nat.check(lib.mi_categorical_forward(
+            logits.data_ptr(), logits.stride(0), logits.stride(1), logits.stride(2), K, N, C,
+            value.data_ptr(), value.stride(0), value.stride(1),
+            None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(1),
+            site.scale, g0, None if dlogits is None else dlogits.data_ptr(), workspace.data_ptr(),
+            size.value, total.data_ptr(), flags.data_ptr(), nat.stream_handle(device)),
+            "mi_categorical_forward")
+        holder["flags"] = flags
+        ctx.dlogits = dlogits
+        ctx.g0 = g0
+        return total
+
+    @staticmethod
+    def backward(ctx, g):  # type: ignore[override]
+        dlogits = ctx.dlogits
+        if dlogits is None:
+            return None, None, None, None, None, None
+        K, N, C = dlogits.shape
+        g = g.contiguous()
+        nat.check(nat.lib().mi_scale_rows(dlogits.data_ptr(), N * C, 1, K, N * C, g.data_ptr(),
+                                          ctx.g0, nat.stream_handle(g.device)), "mi_scale_rows")
+        return None, None, None, dlogits, None, None
+
+
+@dataclasses.dataclass
+class LogJoint:
+    """
+    Per-particle log joint of a trace plus the device-side validation results.
+    """
+    total: torch.Tensor                       # [K] fp32, differentiable
+    pending: List[Tuple[str, dict, List[SiteRecord]]]
+    checks: list
+
+    def raise_on_violation(self) -> None:
+        """
+        One host synchronisation for all validation flags of the step; raises the reference's
+        errors (core.py:186-188 for values, torch validate_args for parameters).
+        """
+        parts = []
+        for _, holder, _ in self.pending:
+            parts.append(holder["flags"].reshape(-1).to(torch.int64))
+        for _, ok in self.checks:
+            parts.append((~ok.reshape(-1).bool()).any().reshape(1).to(torch.int64))
+        if not parts:
+            return
+        flat = torch.cat(parts).cpu().tolist()
+        cursor = 0
+        for kind, holder, sites in self.pending:
+            for site in sites:
+                bits = flat[cursor]
+                cursor += 1
+                if bits & nat.FLAG_PARAM:
+                    raise ValueError(f"Expected parameters of distribution {site.description} for "
+                                     f"site '{site.name}' to satisfy their constraints, but found "
+                                     "invalid values.")
+                if bits & nat.FLAG_SUPPORT:
+                    raise ValueError(f"Parameter '{site.name}' is not in the support of "
+                                     f"{site.description}.")
+        for check, _ in self.checks:
+            if flat[cursor]:
+                raise ValueError(check.message)
+            cursor += 1
+
+
+def log_joint(trace: ParticleTrace, g0: float) -> LogJoint:
+    """
+    Launch the site kernels for every recorded site and return the per-particle log joint.
+    """
+    K = trace.K
+    groups: List[Tuple[torch.Size, _GroupLauncher]] = []
+    totals: List[torch.Tensor] = []
+    pending: List[Tuple[str, dict, List[SiteRecord]]] = []
+    for site in trace.sites:
+        for t in site.tensors:
+            nat.require_device(t, f"site '{site.name}'")
+        if site.family == "categorical":
+            logits, value = site.tensors
+            shape = site.site_shape
+            C = logits.shape[-1]
+            N = int(shape.numel())
+            lg = _float(logits, site.name)
+            lg = lg.reshape((K,) + (1,) * (len(shape) + 1 - (lg.dim() - 1)) + tuple(lg.shape[1:]))
+            lg = lg.expand((K,) + tuple(shape) + (C,)).reshape(K, N, C).contiguous()
+            val = _collapse(value.to(torch.int64), K, shape).tensor.expand(K, N)
+            mask = None if site.mask is None else \
+                site.mask.expand(shape).reshape(1, N).expand(K, N).to(torch.uint8)
+            holder: dict = {}
+            totals.append(_CategoricalFn.apply(site, holder, g0, lg, val, mask))
+            pending.append(("categorical", holder, [site]))
+            continue
+        shape = site.site_shape
+        N = int(shape.numel())
+        tensors = [_collapse(_float(t, site.name), K, shape) for t in site.tensors]
+        mask = None
+        if site.mask is not None:
+            flat_mask = site.mask.bool().expand(shape).reshape(N)
+            mask = _View(flat_mask, 0, flat_mask.stride(0) if N > 1 else 1)
+        placed = False
+        for group_shape, launcher in groups:
+            if group_shape == shape and launcher.shares_dense_operand(tensors) and \
+                    launcher.try_add(site, tensors, mask):
+                placed = True
+                break
+        if not placed:
+            launcher = _GroupLauncher(K, N, g0)
+            launcher.try_add(site, tensors, mask)
+            groups.append((shape, launcher))
+    for _, launcher in groups:
+        holder = {}
+        totals.append(_SiteGroupFn.apply(launcher, holder, *launcher.inputs()))
+        pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
+    for _, value in trace.fallback:
+        totals.append(value.to(torch.float32))
+    if totals:
+        total = totals[0]
+        for extra in totals[1:]:
+            total = total + extra
+    else:
+        total = torch.zeros(K)
+    return LogJoint(total=total, pending=pending, checks=trace.checks)

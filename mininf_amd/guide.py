@@ -1,0 +1,179 @@
+"""
+Reparameterised guide sampling over K particles (replaces ``FactorizedDistribution.rsample``,
+reference ``mininf/nn.py:133-145``, with ONE draw per call at ``nn.py:217``).
+
+Normal and Beta factors are drawn by HIP kernels from a counter-based Philox generator keyed by
+(seed, step, factor index, global particle index, element), so that K particles split over W GPUs
+draw exactly the union of what one GPU would draw. Other families (Gamma, MultivariateNormal, ...)
+use their own ``torch.distributions`` ``rsample`` on the device (outside the north-star families).
+
+Parity mode: ``noise[name]`` injects host-drawn standard normals (Normal factors, [K, *shape]) or
+the draws themselves (Beta factors), exactly as the oracle's sample-injection protocol does
+(SURVEY.md 8(c)).
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Dict, Optional, Tuple
+
+import torch
+from torch.distributions import Beta, Distribution, Normal
+
+from . import _native as nat
+
+
+@dataclasses.dataclass
+class DrawConfig:
+    K: int
+    seed: int
+    step: int
+    stream_id: int
+    particle_offset: int
+    noise: Optional[torch.Tensor] = None
+
+
+def _flat_param(t: torch.Tensor, N: int) -> Tuple[torch.Tensor, int]:
+    """
+    View a parameter of the factor's batch shape as [N] with a single stride (0 for broadcast
+    scalars, 1 for contiguous), materialising it otherwise.
+    """
+    if t.dtype != torch.float32:
+        raise nat.NativeError(f"guide parameters must be float32, got {t.dtype}")
+    if t.numel() == 1:
+        flat = t.reshape(1).expand(N)
+        return flat, 0
+    flat = t.reshape(N)
+    if flat.stride(0) not in (0, 1):
+        flat = flat.contiguous()
+    return flat, flat.stride(0)
+
+
+def _philox_key(cfg: DrawConfig) -> Tuple[int, int]:
+    return cfg.seed & 0xFFFFFFFFFFFFFFFF, cfg.step & 0xFFFFFFFFFFFFFFFF
+
+
+class _NormalRsampleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: DrawConfig, loc: torch.Tensor, loc_s: int, scale: torch.Tensor,
+                scale_s: int):  # type: ignore[override]
+        N = loc.shape[0]
+        K = cfg.K
+        z = torch.empty((K, N), dtype=torch.float32, device=loc.device)
+        seed, step = _philox_key(cfg)
+        eps = cfg.noise
+        nat.check(nat.lib().mi_normal_rsample(
+            loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step, cfg.stream_id,
+            cfg.particle_offset, nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)),
+            "mi_normal_rsample")
+        ctx.cfg = cfg
+        ctx.N = N
+        ctx.save_for_backward(scale)
+        ctx.scale_s = scale_s
+        return z
+
+    @staticmethod
+    def backward(ctx, dz: torch.Tensor):  # type: ignore[override]
+        cfg: DrawConfig = ctx.cfg
+        (scale,) = ctx.saved_tensors
+        N, K = ctx.N, cfg.K
+        device = dz.device
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_normal_rsample_backward_workspace_bytes(K, N, ctypes.byref(size)),
+                  "mi_normal_rsample_backward_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        dloc = torch.empty(N, dtype=torch.float32, device=device)
+        deps_scale = torch.empty(N, dtype=torch.float32, device=device)
+        seed, step = _philox_key(cfg)
+        nat.check(lib.mi_normal_rsample_backward(
+            dz.data_ptr(), dz.stride(0), dz.stride(1), K, N, seed, step, cfg.stream_id,
+            cfg.particle_offset, nat.ptr(cfg.noise), workspace.data_ptr(), size.value,
+            dloc.data_ptr(), deps_scale.data_ptr(), nat.stream_handle(device)),
+            "mi_normal_rsample_backward")
+        # dz/dscale = eps: the kernel returns sum_k dz * eps directly.
+        return None, dloc, None, deps_scale, None
+
+
+class _BetaRsampleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: DrawConfig, c1: torch.Tensor, c1_s: int, c0: torch.Tensor,
+                c0_s: int):  # type: ignore[override]
+        N = c1.shape[0]
+        K = cfg.K
+        x = torch.empty((K, N), dtype=torch.float32, device=c1.device)
+        seed, step = _philox_key(cfg)
+        nat.check(nat.lib().mi_beta_rsample(
+            c1.data_ptr(), c1_s, c0.data_ptr(), c0_s, K, N, seed, step, cfg.stream_id,
+            cfg.particle_offset, nat.ptr(cfg.noise), x.data_ptr(), nat.stream_handle(c1.device)),
+            "mi_beta_rsample")
+        ctx.save_for_backward(x, c1, c0)
+        ctx.strides = (c1_s, c0_s)
+        ctx.K, ctx.N = K, N
+        return x
+
+    @staticmethod
+    def backward(ctx, dx: torch.Tensor):  # type: ignore[override]
+        x, c1, c0 = ctx.saved_tensors
+        c1_s, c0_s = ctx.strides
+        K, N = ctx.K, ctx.N
+        device = dx.device
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_beta_rsample_backward_workspace_bytes(K, N, ctypes.byref(size)),
+                  "mi_beta_rsample_backward_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        dc1 = torch.empty(N, dtype=torch.float32, device=device)
+        dc0 = torch.empty(N, dtype=torch.float32, device=device)
+        nat.check(lib.mi_beta_rsample_backward(
+            dx.data_ptr(), dx.stride(0), dx.stride(1), x.data_ptr(), c1.data_ptr(), c1_s,
+            c0.data_ptr(), c0_s, K, N, workspace.data_ptr(), size.value, dc1.data_ptr(),
+            dc0.data_ptr(), nat.stream_handle(device)), "mi_beta_rsample_backward")
+        return None, dc1, None, dc0, None
+
+
+def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
+    """
+    K reparameterised draws of one guide factor: shape [K, *batch_shape, *event_shape].
+    """
+    cls = type(distribution)
+    if cls is Normal:
+        shape = distribution.batch_shape
+        N = max(1, int(shape.numel()))
+        nat.require_device(distribution.loc, "guide Normal.loc")
+        loc, loc_s = _flat_param(distribution.loc, N)
+        scale, scale_s = _flat_param(distribution.scale, N)
+        if cfg.noise is not None:
+            cfg.noise = cfg.noise.to(device=loc.device, dtype=torch.float32).reshape(cfg.K, N) \
+                .contiguous()
+        z = _NormalRsampleFn.apply(cfg, loc, loc_s, scale, scale_s)
+        return z.reshape((cfg.K,) + tuple(shape))
+    if cls is Beta:
+        shape = distribution.batch_shape
+        N = max(1, int(shape.numel()))
+        c1, c1_s = _flat_param(distribution.concentration1, N)
+        c0, c0_s = _flat_param(distribution.concentration0, N)
+        nat.require_device(c1, "guide Beta.concentration1")
+        if cfg.noise is not None:
+            cfg.noise = cfg.noise.to(device=c1.device, dtype=torch.float32).reshape(cfg.K, N) \
+                .contiguous()
+        x = _BetaRsampleFn.apply(cfg, c1, c1_s, c0, c0_s)
+        return x.reshape((cfg.K,) + tuple(shape))
+    if cfg.noise is not None:
+        return cfg.noise
+    return distribution.rsample(torch.Size([cfg.K]))
+
+
+def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: int,
+             particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None) \
+        -> Dict[str, torch.Tensor]:
+    """
+    Draw every factor of a factorised guide (dict order = stream id order).
+    """
+    samples = {}
+    for stream_id, (name, factor) in enumerate(approximation.items()):
+        cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
+                         particle_offset=particle_offset,
+                         noise=None if noise is None else noise.get(name))
+        samples[name] = draw(factor, cfg)
+    return samples

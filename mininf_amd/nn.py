@@ -1,0 +1,219 @@
+"""
+Learnable guides and losses (mirror of the reference's ``mininf/nn.py``).
+
+``ParameterizedDistribution`` / ``FactorizedDistribution`` / ``ParameterizedFactorizedDistribution``
+keep the reference's semantics exactly (host-side PyTorch modules, reference ``nn.py:29-187``).
+
+``EvidenceLowerBoundLoss`` (reference ``nn.py:190-228``) is the hot path. The reference draws ONE
+guide sample per call and runs the model once under ``LogProbTracer``; here ``num_particles=K``
+draws are taken at once by HIP samplers, the unchanged model is traced once over all particles
+(:mod:`mininf_amd.particles`), and the per-site log densities, their gradients and the
+Monte-Carlo reduction run in fused HIP kernels (:mod:`mininf_amd.engine`). With ``num_particles=1``
+the estimator is the reference's; for K > 1 it is the mean of K independent single-particle
+estimates. The returned loss is a 0-d float32 tensor with ``grad_fn``.
+"""
+from __future__ import annotations
+
+from typing import Callable, cast, Dict, Optional, Set, Type
+
+import torch
+from torch import distributions, nn
+
+from . import engine, guide, particles
+from .core import condition, LogProbTracer
+from .util import _normalize_shape, maybe_as_tensor, OptionalSize, TensorDict
+
+
+DistributionDict = Dict[str, torch.distributions.Distribution]
+
+
+def _is_identity_transform(transform: distributions.Transform) -> bool:
+    """
+    ``transform_to`` of an unconstrained support returns an empty ComposeTransform (reference
+    ``nn.py:16-26``).
+    """
+    return isinstance(transform, torch.distributions.ComposeTransform) and not transform.parts
+
+
+class ParameterizedDistribution(nn.Module):
+    """
+    Distribution whose (constrained) parameters are learnable; they are stored unconstrained via
+    ``transform_to(constraint).inv`` and mapped back on every call (reference ``nn.py:29-97``).
+
+    Args:
+        cls: Distribution type.
+        _const: Names of parameters held constant.
+        _clone: Copy parameters that need no transform so training does not modify the inputs.
+        **parameters: Initial parameter values.
+
+    Example:
+
+        >>> from mininf_amd.nn import ParameterizedDistribution
+        >>> from torch.distributions import Normal
+        >>> ParameterizedDistribution(Normal, loc=0.5, scale=1.2)()
+        Normal(loc: 0.5, scale: 1.2000000476837158)
+    """
+    def __init__(self, cls: Type[distributions.Distribution], *, _const: Set[str] | None = None,
+                 _clone: bool = True, **parameters: torch.Tensor) -> None:
+        super().__init__()
+        self.distribution_cls = cls
+        constant_names = _const or set()
+        constraints = cast(Dict, cls.arg_constraints)
+        self.distribution_constants: TensorDict = {}
+        learnable = {}
+        for name, initial in parameters.items():
+            if name in constant_names or name not in constraints:
+                self.distribution_constants[name] = initial
+                continue
+            initial = cast(torch.Tensor, maybe_as_tensor(initial))
+            transform = distributions.transform_to(constraints[name])
+            if _is_identity_transform(transform) and _clone:
+                unconstrained = 1 * initial
+            else:
+                unconstrained = transform.inv(initial)
+            learnable[name] = nn.Parameter(unconstrained)
+        self.distribution_parameters = nn.ParameterDict(learnable)
+
+    def forward(self) -> distributions.Distribution:
+        """"""
+        constraints = cast(Dict, self.distribution_cls.arg_constraints)
+        arguments = {}
+        for name, unconstrained in self.distribution_parameters.items():
+            transform = distributions.transform_to(constraints[name])
+            # `1 *` so the distribution never exposes the nn.Parameter itself.
+            arguments[name] = 1 * unconstrained if _is_identity_transform(transform) \
+                else transform(unconstrained)
+        return self.distribution_cls(**arguments, **self.distribution_constants)  # type: ignore
+
+
+class FactorizedDistribution(DistributionDict):
+    """
+    Mean-field joint of independent named factors (reference ``nn.py:100-159``).
+    """
+    def entropy(self) -> torch.Tensor:
+        """
+        Total entropy, summed over factors and their elements.
+        """
+        return cast(torch.Tensor, sum(factor.entropy().sum() for factor in self.values()))
+
+    def rsample(self, sample_shape: OptionalSize = None) -> TensorDict:
+        """
+        One reparameterised draw per factor.
+        """
+        shape = _normalize_shape(sample_shape)
+        return {name: factor.rsample(shape) for name, factor in self.items()}
+
+    def sample(self, sample_shape: OptionalSize = None) -> TensorDict:
+        """
+        One draw per factor (no gradient).
+        """
+        shape = _normalize_shape(sample_shape)
+        return {name: factor.sample(shape) for name, factor in self.items()}
+
+
+class ParameterizedFactorizedDistribution(nn.ModuleDict):
+    """
+    Module dictionary of :class:`ParameterizedDistribution` returning a
+    :class:`FactorizedDistribution` (reference ``nn.py:162-187``).
+    """
+    def __init__(self, arg: Dict[str, ParameterizedDistribution] | None = None,
+                 **kwargs: ParameterizedDistribution) -> None:
+        modules = dict(arg or {})
+        modules.update(kwargs)
+        super().__init__(modules)
+
+    def forward(self) -> FactorizedDistribution:
+        return FactorizedDistribution({name: module() for name, module in self.items()})
+
+
+class EvidenceLowerBoundLoss(nn.Module):
+    """
+    Negative evidence lower bound, estimated with ``num_particles`` Monte-Carlo particles on the
+    MI355X (reference ``nn.py:190-228``).
+
+    Args:
+        num_particles: Total number of particles K across all ranks (reference: 1).
+        seed: Seed of the counter-based guide sampler (default: derived from ``torch.initial_seed``).
+        validate: Check value supports and parameter constraints (one host sync per call), as the
+            reference does on every call (``core.py:142-189``).
+        process_group: ``torch.distributed`` group to shard the particles over (one rank per GPU);
+            each rank returns its share of the loss and gradients, combine them with
+            :func:`mininf_amd.distributed.all_reduce_gradients`.
+
+    Example:
+
+        >>> import torch
+        >>> from mininf_amd import sample
+        >>> from mininf_amd.nn import EvidenceLowerBoundLoss
+        >>> from torch.distributions import Normal
+        >>> def model():
+        ...     sample("x", Normal(0, 1))
+        >>> loss = EvidenceLowerBoundLoss(num_particles=256)
+        >>> loss(model, {"x": Normal(torch.zeros((), device="cuda"), 1.0)})  # doctest: +SKIP
+        tensor(..., device='cuda:0')
+    """
+    def __init__(self, num_particles: int = 1, *, seed: Optional[int] = None,
+                 validate: bool = True, process_group=None) -> None:
+        super().__init__()
+        if num_particles < 1:
+            raise ValueError("num_particles must be positive")
+        self.num_particles = int(num_particles)
+        self.seed = int(seed if seed is not None else torch.initial_seed()) & ((1 << 64) - 1)
+        self.validate = validate
+        self.process_group = process_group
+        self._step = 0
+
+    def _shard(self):
+        """
+        (world size, rank, local K, particle offset) of this rank.
+        """
+        if self.process_group is None:
+            return 1, 0, self.num_particles, 0
+        import torch.distributed as dist
+        world = dist.get_world_size(self.process_group)
+        rank = dist.get_rank(self.process_group)
+        if self.num_particles % world:
+            raise ValueError(f"num_particles={self.num_particles} is not divisible by the world "
+                             f"size {world}")
+        local = self.num_particles // world
+        return world, rank, local, rank * local
+
+    def forward(self, model: Callable,
+                approximation: torch.distributions.Distribution | DistributionDict,
+                _noise: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
+        """"""
+        if isinstance(approximation, Dict):
+            approximation = FactorizedDistribution(approximation)
+        world, _, K, offset = self._shard()
+        step = self._step
+        self._step += 1
+        if isinstance(approximation, dict):
+            samples = guide.draw_all(approximation, K, self.seed, step, offset, _noise)
+        else:
+            samples = approximation.rsample(torch.Size([K]))
+        if not isinstance(samples, Dict):
+            raise TypeError("Expected a distribution which samples dictionaries of tensors but got "
+                            f"a sample of type {type(samples)}")
+
+        trace = particles.trace_particles(model, samples, K, validate=self.validate)
+        # d loss / d T_k = -1 / K exactly (fp32), matching the `mul(-1/K)` below.
+        g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
+        joint = engine.log_joint(trace, g0)
+        if self.validate:
+            joint.raise_on_violation()
+        entropy = approximation.entropy()
+        if world > 1:
+            entropy = entropy / world
+        return (joint.total * g0).sum() - entropy
+
+
+class LogLikelihoodLoss(nn.Module):
+    """
+    Negative log likelihood at fixed parameter values (reference ``nn.py:231-257``), evaluated by
+    the reference-semantics :class:`~mininf_amd.core.LogProbTracer`.
+    """
+    def forward(self, model: Callable, parameters: TensorDict) -> torch.Tensor:
+        """"""
+        with LogProbTracer() as log_prob:
+            condition(model, **parameters)()
+        return - log_prob.total

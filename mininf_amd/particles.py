@@ -1,0 +1,281 @@
+"""
+Particle tracer: run an unchanged model once over all K Monte-Carlo particles and record its sites.
+
+The reference evaluates the log joint for ONE guide draw per loss call (``mininf/nn.py:217-226``)
+by running the model under ``LogProbTracer`` (``mininf/core.py:207-277``), which calls
+``distribution.log_prob(value)`` site by site. Here the model runs under :func:`torch.func.vmap`
+over the particle axis: user code still sees per-particle shapes (so ``sample`` shape validation,
+``batch`` and ``no_log_prob`` behave exactly as in the reference), but every tensor it produces is
+batched over K. :class:`ParticleTracer` is a :class:`~mininf_amd.core.TracerMixin` (the reference's
+plugin point, ``core.py:128-140``) that, instead of evaluating log densities, records each site's
+family, parameter tensors, value, mask and minibatch scale. The recorded [K, ...] tensors come back
+out of ``vmap`` and are handed to the HIP site kernels (:mod:`mininf_amd.engine`).
+
+Sites whose family has no HIP kernel (Gamma, Poisson, MultivariateNormal, InverseGamma, ...) are
+evaluated with ``torch.distributions`` inside the same ``vmap`` (on the GPU) and contribute one
+per-particle sum; they are outside the north-star families and listed in DESIGN.md.
+"""
+from __future__ import annotations
+
+import dataclasses
+import weakref
+from typing import Any, Callable, Dict, List, Optional, Tuple, cast
+
+import torch
+from torch.distributions import Bernoulli, Beta, Categorical, Distribution, Normal
+from torch.distributions.constraints import Constraint
+
+from . import core
+from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
+from .util import check_constraint, OptionalSize
+
+
+_functorch = torch._C._functorch
+
+
+def is_batched(tensor: Any) -> bool:
+    return isinstance(tensor, torch.Tensor) and _functorch.is_batchedtensor(tensor)
+
+
+@dataclasses.dataclass
+class SiteRecord:
+    """
+    One ``sample`` statement that contributes to the log joint.
+
+    ``roles`` holds output indices into the vmapped function's outputs for the family's roles
+    (Normal: loc, scale, value; Bernoulli: logits|probs, value; Beta: concentration1,
+    concentration0, value; Categorical: logits, value). After :func:`trace_particles` returns,
+    ``tensors`` holds the corresponding [K, ...] tensors.
+    """
+    name: str
+    family: str
+    roles: List[int]
+    site_shape: torch.Size
+    scale: float
+    mask: Optional[torch.Tensor]
+    description: str
+    tensors: List[torch.Tensor] = dataclasses.field(default_factory=list)
+
+
+@dataclasses.dataclass
+class CheckRecord:
+    """
+    A deferred support / constraint check that could not run inside vmap (a batched value).
+    ``output`` indexes a per-particle boolean output.
+    """
+    name: str
+    output: int
+    message: str
+
+
+# Unbatched (conditioned) data is validated once per tensor version instead of on every step:
+# key -> (weakref to tensor, version). The reference re-checks the full tensor on every call
+# (core.py:186-188), which is 27-63 % of its step time; the result is identical.
+_VALIDATED: Dict[Tuple, Tuple[weakref.ref, int]] = {}
+
+
+def _memo_key(value: torch.Tensor, constraint: Constraint) -> Tuple:
+    return (value.data_ptr(), tuple(value.shape), tuple(value.stride()), value.dtype,
+            str(value.device), repr(constraint))
+
+
+def check_unbatched(value: torch.Tensor, constraint: Constraint) -> bool:
+    """
+    ``check_constraint(constraint, value).all()`` memoised on (storage, layout, version).
+    """
+    masked = isinstance(value, torch.masked.MaskedTensor)
+    # The private fields avoid MaskedTensor.get_data (an autograd.Function, not vmap-compatible);
+    # the reference reads the same fields (mininf/util.py:85-89).
+    plain = value._masked_data if masked else value
+    key = _memo_key(plain, constraint)
+    hit = _VALIDATED.get(key)
+    if hit is not None and hit[0]() is plain and hit[1] == plain._version:
+        return True
+    with torch.no_grad():
+        passed = constraint.check(plain)
+        if masked:
+            mask = value._masked_mask
+            for _ in range(constraint.event_dim):
+                mask = mask.all(-1)
+            passed = passed | ~mask
+        ok = bool(passed.all())
+    if ok:
+        _VALIDATED[key] = (weakref.ref(plain), plain._version)
+    return ok
+
+
+def classify(distribution: Distribution) -> Tuple[str, List[Any]]:
+    """
+    Map a distribution onto a HIP site family and its role tensors, or ``("torch", [])``.
+    Exact type checks: subclasses may override ``log_prob``.
+    """
+    cls = type(distribution)
+    if cls is Normal:
+        return "normal", [distribution.loc, distribution.scale]
+    if cls is Bernoulli:
+        # torch evaluates via self.logits (bernoulli.py:121-125); use whichever parameter the
+        # distribution was constructed with so no extra lazy tensor is materialised.
+        if "logits" in distribution.__dict__:
+            return "bernoulli_logits", [distribution.logits]
+        return "bernoulli_probs", [distribution.probs]
+    if cls is Beta:
+        return "beta", [distribution.concentration1, distribution.concentration0]
+    if cls is Categorical:
+        return "categorical", [distribution.logits]
+    return "torch", []
+
+
+class ParticleTracer(TracerMixin):
+    """
+    Records sites of a model executing under ``vmap`` over particles.
+    """
+    def __init__(self, validate: bool = True) -> None:
+        super().__init__(_validate_parameters=validate)
+        self.sites: List[SiteRecord] = []
+        self.names: set = set()
+        self.outputs: List[torch.Tensor] = []
+        self.checks: List[CheckRecord] = []
+        self.fallback_outputs: List[Tuple[str, int]] = []
+
+    def _emit(self, tensor: torch.Tensor) -> int:
+        self.outputs.append(tensor)
+        return len(self.outputs) - 1
+
+    def _check_support(self, name: str, value: Any, distribution: Distribution,
+                       constraint: Constraint) -> None:
+        if not self._validate_parameters:
+            return
+        if is_batched(value):
+            ok = check_constraint(constraint, value).all()
+            self.checks.append(CheckRecord(name, self._emit(ok), str(core.support_error(
+                name, type(distribution).__name__))))
+        elif not check_unbatched(value, constraint):
+            raise core.support_error(name, distribution)
+
+    def sample(self, state: State, name: str, distribution: Distribution,
+               sample_shape: OptionalSize = None) -> torch.Tensor:
+        if isinstance(distribution, Value):
+            value = state.get(name, distribution.value)
+            if self._validate_parameters:
+                value = self._coerce(value, name)
+                validate_shape(value, name, distribution, sample_shape)
+                self._check_support(name, value, distribution, distribution.support)
+            return value
+
+        value = core._lookup_site_value(self.names, state, name)
+        if self._validate_parameters:
+            value = self._coerce(value, name)
+            validate_shape(value, name, distribution, sample_shape)
+        self.names.add(name)
+        if no_log_prob.get_instance():
+            if self._validate_parameters:
+                self._check_support(name, value, distribution, cast(Constraint,
+                                                                     distribution.support))
+            return value
+
+        masked = isinstance(value, torch.masked.MaskedTensor)
+        mask = None
+        data = value
+        if masked:
+            data, mask = value._masked_data, value._masked_mask
+            if is_batched(data) or is_batched(mask):
+                raise NotImplementedError(f"Masked values that depend on the particle axis are not "
+                                          f"supported (site '{name}').")
+
+        declared = batch.get_shape()
+        family, params = classify(distribution)
+        if family == "categorical":
+            shape = torch.broadcast_shapes(tuple(data.shape), distribution.batch_shape)
+        elif family != "torch":
+            shape = torch.broadcast_shapes(tuple(data.shape), *[tuple(p.shape) for p in params])
+        else:
+            shape = torch.Size(tuple(data.shape)[:data.dim() - len(distribution.event_shape)])
+        shape = torch.Size(shape)
+        if declared:
+            if masked:
+                raise ValueError("Batch dimensions are not supported for masked data.")
+            observed = shape[:len(declared)].numel()
+            scale = float(declared.numel()) / float(observed) if observed else 0.0
+        else:
+            scale = 1.0
+
+        if family == "torch":
+            self._record_torch_site(name, distribution, value, data, mask, scale)
+            return value
+
+        # Value support is checked by the site kernels (fused flag); constraint checks on the
+        # parameters as well (MI_FLAG_PARAM), replacing torch's validate_args at construction.
+        roles = [self._emit(p) for p in params] + [self._emit(data)]
+        self.sites.append(SiteRecord(name=name, family=family, roles=roles, site_shape=shape,
+                                     scale=scale, mask=mask,
+                                     description=type(distribution).__name__))
+        return value
+
+    def _record_torch_site(self, name: str, distribution: Distribution, value: Any,
+                           data: torch.Tensor, mask: Optional[torch.Tensor], scale: float) -> None:
+        if self._validate_parameters:
+            self._check_support(name, value, distribution, cast(Constraint, distribution.support))
+            for param, constraint in distribution.arg_constraints.items():
+                if param not in distribution.__dict__ and not hasattr(type(distribution), param):
+                    continue
+                try:
+                    tensor = getattr(distribution, param)
+                except Exception:  # lazily defined, unused parametrisations
+                    continue
+                if isinstance(tensor, torch.Tensor):
+                    ok = check_constraint(constraint, tensor).all()
+                    self.checks.append(CheckRecord(name, self._emit(ok), (
+                        f"Expected parameter {param} of distribution "
+                        f"{type(distribution).__name__} for site '{name}' to satisfy the "
+                        f"constraint {constraint}, but found invalid values")))
+        log_prob = distribution.log_prob(data)
+        if mask is not None:
+            log_prob = torch.where(mask, log_prob, torch.zeros((), dtype=log_prob.dtype,
+                                                               device=log_prob.device))
+        total = log_prob.sum() * scale if scale != 1.0 else log_prob.sum()
+        self.fallback_outputs.append((name, self._emit(total)))
+
+
+@dataclasses.dataclass
+class ParticleTrace:
+    sites: List[SiteRecord]
+    checks: List[Tuple[CheckRecord, torch.Tensor]]
+    fallback: List[Tuple[str, torch.Tensor]]
+    K: int
+
+
+_NO_VALIDATE = object()
+
+
+def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
+                    validate: bool = True) -> ParticleTrace:
+    """
+    Run ``condition(model, **samples)`` once under ``vmap`` over the leading (particle) dimension of
+    every sample and return the recorded sites with [K, ...] tensors.
+    """
+    names = list(samples)
+    tracer = ParticleTracer(validate=validate)
+
+    def per_particle(*values):
+        with tracer:
+            core.condition(model, **dict(zip(names, values)))()
+        return tuple(tracer.outputs)
+
+    previous = Distribution._validate_args
+    Distribution.set_default_validate_args(False)
+    try:
+        if names:
+            outputs = torch.func.vmap(per_particle, randomness="different")(
+                *[samples[name] for name in names])
+        else:
+            outputs = per_particle()
+            outputs = tuple(torch.as_tensor(o).expand(K, *torch.as_tensor(o).shape)
+                            for o in outputs)
+    finally:
+        Distribution.set_default_validate_args(previous)
+
+    for site in tracer.sites:
+        site.tensors = [outputs[index] for index in site.roles]
+    checks = [(check, outputs[check.output]) for check in tracer.checks]
+    fallback = [(name, outputs[index]) for name, index in tracer.fallback_outputs]
+    return ParticleTrace(sites=tracer.sites, checks=checks, fallback=fallback, K=K)
