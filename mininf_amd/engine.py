@@ -17,6 +17,7 @@ own layout), PARTICLE (one scalar per particle: reduced over elements inside the
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import dataclasses
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -54,6 +55,42 @@ def _collapse(t: torch.Tensor, K: int, shape: torch.Size) -> "_View":
     return _View(flat, flat.stride(0), flat.stride(1) if N > 1 else 1)
 
 
+_DEVICE_CACHE: "collections.OrderedDict[Tuple, Tuple[torch.Tensor, torch.Tensor]]" = \
+    collections.OrderedDict()
+
+
+def _to_device(t: torch.Tensor, K: int, device: torch.device, what: str,
+               allow_constant: bool = True) -> Tuple[Optional[torch.Tensor], Optional[float]]:
+    """
+    Bring a site tensor to the engine's device. Models written against the reference build
+    distributions from Python numbers and CPU data (e.g. ``Beta(2, 2)``): such unbatched host values
+    become kernel constants (scalars) or cached device copies (tensors, keyed on storage and
+    version). Returns (tensor, None) or (None, constant).
+    """
+    if t.device == device:
+        return t, None
+    if t.device.type != "cpu":
+        raise nat.NativeError(f"{what} lives on {t.device}, expected {device}")
+    if t.requires_grad:
+        raise nat.NativeError(f"{what} requires grad but lives on the CPU; move it to {device}")
+    unbatched = t.dim() > 0 and t.stride(0) == 0
+    base = t[0] if unbatched else t
+    if allow_constant and unbatched and base.numel() == 1:
+        return None, float(base.reshape(()))
+    key = (base.data_ptr(), tuple(base.shape), tuple(base.stride()), base.dtype, base._version,
+           str(device))
+    hit = _DEVICE_CACHE.get(key)
+    if hit is None:
+        hit = (base, base.to(device))
+        _DEVICE_CACHE[key] = hit
+        while len(_DEVICE_CACHE) > 64:
+            _DEVICE_CACHE.popitem(last=False)
+    else:
+        _DEVICE_CACHE.move_to_end(key)
+    moved = hit[1]
+    return (moved.expand((K,) + tuple(moved.shape)) if unbatched else moved), None
+
+
 def _float(t: torch.Tensor, what: str) -> torch.Tensor:
     if t.dtype != torch.float32:
         raise nat.NativeError(f"{what}: the HIP site kernels compute in float32 (the reference's "
@@ -63,24 +100,27 @@ def _float(t: torch.Tensor, what: str) -> torch.Tensor:
 
 @dataclasses.dataclass
 class _View:
-    tensor: torch.Tensor   # the autograd input ([K, N] view, or [K, 1] for per-particle scalars)
-    sk: int                # element strides over the logical [K, N] space
+    tensor: Optional[torch.Tensor]  # autograd input ([K, N] view, or [K, 1] per-particle scalars)
+    sk: int                         # element strides over the logical [K, N] space
     si: int
+    constant: Optional[float] = None  # host scalar (e.g. the 2.0 of `Beta(2, 2)`): no operand
 
     @property
     def key(self) -> Tuple:
+        if self.constant is not None:
+            return ("constant", self.constant)
         t = self.tensor
         return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), self.sk, self.si,
                 t.requires_grad)
 
     @property
     def dense(self) -> bool:
-        return self.sk != 0 and self.si != 0
+        return self.constant is None and self.sk != 0 and self.si != 0
 
     @property
     def per_particle(self) -> bool:
         """One scalar per particle: the gradient is reduced over elements inside the kernel."""
-        return self.tensor.shape[1] == 1 and self.si == 0
+        return self.constant is None and self.tensor.shape[1] == 1 and self.si == 0
 
 
 @dataclasses.dataclass
@@ -94,14 +134,17 @@ class _GroupLauncher:
     """
     Owns the ctypes descriptor of one site group and launches ``mi_group_forward``.
     """
-    def __init__(self, K: int, N: int, g0: float) -> None:
-        self.K, self.N, self.g0 = K, N, g0
+    def __init__(self, K: int, N: int, g0: float, device: torch.device) -> None:
+        self.K, self.N, self.g0, self.device = K, N, g0, device
         self.operands: List[_Operand] = []
         self.keys: Dict[Tuple, int] = {}
         self.sites: List[Tuple[SiteRecord, List[int], Optional[torch.Tensor]]] = []
         self.num_slots = 0
 
     def try_add(self, site: SiteRecord, views: List[_View], mask: Optional[_View]) -> bool:
+        constants = [v.constant for v in views]
+        views_in = views
+        views = [v for v in views if v.constant is None]
         new = {v.key for v in views if v.key not in self.keys}
         if len(self.sites) >= nat.MAX_SITES or len(self.operands) + len(new) > nat.MAX_OPERANDS:
             return False
@@ -123,7 +166,10 @@ class _GroupLauncher:
                 self.keys[v.key] = len(self.operands)
                 self.operands.append(_Operand(v, mode, slot))
             indices.append(self.keys[v.key])
-        self.sites.append((site, indices, mask))
+        it = iter(indices)
+        roles = [(-1, c) if c is not None else (next(it), 0.0) for c in constants]
+        assert len(roles) == len(views_in)
+        self.sites.append((site, roles, mask))
         return True
 
     def shares_dense_operand(self, views: List[_View]) -> bool:
@@ -133,7 +179,7 @@ class _GroupLauncher:
         return [op.view.tensor for op in self.operands]
 
     def run(self, compute_grads: bool):
-        device = self.operands[0].view.tensor.device
+        device = self.device
         K, N = self.K, self.N
         group = nat.Group()
         group.K, group.N = K, N
@@ -165,10 +211,10 @@ class _GroupLauncher:
             desc = group.sites[index]
             desc.family = FAMILY_CODES[site.family]
             if site.family.startswith("bernoulli"):
-                roles = [roles[0], -1, roles[1]]
+                roles = [roles[0], (-1, 0.0), roles[1]]
             for q in range(3):
-                desc.operand[q] = roles[q]
-                desc.constant[q] = 0.0
+                desc.operand[q] = roles[q][0]
+                desc.constant[q] = roles[q][1]
             if mask is not None:
                 desc.mask = mask.tensor.data_ptr()
                 desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
@@ -308,7 +354,7 @@ class LogJoint:
             cursor += 1
 
 
-def log_joint(trace: ParticleTrace, g0: float) -> LogJoint:
+def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint:
     """
     Launch the site kernels for every recorded site and return the per-particle log joint.
     """
@@ -317,10 +363,9 @@ def log_joint(trace: ParticleTrace, g0: float) -> LogJoint:
     totals: List[torch.Tensor] = []
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for site in trace.sites:
-        for t in site.tensors:
-            nat.require_device(t, f"site '{site.name}'")
         if site.family == "categorical":
-            logits, value = site.tensors
+            logits, value = (_to_device(t, K, device, f"site '{site.name}'", False)[0]
+                             for t in site.tensors)
             shape = site.site_shape
             C = logits.shape[-1]
             N = int(shape.numel())
@@ -328,18 +373,25 @@ def log_joint(trace: ParticleTrace, g0: float) -> LogJoint:
             lg = lg.reshape((K,) + (1,) * (len(shape) + 1 - (lg.dim() - 1)) + tuple(lg.shape[1:]))
             lg = lg.expand((K,) + tuple(shape) + (C,)).reshape(K, N, C).contiguous()
             val = _collapse(value.to(torch.int64), K, shape).tensor.expand(K, N)
-            mask = None if site.mask is None else \
-                site.mask.expand(shape).reshape(1, N).expand(K, N).to(torch.uint8)
+            mask = None if site.mask is None else site.mask.to(device).bool().expand(shape) \
+                .reshape(1, N).expand(K, N)
             holder: dict = {}
             totals.append(_CategoricalFn.apply(site, holder, g0, lg, val, mask))
             pending.append(("categorical", holder, [site]))
             continue
         shape = site.site_shape
         N = int(shape.numel())
-        tensors = [_collapse(_float(t, site.name), K, shape) for t in site.tensors]
+        views = []
+        for role, t in enumerate(site.tensors):
+            is_value = role == len(site.tensors) - 1
+            moved, constant = _to_device(_float(t, site.name), K, device, f"site '{site.name}'",
+                                         allow_constant=not is_value)
+            views.append(_View(None, 0, 0, constant) if constant is not None
+                         else _collapse(moved, K, shape))
+        tensors = views
         mask = None
         if site.mask is not None:
-            flat_mask = site.mask.bool().expand(shape).reshape(N)
+            flat_mask = site.mask.to(device).bool().expand(shape).reshape(N)
             mask = _View(flat_mask, 0, flat_mask.stride(0) if N > 1 else 1)
         placed = False
         for group_shape, launcher in groups:
@@ -348,7 +400,7 @@ def log_joint(trace: ParticleTrace, g0: float) -> LogJoint:
                 placed = True
                 break
         if not placed:
-            launcher = _GroupLauncher(K, N, g0)
+            launcher = _GroupLauncher(K, N, g0, device)
             launcher.try_add(site, tensors, mask)
             groups.append((shape, launcher))
     for _, launcher in groups:

@@ -198,7 +198,9 @@ class EvidenceLowerBoundLoss(nn.Module):
         trace = particles.trace_particles(model, samples, K, validate=self.validate)
         # d loss / d T_k = -1 / K exactly (fp32), matching the `mul(-1/K)` below.
         g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
-        joint = engine.log_joint(trace, g0)
+        device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)),
+                      torch.device("cuda", torch.cuda.current_device()))
+        joint = engine.log_joint(trace, g0, device)
         if self.validate:
             joint.raise_on_violation()
         entropy = approximation.entropy()
