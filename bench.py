@@ -1,0 +1,309 @@
+"""
+Benchmark of the ELBO hot path: site-log_prob evals/sec and ELBO step wall time on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
+
+One *step* = ``optimizer.zero_grad()`` + ELBO forward + backward (+ one RCCL all-reduce of the guide
+gradients when N > 1) + ``Adam.step()``, as in the reference's training loop (README.md:66-69).
+The default workload is C2 (BASELINE.json configs[1]): the README biased-coin model with n = 1e6
+observations and 4096 Monte-Carlo particles per GPU (particles are sharded across GPUs: weak
+scaling). One site-log_prob eval = one (particle, site, observed element) triple.
+
+Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (timed with HIP
+events around exactly that kernel during the timed steps) and the CPU baseline (the reference's
+torch-CPU semantics, oracle/cpu_port.py, on a bounded sample, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import mininf_amd  # noqa: E402
+from mininf_amd import engine  # noqa: E402
+from mininf_amd.distributed import all_reduce_gradients  # noqa: E402
+from torch.distributions import Bernoulli, Beta, Normal  # noqa: E402
+
+METRIC = "site-log_prob evals/sec + ELBO step wall-time, 1/2/4/8 MI355X"
+UNIT = "site-log_prob evals/s"
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (FMA = 2 FLOP)
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
+
+
+class EventTimer:
+    """
+    Collects (start, stop) HIP event pairs recorded by mi_group_forward_timed around the main site
+    kernel of each launch (engine.KERNEL_TIMER hook); keyed by the group's element count N so the
+    dominant kernel can be picked out.
+    """
+    def __init__(self):
+        self.pairs = []
+        self.active = False
+
+    def pair(self, launcher):
+        if not self.active:
+            return None, None
+        start = torch.cuda.Event(enable_timing=True)
+        stop = torch.cuda.Event(enable_timing=True)
+        start.record()   # materialise the underlying hipEvent_t; re-recorded by the library
+        stop.record()
+        self.pairs.append((launcher.N, launcher.K, start, stop))
+        return start, stop
+
+    def mean_ms(self, N):
+        times = [s.elapsed_time(e) for n, _, s, e in self.pairs if n == N]
+        return sum(times) / len(times) if times else float("nan"), len(times)
+
+
+# ------------------------------------------------------------------------------------------------
+# Workloads (restated from the reference's README / examples).
+# ------------------------------------------------------------------------------------------------
+def workload(name, device, world, rank):
+    gen = torch.Generator().manual_seed(0)
+    if name in ("c1", "c2"):
+        n = 10 if name == "c1" else 1_000_000
+        k_local = 1 if name == "c1" else 4096
+        x = (torch.rand(n, generator=gen) < 0.7).float().to(device)
+
+        def model():
+            theta = mininf_amd.sample("theta", Beta(2, 2))
+            mininf_amd.sample("x", Bernoulli(theta), sample_shape=[n])
+
+        guide = mininf_amd.nn.ParameterizedDistribution(Beta, concentration0=2.0,
+                                                        concentration1=2.0).to(device)
+        conditioned = mininf_amd.condition(model, x=x)
+        return dict(
+            desc=f"{name.upper()} Beta-Bernoulli (README model), n={n}, {k_local} particles/GPU",
+            k_local=k_local, n=n, module=guide, guide=lambda: {"theta": guide()},
+            conditioned=lambda step: conditioned, evals=k_local * (n + 1), lr=0.02,
+            dominant_N=n, bound="valu", flops_per_eval=2.0, bytes_per_eval=0.0,
+            data=f"synthetic: x ~ Bernoulli(0.7)[{n}] fp32 (seed 0); Beta(2,2) guide init")
+    if name in ("c3", "c4"):
+        p = 32
+        if name == "c3":
+            n_total, n_obs, k_local = 1_000_000, 1_000_000, 256
+        else:
+            n_total, n_obs, k_local = 10_000_000, 65536, 32
+        X = torch.randn(n_total, p, generator=gen)
+        true = torch.randn(p, generator=gen)
+        y = X @ true + torch.randn(n_total, generator=gen)
+        X, y = X.to(device), y.to(device)
+
+        def model():
+            theta = mininf_amd.sample("theta", Normal(0, 1), sample_shape=p)
+            with mininf_amd.batch(n_total):
+                with mininf_amd.no_log_prob():
+                    Xs = mininf_amd.sample("X", Normal(0, 1), sample_shape=(n_total, p))
+                mininf_amd.sample("y", Normal(Xs @ theta, 1))
+
+        guide = mininf_amd.nn.ParameterizedDistribution(
+            Normal, loc=1e-3 * torch.randn(p, generator=gen),
+            scale=(1e-3 * torch.randn(p, generator=gen)).exp()).to(device)
+        blocks = n_total // n_obs
+
+        def conditioned(step):
+            # Device-resident minibatch: a contiguous window (no host DataLoader, no copy).
+            start = ((step * 7919) % blocks) * n_obs
+            return mininf_amd.condition(model, X=X[start:start + n_obs], y=y[start:start + n_obs])
+
+        return dict(
+            desc=(f"{name.upper()} Bayesian linear regression, {n_total}x{p} (minibatch {n_obs}), "
+                  f"MF Normal guide, {k_local} particles/GPU"),
+            k_local=k_local, n=n_obs, module=guide, guide=lambda: {"theta": guide()},
+            conditioned=conditioned, evals=k_local * (n_obs + p), lr=0.01,
+            dominant_N=n_obs, bound="hbm", flops_per_eval=0.0, bytes_per_eval=8.0,
+            data=f"synthetic: X ~ N(0,1)[{n_total},{p}], y = X theta* + N(0,1) (seed 0)")
+    if name == "c5":
+        n, k_local = 1_000_000, 128
+        mu_true = torch.randn((), generator=gen)
+        z_true = mu_true + torch.randn(n, generator=gen)
+        y = (z_true + 0.5 * torch.randn(n, generator=gen)).to(device)
+        b = (torch.rand(n, generator=gen) < torch.sigmoid(z_true)).float().to(device)
+        mask = (torch.rand(n, generator=gen) > 0.2).to(device)
+        ym = torch.masked.as_masked_tensor(y, mask)
+        bm = torch.masked.as_masked_tensor(b, mask)
+
+        def model():
+            mu = mininf_amd.sample("mu", Normal(0, 1))
+            z = mininf_amd.sample("z", Normal(mu, 1), sample_shape=[n])
+            mininf_amd.sample("y", Normal(z, 0.5))
+            mininf_amd.sample("b", Bernoulli(logits=z))
+
+        guide = mininf_amd.nn.ParameterizedFactorizedDistribution(
+            mu=mininf_amd.nn.ParameterizedDistribution(Normal, loc=0.0, scale=1.0),
+            z=mininf_amd.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n),
+                                                      scale=torch.ones(n)),
+        ).to(device)
+        conditioned = mininf_amd.condition(model, y=ym, b=bm)
+        observed = int(mask.sum())
+        return dict(
+            desc=f"C5 masked hierarchical model, n={n}, {k_local} particles/GPU",
+            k_local=k_local, n=n, module=guide, guide=lambda: guide(),
+            conditioned=lambda step: conditioned,
+            evals=k_local * (1 + n + 2 * observed), lr=0.01, dominant_N=n, bound="hbm",
+            flops_per_eval=0.0, bytes_per_eval=None, observed=observed,
+            data=f"synthetic: y ~ N(z, 0.5), b ~ Bernoulli(logits=z), 20% masked (seed 0)")
+    raise SystemExit(f"unknown config {name}")
+
+
+def c5_bytes(w):
+    """
+    Algorithmic bytes of C5's dominant kernel (the fused z / y / b site group) per launch:
+    read z + write dz ([K, n] fp32 each) + y, b (fp32) and the mask (u8) once.
+    """
+    K, n = w["k_local"], w["n"]
+    return 8.0 * K * n + 9.0 * n
+
+
+def cpu_baseline(name, budget_s=12.0):
+    """
+    The reference's semantics on the host cores (oracle/cpu_port.py): K_cpu single-draw losses per
+    step, timed on a bounded sample; reported as evals/s of the same workload.
+    """
+    from oracle import cpu_port
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    cpu = torch.device("cpu")
+    w = workload(name, cpu, 1, 0)
+    k_cpu = min(w["k_local"], 16)
+    optimizer = torch.optim.Adam(w["module"].parameters(), lr=w["lr"])
+    steps = 0
+    evals_per_particle = w["evals"] / w["k_local"]
+    cpu_port.k_particle_step(w["conditioned"](0), w["guide"], optimizer, 1)   # warm-up
+    start = time.perf_counter()
+    while True:
+        cpu_port.k_particle_step(w["conditioned"](steps), w["guide"], optimizer, k_cpu)
+        steps += 1
+        elapsed = time.perf_counter() - start
+        if elapsed > budget_s or steps >= 200:
+            break
+    rate = evals_per_particle * k_cpu * steps / elapsed
+    model_name = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model_name = next(line.split(":", 1)[1].strip() for line in fh
+                              if line.startswith("model name"))
+    except (OSError, StopIteration):
+        model_name = platform.processor()
+    return {"value": rate, "unit": UNIT, "cores": torch.get_num_threads(), "kind": "port",
+            "sample": (f"{steps} steps x {k_cpu} single-draw particles of {w['desc']} in "
+                       f"{elapsed:.1f} s (reference semantics, torch {torch.__version__} CPU, "
+                       f"os.cpu_count()={os.cpu_count()}, {model_name})"),
+            "ms_per_step_extrapolated": 1e3 * elapsed / steps * w["k_local"] / k_cpu}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+        group = dist.group.WORLD
+
+    w = workload(args.config, device, world, rank)
+    module = w["module"]
+    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"])
+    loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(
+        num_particles=w["k_local"] * world, seed=1, validate=not args.no_validate,
+        process_group=group)
+    timer = EventTimer()
+    engine.KERNEL_TIMER = timer
+
+    def step(i):
+        optimizer.zero_grad()
+        loss = loss_fn(w["conditioned"](i), w["guide"]())
+        loss.backward()
+        if world > 1:
+            all_reduce_gradients(module.parameters(), group)
+        optimizer.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    timer.active = True
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.active = False
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    ms = 1e3 * elapsed / args.steps
+    value = w["evals"] * world * args.steps / elapsed
+    kernel_ms, launches = timer.mean_ms(w["dominant_N"])
+    kernel_s = kernel_ms * 1e-3
+    if w["bound"] == "valu":
+        flops = w["flops_per_eval"] * w["k_local"] * w["n"]
+        achieved = flops / kernel_s / 1e12
+        roof = {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                "kernel": "k_site_bcast<Bernoulli-probs>", "kernel_ms": kernel_ms,
+                "launches_timed": launches,
+                "algorithmic_per_launch": f"{flops:.4g} FLOP (2 FLOP/eval x K x n)"}
+    else:
+        if w["bytes_per_eval"] is None:
+            nbytes = c5_bytes(w)
+            kname = "k_group_row (z, y, b fused site group)"
+        else:
+            nbytes = w["bytes_per_eval"] * w["k_local"] * w["n"] + 8.0 * w["n"]
+            kname = "k_group_col (Normal(X@theta, 1) site)"
+        achieved = nbytes / kernel_s / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
+                "kernel_ms": kernel_ms, "launches_timed": launches,
+                "algorithmic_per_launch": f"{nbytes:.4g} B"}
+    out = {
+        "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": w["data"],
+        "config": {"workload": w["desc"], "particles_per_gpu": w["k_local"],
+                   "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
+                   "parallelism": f"particle-sharded x{world}" + (" + RCCL grad all-reduce"
+                                                                  if world > 1 else ""),
+                   "validate": not args.no_validate, "final_loss": float(loss.detach())},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.config)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -61,10 +61,17 @@ class Group(ctypes.Structure):
 # name -> (restype, argtypes). Mirrors include/mininf_amd.h one to one.
 _SIGNATURES = {
     "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "mi_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 3),
     "mi_group_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Group),
                                                 ctypes.POINTER(ctypes.c_size_t)]),
     "mi_group_forward": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp, c_vp,
                                         c_vp, c_vp, c_vp]),
+    "mi_group_forward_timed": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp,
+                                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mi_group_source": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.c_char_p, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_group_compile_check": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.c_char_p,
+                                              ctypes.c_size_t]),
     "mi_scale_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_float,
                                      c_vp]),
     "mi_categorical_workspace_bytes": (ctypes.c_int, [c_i64, c_i64,

@@ -4,15 +4,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/mininf_amd.h"
+#include "mininf_amd.h"
+#include "device_math.hpp"
 
-#define MI_DEV __device__ __forceinline__
 
 namespace mi {
 
-constexpr int kWave = 64;
-constexpr float kHalfLog2Pi = 0.91893853320467274178f;   // log(sqrt(2*pi)), normal.py:103
-constexpr float kFloatEps = 1.1920928955078125e-07f;    // torch.finfo(float32).eps, utils.py:101
 
 // ---------------------------------------------------------------------------------------------
 // Philox-4x32-10 (Salmon, Moraes, Dror, Shaw: "Parallel random numbers: as easy as 1, 2, 3",
@@ -65,57 +62,6 @@ MI_DEV void guide_normals(uint64_t seed, uint64_t step, uint32_t stream_id, uint
   const U4 b = guide_bits(seed, step, stream_id, 0, quad, particle);
   box_muller(b.x, b.y, out[0], out[1]);
   box_muller(b.z, b.w, out[2], out[3]);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Special functions (fp64).
-// ---------------------------------------------------------------------------------------------
-MI_DEV double digamma(double x) {
-  // Recurrence up to x >= 6, then the asymptotic (Bernoulli-number) series.
-  double shift = 0.0;
-  if (x <= 0.0 && x == floor(x)) return __builtin_inf();
-  if (x < 0.0) {
-    // Reflection: psi(1 - x) - psi(x) = pi * cot(pi * x).
-    shift = -M_PI / tan(M_PI * x);
-    x = 1.0 - x;
-  }
-  while (x < 6.0) {
-    shift -= 1.0 / x;
-    x += 1.0;
-  }
-  const double r = 1.0 / (x * x);
-  const double series =
-      r * (1.0 / 12 - r * (1.0 / 120 - r * (1.0 / 252 - r * (1.0 / 240 - r * (1.0 / 132)))));
-  return shift + log(x) - 0.5 / x - series;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Wavefront reductions.
-// ---------------------------------------------------------------------------------------------
-MI_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int offset = 32; offset > 0; offset >>= 1) v += __shfl_xor(v, offset, kWave);
-  return v;
-}
-
-MI_DEV double wave_sum(double v) {
-#pragma unroll
-  for (int offset = 32; offset > 0; offset >>= 1) v += __shfl_xor(v, offset, kWave);
-  return v;
-}
-
-// Sum over lanes that differ only in bits >= log2(width) (lanes sharing lane % width).
-MI_DEV float wave_sum_strided(float v, int width) {
-  for (int offset = 32; offset >= width; offset >>= 1) v += __shfl_xor(v, offset, kWave);
-  return v;
-}
-
-// OR-combine per-lane flag words across the wave and publish them with one atomic; must be called
-// with every lane of the wave active.
-MI_DEV void publish_flags(uint32_t* flags, uint32_t mine) {
-#pragma unroll
-  for (int offset = 32; offset > 0; offset >>= 1) mine |= __shfl_xor(mine, offset, kWave);
-  if (mine != 0u && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, mine);
 }
 
 }  // namespace mi

@@ -1,0 +1,147 @@
+// Device math shared by the precompiled kernels (sites.hip) and the site programs specialised at
+// trace time with hiprtc (jit.cpp embeds this file verbatim): family log-densities and their
+// derivatives, special functions, wavefront reductions. No includes beyond mininf_amd.h so that it
+// compiles both under hipcc (after hip_runtime.h) and under hiprtc.
+#pragma once
+
+#include "mininf_amd.h"
+
+#define MI_DEV __device__ __forceinline__
+
+namespace mi {
+
+constexpr int kWave = 64;
+constexpr float kHalfLog2Pi = 0.91893853320467274178f;   // log(sqrt(2*pi)), normal.py:103
+constexpr float kFloatEps = 1.1920928955078125e-07f;    // torch.finfo(float32).eps, utils.py:101
+
+// ---------------------------------------------------------------------------------------------
+// Special functions (fp64).
+// ---------------------------------------------------------------------------------------------
+MI_DEV double digamma(double x) {
+  // Recurrence up to x >= 6, then the asymptotic (Bernoulli-number) series.
+  double shift = 0.0;
+  if (x <= 0.0 && x == floor(x)) return __builtin_inf();
+  if (x < 0.0) {
+    // Reflection: psi(1 - x) - psi(x) = pi * cot(pi * x).
+    shift = -3.14159265358979323846 / tan(3.14159265358979323846 * x);
+    x = 1.0 - x;
+  }
+  while (x < 6.0) {
+    shift -= 1.0 / x;
+    x += 1.0;
+  }
+  const double r = 1.0 / (x * x);
+  const double series =
+      r * (1.0 / 12 - r * (1.0 / 120 - r * (1.0 / 252 - r * (1.0 / 240 - r * (1.0 / 132)))));
+  return shift + log(x) - 0.5 / x - series;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wavefront reductions.
+// ---------------------------------------------------------------------------------------------
+MI_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int offset = 32; offset > 0; offset >>= 1) v += __shfl_xor(v, offset, kWave);
+  return v;
+}
+
+MI_DEV double wave_sum(double v) {
+#pragma unroll
+  for (int offset = 32; offset > 0; offset >>= 1) v += __shfl_xor(v, offset, kWave);
+  return v;
+}
+
+// Sum over lanes that differ only in bits >= log2(width) (lanes sharing lane % width).
+MI_DEV float wave_sum_strided(float v, int width) {
+  for (int offset = 32; offset >= width; offset >>= 1) v += __shfl_xor(v, offset, kWave);
+  return v;
+}
+
+// OR-combine per-lane flag words across the wave and publish them with one atomic; must be called
+// with every lane of the wave active.
+MI_DEV void publish_flags(uint32_t* flags, uint32_t mine) {
+#pragma unroll
+  for (int offset = 32; offset > 0; offset >>= 1) mine |= __shfl_xor(mine, offset, kWave);
+  if (mine != 0u && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, mine);
+}
+
+// -------------------------------------------------------------------------------------------------
+// Per-element family math.  d[r] = d log p / d role_r.
+// -------------------------------------------------------------------------------------------------
+struct Elem {
+  float lp;
+  float d[3];
+  uint32_t param_bad;
+  uint32_t support_bad;
+};
+
+// Normal(loc, scale): -(v-loc)^2 / (2 scale^2) - log(scale) - log(sqrt(2 pi))
+// torch/distributions/normal.py:88-103; support real (constraints.py: `value == value`).
+MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
+  const float inv = 1.0f / scale;
+  const float z = (v - loc) * inv;
+  e.lp = -0.5f * z * z - logf(scale) - kHalfLog2Pi;
+  e.d[0] = z * inv;
+  e.d[1] = (z * z - 1.0f) * inv;
+  e.d[2] = -z * inv;
+  e.param_bad = !(scale > 0.0f) || (loc != loc);
+  e.support_bad = (v != v);
+}
+
+// Bernoulli(logits): -BCE_with_logits(l, v) = -(max(l, 0) - l v + log1p(exp(-|l|)))
+// torch/distributions/bernoulli.py:121-125; support boolean {0, 1} (constraints.py:317-325).
+MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
+  const float t = expf(-fabsf(l));
+  e.lp = -(fmaxf(l, 0.0f) - l * v + log1pf(t));
+  const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
+  e.d[0] = v - sig;
+  e.d[1] = 0.0f;
+  e.d[2] = l;
+  e.param_bad = (l != l);
+  e.support_bad = !(v == 0.0f || v == 1.0f);
+}
+
+// Bernoulli(probs): logits = log(p_c) - log1p(-p_c), p_c = clamp(p, eps, 1 - eps)
+// (bernoulli.py:104-106 -> utils.py probs_to_logits / clamp_probs); clamp passes the gradient
+// only inside [eps, 1 - eps].
+MI_DEV void bernoulli_probs_to_logits(float p, float& l, float& dl_dp) {
+  const float hi = 1.0f - kFloatEps;
+  const float pc = fminf(fmaxf(p, kFloatEps), hi);
+  l = logf(pc) - log1pf(-pc);
+  dl_dp = (p >= kFloatEps && p <= hi) ? (1.0f / pc + 1.0f / (1.0f - pc)) : 0.0f;
+}
+
+MI_DEV void eval_bernoulli_probs(float p, float v, Elem& e) {
+  float l, dl_dp;
+  bernoulli_probs_to_logits(p, l, dl_dp);
+  eval_bernoulli_logits(l, v, e);
+  e.d[0] *= dl_dp;
+  e.param_bad = !(p >= 0.0f && p <= 1.0f);
+}
+
+MI_DEV float xlogy(float x, float y) { return (y != y) ? y : (x == 0.0f ? 0.0f : x * logf(y)); }
+
+// Beta(c1, c0) = Dirichlet([c1, c0]) at [v, 1 - v]:
+//   xlogy(c1 - 1, v) + xlogy(c0 - 1, 1 - v) + lgamma(c1 + c0) - lgamma(c1) - lgamma(c0)
+// torch/distributions/beta.py:88-92 -> dirichlet.py:90-97; support [0, 1] (unit_interval).
+MI_DEV void eval_beta(float a, float b, float v, Elem& e) {
+  const float w = 1.0f - v;
+  e.lp = xlogy(a - 1.0f, v) + xlogy(b - 1.0f, w) + lgammaf(a + b) - lgammaf(a) - lgammaf(b);
+  const double psi_ab = digamma((double)a + (double)b);
+  e.d[0] = logf(v) + (float)(psi_ab - digamma((double)a));
+  e.d[1] = logf(w) + (float)(psi_ab - digamma((double)b));
+  e.d[2] = (a - 1.0f) / v - (b - 1.0f) / w;
+  e.param_bad = !(a > 0.0f) || !(b > 0.0f);
+  e.support_bad = !(v >= 0.0f && v <= 1.0f);
+}
+
+MI_DEV void eval_family(int family, float r0, float r1, float r2, Elem& e) {
+  switch (family) {
+    case MI_NORMAL: eval_normal(r0, r1, r2, e); break;
+    case MI_BERNOULLI_LOGITS: eval_bernoulli_logits(r0, r2, e); break;
+    case MI_BERNOULLI_PROBS: eval_bernoulli_probs(r0, r2, e); break;
+    default: eval_beta(r0, r1, r2, e); break;
+  }
+}
+
+}  // namespace mi

@@ -58,48 +58,70 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
   }
 }
 
-// Partial sums over particle slices: part[(slice * 2 + {0: dloc, 1: dscale}) * N + i].
+// Backward of the Normal draw, reduced over particles. A block is TI quad-lanes x TK particle-lanes
+// (TI * TK = 256, TI = min(64, quads)): coalesced along elements for large N, and still 256-wide for
+// N = 1 (a scalar guide factor with thousands of particles). Each block covers one slice of the
+// particles; per-block sums are combined in a fixed order through LDS and written per slice.
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
     const float* __restrict__ dz, int64_t dz_sk, int64_t dz_si, int64_t K, int64_t N,
     uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in,
     float* __restrict__ out_loc, float* __restrict__ out_scale, int64_t out_stride,
-    int64_t rows_per_block) {
-  const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+    int64_t rows_per_block, int ti) {
+  __shared__ float red[kGuideThreads][8];
+  const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kGuideThreads / ti;
+  const int64_t quad = (int64_t)blockIdx.x * ti + tx;
   const int64_t i0 = quad * 4;
-  if (i0 >= N) return;
   const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t k1 = min(K, k0 + rows_per_block);
-  const bool vec = (dz_si == 1) && (i0 + 4 <= N) && ((N & 3) == 0) && ((dz_sk & 3) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(dz) & 15) == 0);
   float sl[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t k = k0; k < k1; ++k) {
-    float g[4];
-    if (vec) {
-      const float4 v = *reinterpret_cast<const float4*>(dz + k * dz_sk + i0);
-      g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
-    } else {
+  if (i0 < N) {
+    const bool vec = (dz_si == 1) && (i0 + 4 <= N) && ((N & 3) == 0) && ((dz_sk & 3) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(dz) & 15) == 0);
+    for (int64_t k = k0 + ty; k < k1; k += tk) {
+      float g[4];
+      if (vec) {
+        const float4 v = *reinterpret_cast<const float4*>(dz + k * dz_sk + i0);
+        g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = (i0 + j < N) ? dz[k * dz_sk + (i0 + j) * dz_si] : 0.0f;
-    }
-    float e[4];
-    if (eps_in != nullptr) {
+        for (int j = 0; j < 4; ++j) g[j] = (i0 + j < N) ? dz[k * dz_sk + (i0 + j) * dz_si] : 0.0f;
+      }
+      float e[4];
+      if (eps_in != nullptr) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
-    } else {
-      guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
-    }
+        for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
+      } else {
+        guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sl[j] += g[j];
-      ss[j] = fmaf(g[j], e[j], ss[j]);
+      for (int j = 0; j < 4; ++j) {
+        sl[j] += g[j];
+        ss[j] = fmaf(g[j], e[j], ss[j]);
+      }
     }
   }
-  const int64_t slice = blockIdx.y;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    if (i0 + j < N) {
-      out_loc[slice * out_stride + i0 + j] = sl[j];
-      out_scale[slice * out_stride + i0 + j] = ss[j];
+    red[threadIdx.x][j] = sl[j];
+    red[threadIdx.x][4 + j] = ss[j];
+  }
+  __syncthreads();
+  if (ty == 0 && i0 < N) {
+    float tl[4] = {0.f, 0.f, 0.f, 0.f}, ts[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < tk; ++r) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        tl[j] += red[r * ti + tx][j];
+        ts[j] += red[r * ti + tx][4 + j];
+      }
+    }
+    const int64_t slice = blockIdx.y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j < N) {
+        out_loc[slice * out_stride + i0 + j] = tl[j];
+        out_scale[slice * out_stride + i0 + j] = ts[j];
+      }
     }
   }
 }
@@ -306,25 +328,38 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
     const float* __restrict__ dx, int64_t dx_sk, int64_t dx_si, const float* __restrict__ x,
     const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
     int64_t K, int64_t N, float* __restrict__ out1, float* __restrict__ out0, int64_t out_stride,
-    int64_t rows_per_block) {
-  const int64_t i = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
-  if (i >= N) return;
+    int64_t rows_per_block, int ti) {
+  __shared__ double red[kGuideThreads][2];
+  const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kGuideThreads / ti;
+  const int64_t i = (int64_t)blockIdx.x * ti + tx;
   const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
   const int64_t k1 = min(K, k0 + rows_per_block);
-  const float a = c1[i * c1_s], b = c0[i * c0_s];
-  const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
   double s1 = 0.0, s0 = 0.0;
-  for (int64_t k = k0; k < k1; ++k) {
-    const float g = dx[k * dx_sk + i * dx_si];
-    if (g == 0.0f) continue;
-    const float xv = x[k * N + i];
-    const float xw = 1.0f - xv;
-    // _Dirichlet_backward: grad_j * (go_j - sum(x * go)) with go = (g, 0)
-    s1 += dirichlet_grad(xv, a, tot) * (double)g * (double)(1.0f - xv);
-    s0 -= dirichlet_grad(xw, b, tot) * (double)g * (double)xv;
+  if (i < N) {
+    const float a = c1[i * c1_s], b = c0[i * c0_s];
+    const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
+    for (int64_t k = k0 + ty; k < k1; k += tk) {
+      const float g = dx[k * dx_sk + i * dx_si];
+      if (g == 0.0f) continue;
+      const float xv = x[k * N + i];
+      const float xw = 1.0f - xv;
+      // _Dirichlet_backward: grad_j * (go_j - sum(x * go)) with go = (g, 0)
+      s1 += dirichlet_grad(xv, a, tot) * (double)g * (double)(1.0f - xv);
+      s0 -= dirichlet_grad(xw, b, tot) * (double)g * (double)xv;
+    }
   }
-  out1[blockIdx.y * out_stride + i] = (float)s1;
-  out0[blockIdx.y * out_stride + i] = (float)s0;
+  red[threadIdx.x][0] = s1;
+  red[threadIdx.x][1] = s0;
+  __syncthreads();
+  if (ty == 0 && i < N) {
+    double t1 = 0.0, t0 = 0.0;
+    for (int r = 0; r < tk; ++r) {
+      t1 += red[r * ti + tx][0];
+      t0 += red[r * ti + tx][1];
+    }
+    out1[blockIdx.y * out_stride + i] = (float)t1;
+    out0[blockIdx.y * out_stride + i] = (float)t0;
+  }
 }
 
 // Raw generator access for tests.
@@ -358,13 +393,26 @@ namespace {
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
-// Particle slices for the particle-reducing backward kernels: enough blocks to fill the chip,
-// at least 16 particles per slice.
-int64_t bwd_slices(int64_t K, int64_t N, int64_t elems_per_block) {
-  const int64_t gx = ceil_div(N, elems_per_block);
-  int64_t slices = ceil_div(2048, gx);
-  slices = std::min<int64_t>(slices, ceil_div(K, 16));
-  return std::max<int64_t>(1, slices);
+// Launch geometry of the particle-reducing backward kernels: `lanes` element lanes per block
+// (TI), 256 / TI particle lanes, and enough particle slices to fill the chip.
+struct BwdGeometry {
+  int ti;
+  int64_t gx, slices, rows;
+};
+
+BwdGeometry bwd_geometry(int64_t K, int64_t units) {
+  BwdGeometry g{};
+  int ti = 1;
+  while (ti < 64 && ti < units) ti <<= 1;
+  g.ti = ti;
+  const int tk = 256 / ti;
+  g.gx = ceil_div(units, ti);
+  int64_t slices = ceil_div(1024, g.gx);
+  slices = std::min<int64_t>(slices, ceil_div(K, (int64_t)tk * 4));
+  slices = std::max<int64_t>(1, slices);
+  g.rows = ceil_div(K, slices);
+  g.slices = ceil_div(K, g.rows);
+  return g;
 }
 
 }  // namespace
@@ -387,8 +435,8 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
 
 int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
   if (K < 1 || N < 1 || bytes == nullptr) return MI_EINVAL;
-  const int64_t slices = bwd_slices(K, N, 4 * mi::kGuideThreads);
-  *bytes = slices > 1 ? (size_t)slices * 2 * (size_t)N * sizeof(float) : 0;
+  const BwdGeometry geo = bwd_geometry(K, ceil_div(N, 4));
+  *bytes = geo.slices > 1 ? (size_t)geo.slices * 2 * (size_t)N * sizeof(float) : 0;
   return 0;
 }
 
@@ -402,10 +450,8 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
   mi_normal_rsample_backward_workspace_bytes(K, N, &need);
   if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t slices = bwd_slices(K, N, 4 * mi::kGuideThreads);
-  const int64_t rows = ceil_div(K, slices);
-  const int64_t gy = ceil_div(K, rows);
-  const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
+  const BwdGeometry geo = bwd_geometry(K, ceil_div(N, 4));
+  const int64_t rows = geo.rows, gy = geo.slices, gx = geo.gx;
   float* out_loc = dloc;
   float* out_scale = dscale;
   if (gy > 1) {
@@ -414,7 +460,7 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
   }
   hipLaunchKernelGGL(mi::k_normal_rsample_bwd, dim3((unsigned)gx, (unsigned)gy),
                      dim3(mi::kGuideThreads), 0, s, dz, dz_stride_k, dz_stride_i, K, N, seed, step,
-                     stream_id, particle_offset, eps, out_loc, out_scale, N, rows);
+                     stream_id, particle_offset, eps, out_loc, out_scale, N, rows, geo.ti);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
@@ -436,8 +482,8 @@ int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t
 
 int mi_beta_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
   if (K < 1 || N < 1 || bytes == nullptr) return MI_EINVAL;
-  const int64_t slices = bwd_slices(K, N, mi::kGuideThreads);
-  *bytes = slices > 1 ? (size_t)slices * 2 * (size_t)N * sizeof(float) : 0;
+  const BwdGeometry geo = bwd_geometry(K, N);
+  *bytes = geo.slices > 1 ? (size_t)geo.slices * 2 * (size_t)N * sizeof(float) : 0;
   return 0;
 }
 
@@ -452,19 +498,17 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
   mi_beta_rsample_backward_workspace_bytes(K, N, &need);
   if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t slices = bwd_slices(K, N, mi::kGuideThreads);
-  const int64_t rows = ceil_div(K, slices);
-  const int64_t gy = ceil_div(K, rows);
+  const BwdGeometry geo = bwd_geometry(K, N);
+  const int64_t rows = geo.rows, gy = geo.slices;
   float* o1 = dc1;
   float* o0 = dc0;
   if (gy > 1) {
     o1 = static_cast<float*>(workspace);
     o0 = o1 + gy * N;
   }
-  hipLaunchKernelGGL(mi::k_beta_rsample_bwd,
-                     dim3((unsigned)ceil_div(N, mi::kGuideThreads), (unsigned)gy),
+  hipLaunchKernelGGL(mi::k_beta_rsample_bwd, dim3((unsigned)geo.gx, (unsigned)gy),
                      dim3(mi::kGuideThreads), 0, s, dx, dx_stride_k, dx_stride_i, x, c1, c1_stride,
-                     c0, c0_stride, K, N, o1, o0, N, rows);
+                     c0, c0_stride, K, N, o1, o0, N, rows, geo.ti);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);

@@ -22,87 +22,12 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "jit.hpp"
 
 namespace mi {
-
-// -------------------------------------------------------------------------------------------------
-// Per-element family math.  d[r] = d log p / d role_r.
-// -------------------------------------------------------------------------------------------------
-struct Elem {
-  float lp;
-  float d[3];
-  uint32_t param_bad;
-  uint32_t support_bad;
-};
-
-// Normal(loc, scale): -(v-loc)^2 / (2 scale^2) - log(scale) - log(sqrt(2 pi))
-// torch/distributions/normal.py:88-103; support real (constraints.py: `value == value`).
-MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
-  const float inv = 1.0f / scale;
-  const float z = (v - loc) * inv;
-  e.lp = -0.5f * z * z - logf(scale) - kHalfLog2Pi;
-  e.d[0] = z * inv;
-  e.d[1] = (z * z - 1.0f) * inv;
-  e.d[2] = -z * inv;
-  e.param_bad = !(scale > 0.0f) || (loc != loc);
-  e.support_bad = (v != v);
-}
-
-// Bernoulli(logits): -BCE_with_logits(l, v) = -(max(l, 0) - l v + log1p(exp(-|l|)))
-// torch/distributions/bernoulli.py:121-125; support boolean {0, 1} (constraints.py:317-325).
-MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
-  const float t = expf(-fabsf(l));
-  e.lp = -(fmaxf(l, 0.0f) - l * v + log1pf(t));
-  const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
-  e.d[0] = v - sig;
-  e.d[1] = 0.0f;
-  e.d[2] = l;
-  e.param_bad = (l != l);
-  e.support_bad = !(v == 0.0f || v == 1.0f);
-}
-
-// Bernoulli(probs): logits = log(p_c) - log1p(-p_c), p_c = clamp(p, eps, 1 - eps)
-// (bernoulli.py:104-106 -> utils.py probs_to_logits / clamp_probs); clamp passes the gradient
-// only inside [eps, 1 - eps].
-MI_DEV void bernoulli_probs_to_logits(float p, float& l, float& dl_dp) {
-  const float hi = 1.0f - kFloatEps;
-  const float pc = fminf(fmaxf(p, kFloatEps), hi);
-  l = logf(pc) - log1pf(-pc);
-  dl_dp = (p >= kFloatEps && p <= hi) ? (1.0f / pc + 1.0f / (1.0f - pc)) : 0.0f;
-}
-
-MI_DEV void eval_bernoulli_probs(float p, float v, Elem& e) {
-  float l, dl_dp;
-  bernoulli_probs_to_logits(p, l, dl_dp);
-  eval_bernoulli_logits(l, v, e);
-  e.d[0] *= dl_dp;
-  e.param_bad = !(p >= 0.0f && p <= 1.0f);
-}
-
-MI_DEV float xlogy(float x, float y) { return (y != y) ? y : (x == 0.0f ? 0.0f : x * logf(y)); }
-
-// Beta(c1, c0) = Dirichlet([c1, c0]) at [v, 1 - v]:
-//   xlogy(c1 - 1, v) + xlogy(c0 - 1, 1 - v) + lgamma(c1 + c0) - lgamma(c1) - lgamma(c0)
-// torch/distributions/beta.py:88-92 -> dirichlet.py:90-97; support [0, 1] (unit_interval).
-MI_DEV void eval_beta(float a, float b, float v, Elem& e) {
-  const float w = 1.0f - v;
-  e.lp = xlogy(a - 1.0f, v) + xlogy(b - 1.0f, w) + lgammaf(a + b) - lgammaf(a) - lgammaf(b);
-  const double psi_ab = digamma((double)a + (double)b);
-  e.d[0] = logf(v) + (float)(psi_ab - digamma((double)a));
-  e.d[1] = logf(w) + (float)(psi_ab - digamma((double)b));
-  e.d[2] = (a - 1.0f) / v - (b - 1.0f) / w;
-  e.param_bad = !(a > 0.0f) || !(b > 0.0f);
-  e.support_bad = !(v >= 0.0f && v <= 1.0f);
-}
-
-MI_DEV void eval_family(int family, float r0, float r1, float r2, Elem& e) {
-  switch (family) {
-    case MI_NORMAL: eval_normal(r0, r1, r2, e); break;
-    case MI_BERNOULLI_LOGITS: eval_bernoulli_logits(r0, r2, e); break;
-    case MI_BERNOULLI_PROBS: eval_bernoulli_probs(r0, r2, e); break;
-    default: eval_beta(r0, r1, r2, e); break;
-  }
-}
 
 // Uniform (scalar-branch) selection from compile-time-indexed register arrays; `idx` is always
 // wave-uniform (it comes from the kernel argument block), so no VALU select chains are emitted.
@@ -287,8 +212,8 @@ __global__ __launch_bounds__(256) void k_group_col(const mi_group G, float* __re
 // BCAST: one site, parameters are per-particle scalars (or constants), the value is shared data.
 // -------------------------------------------------------------------------------------------------
 constexpr int kBcastThreads = 256;
-constexpr int kBcastP = 4;          // particles per lane
-constexpr int kBcastChunk = 4096;   // elements staged per block
+constexpr int kBcastP = 8;          // particles per lane
+constexpr int kBcastChunk = 2048;   // elements staged per block
 
 MI_DEV float role_scalar(const mi_group& G, const mi_site& st, int q, int64_t k) {
   const int o = st.operand[q];
@@ -411,45 +336,74 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
   double acc1[kBcastP], acc2[kBcastP];
 #pragma unroll
   for (int p = 0; p < kBcastP; ++p) acc1[p] = acc2[p] = 0.0;
+
+  // One quad of staged features against all P particles of this lane. `exact` quads hold four real
+  // elements; the others (the chunk's tail) use the masked formulation, which is neutral for the
+  // zero padding.
+  auto quad = [&](const float4 x, const float4 y, float (&in1)[kBcastP], float (&in2)[kBcastP],
+                  bool exact) {
+    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+      // log p(x | l) = x l - softplus(l): one FMA per (particle, element)
+#pragma unroll
+      for (int p = 0; p < kBcastP; ++p) {
+        in1[p] = fmaf(x.x, ca[p], in1[p]);
+        in1[p] = fmaf(x.y, ca[p], in1[p]);
+        in1[p] = fmaf(x.z, ca[p], in1[p]);
+        in1[p] = fmaf(x.w, ca[p], in1[p]);
+      }
+    } else if (FAMILY == MI_NORMAL) {
+#pragma unroll
+      for (int p = 0; p < kBcastP; ++p) {
+        const float d0 = x.x - ca[p], d1 = x.y - ca[p], d2 = x.z - ca[p], d3 = x.w - ca[p];
+        if (MASKED || !exact) {
+          const float e0 = y.x * d0, e1 = y.y * d1, e2 = y.z * d2, e3 = y.w * d3;
+          in1[p] += (e0 + e1) + (e2 + e3);
+          in2[p] = fmaf(e0, d0, fmaf(e1, d1, fmaf(e2, d2, fmaf(e3, d3, in2[p]))));
+        } else {
+          in1[p] += (d0 + d1) + (d2 + d3);
+          in2[p] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, in2[p]))));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < kBcastP; ++p) {
+        in1[p] = fmaf(x.x, ca[p], fmaf(x.y, ca[p], fmaf(x.z, ca[p], fmaf(x.w, ca[p], in1[p]))));
+        in1[p] = fmaf(y.x, cb[p], fmaf(y.y, cb[p], fmaf(y.z, cb[p], fmaf(y.w, cb[p], in1[p]))));
+      }
+    }
+  };
+
   const int nq = (int)((len + 3) / 4);
-  for (int q0 = 0; q0 < nq; q0 += 16) {
+  const int full = (int)(len / 4) & ~15;
+  for (int q0 = 0; q0 < full; q0 += 16) {
     float in1[kBcastP], in2[kBcastP];
 #pragma unroll
     for (int p = 0; p < kBcastP; ++p) in1[p] = in2[p] = 0.0f;
-    const int q1 = min(nq, q0 + 16);
-    for (int q = q0; q < q1; ++q) {
-      const float4 x = feat[0][q];
-      if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
-        // log p(x | l) = x l - softplus(l): one FMA per (particle, element)
 #pragma unroll
-        for (int p = 0; p < kBcastP; ++p) {
-          in1[p] = fmaf(x.x, ca[p], in1[p]);
-          in1[p] = fmaf(x.y, ca[p], in1[p]);
-          in1[p] = fmaf(x.z, ca[p], in1[p]);
-          in1[p] = fmaf(x.w, ca[p], in1[p]);
-        }
-      } else if (FAMILY == MI_NORMAL) {
-        const float4 m = feat[NF - 1][q];
+    for (int h = 0; h < 2; ++h) {
+      float4 xs[8], ys[8];
 #pragma unroll
-        for (int p = 0; p < kBcastP; ++p) {
-          const float d0 = x.x - ca[p], d1 = x.y - ca[p], d2 = x.z - ca[p], d3 = x.w - ca[p];
-          if (MASKED) {
-            const float e0 = m.x * d0, e1 = m.y * d1, e2 = m.z * d2, e3 = m.w * d3;
-            in1[p] += (e0 + e1) + (e2 + e3);
-            in2[p] = fmaf(e0, d0, fmaf(e1, d1, fmaf(e2, d2, fmaf(e3, d3, in2[p]))));
-          } else {
-            in1[p] += (d0 + d1) + (d2 + d3);
-            in2[p] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, in2[p]))));
-          }
-        }
-      } else {
-        const float4 y = feat[NF - 1][q];
-#pragma unroll
-        for (int p = 0; p < kBcastP; ++p) {
-          in1[p] = fmaf(x.x, ca[p], fmaf(x.y, ca[p], fmaf(x.z, ca[p], fmaf(x.w, ca[p], in1[p]))));
-          in1[p] = fmaf(y.x, cb[p], fmaf(y.y, cb[p], fmaf(y.z, cb[p], fmaf(y.w, cb[p], in1[p]))));
-        }
+      for (int j = 0; j < 8; ++j) {
+        xs[j] = feat[0][q0 + 8 * h + j];
+        ys[j] = NF > 1 ? feat[NF - 1][q0 + 8 * h + j] : xs[j];
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) quad(xs[j], ys[j], in1, in2, true);
+    }
+#pragma unroll
+    for (int p = 0; p < kBcastP; ++p) {
+      acc1[p] += (double)in1[p];
+      acc2[p] += (double)in2[p];
+    }
+  }
+  {
+    float in1[kBcastP], in2[kBcastP];
+#pragma unroll
+    for (int p = 0; p < kBcastP; ++p) in1[p] = in2[p] = 0.0f;
+    for (int q = full; q < nq; ++q) {
+      const float4 x = feat[0][q];
+      const float4 y = NF > 1 ? feat[NF - 1][q] : x;
+      quad(x, y, in1, in2, false);
     }
 #pragma unroll
     for (int p = 0; p < kBcastP; ++p) {
@@ -513,29 +467,54 @@ struct FinalizeArgs {
   double scale[MI_MAX_SITES];
 };
 
-__global__ __launch_bounds__(256) void k_finalize(const float* __restrict__ part, int64_t nseg,
-                                                  int64_t K, const FinalizeArgs A,
-                                                  float* __restrict__ total,
-                                                  double* __restrict__ site_lp,
-                                                  float* __restrict__ slot_grad) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
+// One block per 64 particles; its 1024 threads split the segments 16 ways (fixed assignment), each
+// sums its share in fp64 with independent loads in flight, then the 16 shares are combined in a
+// fixed order through LDS -- deterministic, and ~16x the memory-level parallelism of a thread-per-
+// particle loop.
+constexpr int kFinK = 64;
+constexpr int kFinG = 16;
+
+__global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restrict__ part,
+                                                           int64_t nseg, int64_t K,
+                                                           const FinalizeArgs A,
+                                                           float* __restrict__ total,
+                                                           double* __restrict__ site_lp,
+                                                           float* __restrict__ slot_grad) {
+  __shared__ double red[kFinG][kFinK];
+  const int kl = threadIdx.x % kFinK;
+  const int gl = threadIdx.x / kFinK;
+  const int64_t k = (int64_t)blockIdx.x * kFinK + kl;
+  const int64_t kc = k < K ? k : K - 1;
   double t = 0.0;
-  for (int s = 0; s < A.num_sites; ++s) {
-    double acc = 0.0;
-    const float* p = part + (int64_t)s * nseg * K + k;
-    for (int64_t g = 0; g < nseg; ++g) acc += (double)p[g * K];
-    acc *= A.scale[s];
-    if (site_lp != nullptr) site_lp[(int64_t)s * K + k] = acc;
-    t += acc;
+  const int nv = A.num_sites + A.num_slots;
+  for (int v = 0; v < nv; ++v) {
+    const float* p = part + (int64_t)v * nseg * K + kc;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int64_t g = gl;
+    for (; g + 3 * kFinG < nseg; g += 4 * kFinG) {
+      a0 += (double)p[g * K];
+      a1 += (double)p[(g + kFinG) * K];
+      a2 += (double)p[(g + 2 * kFinG) * K];
+      a3 += (double)p[(g + 3 * kFinG) * K];
+    }
+    for (; g < nseg; g += kFinG) a0 += (double)p[g * K];
+    __syncthreads();
+    red[gl][kl] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (gl == 0 && k < K) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < kFinG; ++j) acc += red[j][kl];
+      if (v < A.num_sites) {
+        acc *= A.scale[v];
+        if (site_lp != nullptr) site_lp[(int64_t)v * K + k] = acc;
+        t += acc;
+      } else {
+        slot_grad[(int64_t)(v - A.num_sites) * K + k] = (float)acc;
+      }
+    }
   }
-  total[k] = (float)t;
-  for (int j = 0; j < A.num_slots; ++j) {
-    double acc = 0.0;
-    const float* p = part + (int64_t)(A.num_sites + j) * nseg * K + k;
-    for (int64_t g = 0; g < nseg; ++g) acc += (double)p[g * K];
-    slot_grad[(int64_t)j * K + k] = (float)acc;
-  }
+  if (gl == 0 && k < K) total[k] = (float)t;
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -610,7 +589,8 @@ namespace {
 
 enum Shape { kRow = 0, kCol = 1, kBcast = 2 };
 
-constexpr int kRowElems = 16;
+constexpr int kRowElems = 8;
+constexpr int kColUnroll = 4;
 constexpr int64_t kTargetBlocks = 2048;
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -704,6 +684,16 @@ Plan make_plan(const mi_group* g) {
   return p;
 }
 
+PlanInfo plan_info(const Plan& p) {
+  PlanInfo info{};
+  info.row = p.shape == kRow;
+  info.elems = p.shape == kRow ? kRowElems : kColUnroll;
+  info.kw = p.kw;
+  info.grid_x = p.grid.x;
+  info.grid_y = p.grid.y;
+  return info;
+}
+
 size_t partial_bytes(const mi_group* g, const Plan& p) {
   const int nv = g->num_sites + g->num_slots;
   return (size_t)nv * (size_t)p.nseg * (size_t)g->K * sizeof(float);
@@ -725,6 +715,14 @@ int mi_abi_version(char* target, size_t target_bytes) {
   return MI_ABI_VERSION;
 }
 
+int mi_struct_sizes(size_t* operand, size_t* site, size_t* group) {
+  if (operand == nullptr || site == nullptr || group == nullptr) return MI_EINVAL;
+  *operand = sizeof(mi_operand);
+  *site = sizeof(mi_site);
+  *group = sizeof(mi_group);
+  return 0;
+}
+
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
   if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -734,6 +732,13 @@ int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
 
 int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,
                      double* site_lp, float* slot_grad, uint32_t* flags, void* stream) {
+  return mi_group_forward_timed(group, workspace, workspace_bytes, total, site_lp, slot_grad, flags,
+                                nullptr, nullptr, stream);
+}
+
+int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
+                           float* total, double* site_lp, float* slot_grad, uint32_t* flags,
+                           void* start_event, void* stop_event, void* stream) {
   if (!validate_group(group) || total == nullptr || flags == nullptr) return MI_EINVAL;
   if (group->num_slots > 0 && slot_grad == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -743,6 +748,10 @@ int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_by
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
   if (e != hipSuccess) return to_code(e);
   const mi_group G = *group;
+  if (start_event != nullptr) {
+    e = hipEventRecord(static_cast<hipEvent_t>(start_event), s);
+    if (e != hipSuccess) return to_code(e);
+  }
   switch (p.shape) {
     case kBcast: {
       const bool masked = G.sites[0].mask != nullptr;
@@ -766,23 +775,64 @@ int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_by
       break;
     }
     case kRow:
-      hipLaunchKernelGGL((mi::k_group_row<kRowElems>), p.grid, dim3(256), 0, s, G, part, p.nseg,
-                         p.rows_per_block, flags);
+    case kCol: {
+      const PlanInfo info = plan_info(p);
+      const int rc = mi_jit_launch(G, info, part, p.nseg,
+                                   p.shape == kRow ? p.rows_per_block : p.seg_len, flags, s);
+      if (rc < 0) return -rc;
+      if (rc == 0) break;
+      if (p.shape == kRow)
+        hipLaunchKernelGGL((mi::k_group_row<kRowElems>), p.grid, dim3(256), 0, s, G, part, p.nseg,
+                           p.rows_per_block, flags);
+      else
+        hipLaunchKernelGGL(mi::k_group_col, p.grid, dim3(256), 0, s, G, part, p.nseg, p.seg_len,
+                           p.kw, flags);
       break;
-    case kCol:
-      hipLaunchKernelGGL(mi::k_group_col, p.grid, dim3(256), 0, s, G, part, p.nseg, p.seg_len,
-                         p.kw, flags);
-      break;
+    }
   }
   e = hipGetLastError();
   if (e != hipSuccess) return to_code(e);
+  if (stop_event != nullptr) {
+    e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s);
+    if (e != hipSuccess) return to_code(e);
+  }
   mi::FinalizeArgs A{};
   A.num_sites = G.num_sites;
   A.num_slots = G.num_slots;
   for (int i = 0; i < G.num_sites; ++i) A.scale[i] = G.sites[i].scale;
-  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, 256)), dim3(256), 0, s, part,
-                     p.nseg, G.K, A, total, site_lp, slot_grad);
+  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK)),
+                     dim3(mi::kFinK * mi::kFinG), 0, s, part, p.nseg, G.K, A, total, site_lp,
+                     slot_grad);
   return to_code(hipGetLastError());
+}
+
+int mi_group_source(const mi_group* group, char* out, size_t out_bytes, size_t* needed) {
+  if (!validate_group(group)) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  std::string text;
+  if (p.shape == kBcast) text = "// BCAST shape: precompiled k_site_bcast\n";
+  else text = mi_jit_source(*group, plan_info(p));
+  if (needed != nullptr) *needed = text.size() + 1;
+  if (out != nullptr && out_bytes > 0) {
+    const size_t n = std::min(out_bytes - 1, text.size());
+    std::memcpy(out, text.data(), n);
+    out[n] = '\0';
+  }
+  return 0;
+}
+
+int mi_group_compile_check(const mi_group* group, char* log, size_t log_bytes) {
+  if (!validate_group(group)) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  if (p.shape == kBcast) return 0;
+  std::string text;
+  const bool ok = mi_jit_compile_check(*group, plan_info(p), &text);
+  if (log != nullptr && log_bytes > 0) {
+    const size_t n = std::min(log_bytes - 1, text.size());
+    std::memcpy(log, text.data(), n);
+    log[n] = '\0';
+  }
+  return ok ? 0 : MI_EUNSUPPORTED;
 }
 
 int mi_scale_rows(float* x, int64_t stride_k, int64_t stride_i, int64_t K, int64_t N,

@@ -28,6 +28,11 @@ from . import _native as nat
 from .particles import ParticleTrace, SiteRecord
 
 
+# Optional instrumentation (bench.py): an object with `pair(launcher) -> (start, stop)` returning
+# torch.cuda.Event pairs (already created) that mi_group_forward_timed records around the main site
+# kernel of each launch.
+KERNEL_TIMER = None
+
 FAMILY_CODES = {
     "normal": nat.NORMAL,
     "bernoulli_logits": nat.BERNOULLI_LOGITS,
@@ -178,7 +183,11 @@ class _GroupLauncher:
     def inputs(self) -> List[torch.Tensor]:
         return [op.view.tensor for op in self.operands]
 
-    def run(self, compute_grads: bool):
+    def describe(self, compute_grads: bool):
+        """
+        The ctypes ``mi_group`` descriptor of this group plus freshly allocated dense gradient
+        buffers (one per DENSE operand, None otherwise).
+        """
         device = self.device
         K, N = self.K, self.N
         group = nat.Group()
@@ -219,6 +228,37 @@ class _GroupLauncher:
                 desc.mask = mask.tensor.data_ptr()
                 desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
             desc.scale = site.scale
+        return group, grads
+
+    def source(self) -> str:
+        """
+        The specialised kernel source the library generates for this group (diagnostics).
+        """
+        group, _ = self.describe(True)
+        needed = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_group_source(ctypes.byref(group), None, 0, ctypes.byref(needed)),
+                  "mi_group_source")
+        buf = ctypes.create_string_buffer(needed.value)
+        nat.check(lib.mi_group_source(ctypes.byref(group), buf, needed.value, None),
+                  "mi_group_source")
+        return buf.value.decode()
+
+    def compile_check(self, compute_grads: bool = True) -> str:
+        """
+        Compile the specialised kernel with hiprtc (no device needed); raises with the log.
+        """
+        group, _ = self.describe(compute_grads)
+        log = ctypes.create_string_buffer(1 << 16)
+        code = nat.lib().mi_group_compile_check(ctypes.byref(group), log, len(log))
+        if code != 0:
+            raise nat.NativeError("site program failed to compile:\n" + log.value.decode())
+        return log.value.decode()
+
+    def run(self, compute_grads: bool):
+        device = self.device
+        K, N = self.K, self.N
+        group, grads = self.describe(compute_grads)
         size = ctypes.c_size_t()
         lib = nat.lib()
         nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
@@ -228,10 +268,14 @@ class _GroupLauncher:
         site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device)
         slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
         flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
-        nat.check(lib.mi_group_forward(ctypes.byref(group), workspace.data_ptr(), size.value,
-                                       total.data_ptr(), site_lp.data_ptr(), slot_grad.data_ptr(),
-                                       flags.data_ptr(), nat.stream_handle(device)),
-                  "mi_group_forward")
+        start = stop = None
+        if KERNEL_TIMER is not None:
+            start, stop = KERNEL_TIMER.pair(self)
+        nat.check(lib.mi_group_forward_timed(
+            ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
+            site_lp.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(),
+            None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
+            nat.stream_handle(device)), "mi_group_forward_timed")
         return total, site_lp, grads, slot_grad, flags
 
 
@@ -354,14 +398,14 @@ class LogJoint:
             cursor += 1
 
 
-def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint:
+def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
     """
-    Launch the site kernels for every recorded site and return the per-particle log joint.
+    Prepare every recorded site for launch: categorical sites as (site, logits, value, mask) and
+    the other families packed into site groups sharing their element space and a dense operand.
     """
     K = trace.K
     groups: List[Tuple[torch.Size, _GroupLauncher]] = []
-    totals: List[torch.Tensor] = []
-    pending: List[Tuple[str, dict, List[SiteRecord]]] = []
+    categorical = []
     for site in trace.sites:
         if site.family == "categorical":
             logits, value = (_to_device(t, K, device, f"site '{site.name}'", False)[0]
@@ -375,9 +419,7 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
             val = _collapse(value.to(torch.int64), K, shape).tensor.expand(K, N)
             mask = None if site.mask is None else site.mask.to(device).bool().expand(shape) \
                 .reshape(1, N).expand(K, N)
-            holder: dict = {}
-            totals.append(_CategoricalFn.apply(site, holder, g0, lg, val, mask))
-            pending.append(("categorical", holder, [site]))
+            categorical.append((site, lg, val, mask))
             continue
         shape = site.site_shape
         N = int(shape.numel())
@@ -388,22 +430,36 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
                                          allow_constant=not is_value)
             views.append(_View(None, 0, 0, constant) if constant is not None
                          else _collapse(moved, K, shape))
-        tensors = views
         mask = None
         if site.mask is not None:
             flat_mask = site.mask.to(device).bool().expand(shape).reshape(N)
             mask = _View(flat_mask, 0, flat_mask.stride(0) if N > 1 else 1)
         placed = False
         for group_shape, launcher in groups:
-            if group_shape == shape and launcher.shares_dense_operand(tensors) and \
-                    launcher.try_add(site, tensors, mask):
+            if group_shape == shape and launcher.shares_dense_operand(views) and \
+                    launcher.try_add(site, views, mask):
                 placed = True
                 break
         if not placed:
             launcher = _GroupLauncher(K, N, g0, device)
-            launcher.try_add(site, tensors, mask)
+            launcher.try_add(site, views, mask)
             groups.append((shape, launcher))
-    for _, launcher in groups:
+    return [launcher for _, launcher in groups], categorical
+
+
+def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint:
+    """
+    Launch the site kernels for every recorded site and return the per-particle log joint.
+    """
+    K = trace.K
+    launchers, categorical = plan_groups(trace, g0, device)
+    totals: List[torch.Tensor] = []
+    pending: List[Tuple[str, dict, List[SiteRecord]]] = []
+    for site, lg, val, mask in categorical:
+        holder: dict = {}
+        totals.append(_CategoricalFn.apply(site, holder, g0, lg, val, mask))
+        pending.append(("categorical", holder, [site]))
+    for launcher in launchers:
         holder = {}
         totals.append(_SiteGroupFn.apply(launcher, holder, *launcher.inputs()))
         pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
@@ -414,5 +470,5 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
         for extra in totals[1:]:
             total = total + extra
     else:
-        total = torch.zeros(K)
+        total = torch.zeros(K, device=device)
     return LogJoint(total=total, pending=pending, checks=trace.checks)

@@ -1,0 +1,363 @@
+"""
+Behavioural spec of the probabilistic-program layer (reference tests/test_core.py), written against
+mininf_amd: contexts, state, conditioning, validation messages, values, batching, masking.
+"""
+import logging
+
+import numpy as np
+import pytest
+import torch
+from torch.distributions import constraints, Gamma, LKJCholesky, Normal, Uniform
+
+import mininf_amd as mi
+from mininf_amd import core
+
+
+# ---- singleton contexts (core.py:19-83) ------------------------------------------------------
+
+def test_context_without_key_is_rejected():
+    with pytest.raises(RuntimeError, match="must define"):
+        with core.SingletonContextMixin():
+            pass
+
+
+def test_second_state_cannot_activate():
+    with mi.State():
+        with pytest.raises(RuntimeError, match="is already active."):
+            with mi.State():
+                pass
+
+
+def test_state_cannot_reactivate_itself():
+    with mi.State() as outer:
+        with pytest.raises(RuntimeError, match="Cannot reactivate"):
+            with outer:
+                pass
+
+
+def test_exit_errors():
+    with pytest.raises(RuntimeError, match="no context is active."):
+        with mi.State():
+            del mi.State.INSTANCES["state"]
+    impostor = mi.State({"a": 3})
+    with pytest.raises(RuntimeError, match="comprising {'a': <class 'int'>}> is active."):
+        with mi.State():
+            mi.State.INSTANCES["state"] = impostor
+    assert mi.State.INSTANCES.pop("state") is impostor
+
+
+def test_get_instance_semantics():
+    assert mi.State.get_instance() is None
+    with pytest.raises(KeyError, match="context is active."):
+        mi.State.get_instance(True)
+    with mi.State() as state:
+        assert mi.State.get_instance() is state
+
+    class Squatter(core.SingletonContextMixin):
+        SINGLETON_KEY = "state"
+
+    with Squatter(), pytest.raises(TypeError, match="is not an instance of."):
+        mi.State.get_instance()
+
+
+def test_reprs_do_not_fail():
+    assert "LogProbTracer" in repr(core.LogProbTracer())
+    assert "comprising" in repr(mi.State(x=torch.zeros(2)))
+
+
+# ---- tracing and log probabilities (core.py:192-277) ----------------------------------------
+
+def test_log_prob_tracer_matches_distribution():
+    dist = Uniform(0, 2)
+
+    def model():
+        mi.sample("x", dist, (7, 8))
+
+    with mi.State() as state:
+        model()
+        with core.LogProbTracer() as lp:
+            model()
+    np.testing.assert_allclose(lp["x"][0], dist.log_prob(state["x"]))
+    assert lp.total.ndim == 0
+    torch.testing.assert_close(lp.total, dist.log_prob(state["x"]).sum())
+
+
+def test_missing_and_non_tensor_values():
+    with mi.State() as state, core.LogProbTracer():
+        with pytest.raises(ValueError, match="'a' is missing."):
+            mi.sample("a", None)
+        state["a"] = "not a tensor"
+        with pytest.raises(TypeError, match="Expected a tensor"):
+            mi.sample("a", None)
+
+
+def test_event_shaped_values_trace():
+    dist = LKJCholesky(9, 4)
+    with mi.State(x=dist.sample((7, 8))) as state, core.LogProbTracer() as lp:
+        mi.sample("x", dist, (7, 8))
+    assert state["x"].shape == (7, 8, 9, 9)
+    assert torch.isfinite(lp.total)
+
+
+def test_condition_and_precedence():
+    def model():
+        x = mi.sample("x", Uniform(0, 1))
+        mi.sample("y", Gamma(2, 2), 3)
+        return x
+
+    fixed = mi.condition(model, x=0.3)
+    with mi.State() as a:
+        fixed()
+    with mi.State() as b:
+        fixed()
+    np.testing.assert_allclose(a["x"], 0.3)
+    np.testing.assert_allclose(b["x"], 0.3)
+    assert (a["y"] - b["y"]).abs().min() > 1e-12
+    with mi.State() as free:
+        model()
+    assert abs(free["x"] - 0.3) > 1e-6
+    assert mi.condition(model, x=0.25)() == 0.25
+    assert mi.condition(model, {"x": 0.1})() == 0.1
+    assert mi.condition(model, {"x": 0.1}, x=0.7)() == 0.7
+
+
+@pytest.mark.parametrize("value, error, message", [
+    ("foo", TypeError, "Expected a tensor"),
+    (LKJCholesky(2, 4).sample(), ValueError, "Expected shape"),
+    (LKJCholesky(2, 4).sample((5, 6)), ValueError, "Expected shape"),
+    (torch.randn(5, 7, 2, 2), ValueError, "is not in the support"),
+])
+def test_parameter_validation_messages(value, error, message):
+    def model():
+        mi.sample("x", LKJCholesky(2, 4), (5, 7))
+
+    with pytest.raises(error, match=message):
+        mi.condition(model, x=value)()
+
+
+def test_validation_can_be_disabled():
+    with mi.State() as state, core.SampleTracer(_validate_parameters=False):
+        mi.condition(lambda: mi.sample("x", LKJCholesky(2, 4), (5, 7)), x="foo")()
+        assert state["x"] == "foo"
+
+
+def test_with_active_state_injects_or_creates():
+    @core.with_active_state
+    def current(state):
+        return state
+
+    mine = mi.State()
+    assert current() is not None and current() is not mine
+    with mine:
+        assert current() is mine
+
+
+def test_duplicate_site_raises():
+    def twice():
+        mi.sample("x", Normal(0, 1))
+        mi.sample("x", Normal(0, 1))
+
+    with mi.State():
+        twice()
+        with pytest.raises(RuntimeError, match="call `sample` twice"), core.LogProbTracer():
+            twice()
+
+
+def test_state_subset_keeps_objects():
+    state = mi.State({"a": torch.randn(3), "b": torch.randn(4), "c": torch.rand(7)})
+    part = state.subset("a", "b")
+    assert set(part) == {"a", "b"} and all(part[k] is state[k] for k in part)
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_conditioning_twice(strict):
+    def model():
+        return mi.sample("x", Normal(0, 1))
+
+    inner = mi.condition(model, x=0.1, _strict=strict)
+    assert inner() == 0.1
+    outer = mi.condition(inner, x=0.7)
+    if strict:
+        with pytest.raises(ValueError, match="Cannot update"):
+            outer()
+    else:
+        assert outer() == 0.1
+
+
+# ---- masked values (core.py:231-239, 262-265) ------------------------------------------------
+
+def test_masked_log_prob_and_support():
+    dist = Gamma(2, 2)
+    with mi.State() as state:
+        mi.sample("x", dist, (7, 8))
+    original = state["x"].clone()
+    mask = torch.rand(7, 8) < 0.5
+    state["x"] = torch.masked.as_masked_tensor(torch.where(mask, original, -9), mask)
+    with state, core.LogProbTracer() as lp:
+        mi.sample("x", dist, (7, 8))
+    expected = dist.log_prob(original)
+    assert (lp["x"][0].data[mask] == expected[mask]).all()
+    torch.testing.assert_close(lp.total, expected[mask].sum())
+
+    state["x"] = torch.masked.as_masked_tensor(torch.where(mask, -9, original), mask)
+    with state, pytest.raises(ValueError, match="is not in the support GreaterThanEq"), \
+            core.LogProbTracer(_validate_parameters=False):
+        mi.sample("x", dist, (7, 8))
+
+
+def test_masked_gradients_flow():
+    x = torch.randn(100, requires_grad=True)
+    with mi.State(x=torch.masked.as_masked_tensor(x, torch.randn(100) < 0)), \
+            core.LogProbTracer() as lp:
+        mi.sample("x", Normal(0, 1), [100])
+    assert lp.total.grad_fn and torch.isfinite(lp.total)
+    lp.total.backward()
+    assert x.grad is not None
+
+
+# ---- values (core.py:390-492) ----------------------------------------------------------------
+
+def test_value_without_default():
+    def model():
+        return mi.value("x")
+
+    with pytest.raises(ValueError, match="No default value given."):
+        model()
+    assert mi.condition(model, x=3)() == 3
+    with pytest.raises(ValueError, match=r"Expected shape \(\) for parameter"):
+        mi.condition(model, x=torch.randn(3))()
+
+
+def test_value_with_shape_and_default():
+    with pytest.raises(ValueError, match="No default value given."):
+        mi.value("x", shape=(3, 4))
+    x = torch.randn(3, 4)
+    torch.testing.assert_close(mi.condition(lambda: mi.value("x", shape=(3, 4)), x=x)(), x)
+    default = torch.randn(5, 7)
+    torch.testing.assert_close(mi.value("x", value=default), default)
+    other = torch.randn(5, 7)
+    torch.testing.assert_close(mi.condition(lambda: mi.value("x", value=default), x=other)(),
+                               other)
+
+
+@pytest.mark.parametrize("scalar", [3, 3.2])
+def test_value_scalar_default_is_tensor(scalar):
+    out = mi.value("x", scalar)
+    assert torch.is_tensor(out) and out == scalar
+
+
+def test_values_do_not_contribute():
+    with mi.State(x=torch.randn(3, 4)), core.LogProbTracer() as lp:
+        mi.value("x", torch.randn(3, 4))
+    assert "x" not in lp and lp.total == 0
+
+
+def test_value_support():
+    with pytest.raises(ValueError, match="is not in the specified support"):
+        core.Value(-3, support=constraints.nonnegative)
+    with pytest.raises(ValueError, match=r"is not in the support of Value\(support=GreaterThanEq"):
+        mi.condition(lambda: mi.value("x", support=constraints.nonnegative), x=-2)()
+
+
+@pytest.mark.parametrize("tracer", [core.SampleTracer, core.LogProbTracer])
+def test_value_shape_validation(tracer):
+    with tracer(), mi.State(x=torch.arange(3)), \
+            pytest.raises(ValueError, match=r"Expected shape \(5,\)"):
+        mi.value("x", shape=5)
+
+
+# ---- batches of states (core.py:495-584) -----------------------------------------------------
+
+def test_broadcast_samples():
+    def model():
+        a = mi.value("a")
+        x = mi.sample("x", Normal(0, 1))
+        assert x.shape == ()
+        mi.value("y", x + a)
+
+    x = torch.randn(7)
+    out = mi.broadcast_samples(mi.condition(model, a=1.3), x=x)
+    torch.testing.assert_close(out["y"], x + 1.3)
+
+
+def test_batch_size_consistency():
+    assert core._assert_same_batch_size({"a": torch.randn(5), "b": torch.randn(5, 7)}) == 5
+    with pytest.raises(ValueError, match="Inconsistent batch sizes"):
+        core._assert_same_batch_size({"a": torch.randn(5), "b": torch.randn(7, 5)})
+    with pytest.raises(ValueError, match="state is empty"):
+        core._assert_same_batch_size({})
+
+
+def test_transpose_round_trip():
+    states = {"a": torch.randn(5), "b": torch.randn(5, 7, 8)}
+    rows = core.transpose_states(states)
+    assert len(rows) == 5
+    back = core.transpose_states(rows)
+    assert set(back) == set(states)
+    for key in states:
+        torch.testing.assert_close(back[key], states[key])
+
+
+# ---- minibatch scaling (core.py:587-622, 267-271) -------------------------------------------
+
+@pytest.mark.parametrize("declared, observed, factor", [
+    (14, (7, 9), 2.0), ((14, 9), (14, 1), 9.0), ((14, 9), (2, 3), 21.0),
+])
+def test_batch_scaling(declared, observed, factor):
+    dist = Normal(0, 1)
+    x = dist.sample(observed)
+    with mi.State(x=x), core.LogProbTracer() as lp:
+        with mi.batch(declared):
+            mi.sample("x", dist, (14, 9))
+    torch.testing.assert_close(lp["x"][0], dist.log_prob(x))
+    torch.testing.assert_close(lp.total, dist.log_prob(x).sum() * factor)
+
+
+def test_batch_oversize_warns_and_errors(caplog):
+    dist = Normal(0, 1)
+    x = dist.sample([15, 9])
+    with caplog.at_level(logging.WARNING), mi.State(x=x), core.LogProbTracer() as lp:
+        with mi.batch((14, 9)):
+            mi.sample("x", dist, (14, 9))
+    torch.testing.assert_close(lp.total, dist.log_prob(x).sum() * 14 / 15)
+    assert "exceeds expected batch shape" in caplog.messages[0]
+    with mi.State(x=x), pytest.raises(ValueError, match="has more dimensions"), \
+            core.LogProbTracer(), mi.batch([7, 9, 2]):
+        mi.sample("x", dist, (14, 9))
+    with mi.State(x=torch.masked.as_masked_tensor(x, x > 0)), core.LogProbTracer() as lp, \
+            pytest.raises(ValueError, match="not supported for masked data"):
+        with mi.batch([7]):
+            mi.sample("x", dist, (14, 9))
+        lp.total
+
+
+def test_adaptive_batch_with_index():
+    def model():
+        n = mi.value("n")
+        with mi.batch(n):
+            i = mi.value("i", shape=n)
+            x = mi.sample("x", Normal(torch.ones(n), 1))
+            mi.sample("y", Normal(x[i], 1))
+
+    n = 7
+    x, i = torch.randn(n), torch.as_tensor([2, 3, 6])
+    y = torch.randn(n) + x
+    with mi.State(n=n, x=x, y=y[i], i=i), core.LogProbTracer() as lp:
+        model()
+    torch.testing.assert_close(lp.contribution("x"), Normal(1, 1).log_prob(x).sum())
+    torch.testing.assert_close(lp.contribution("y"),
+                               Normal(x[i], 1).log_prob(y[i]).sum() * n / i.numel())
+
+
+def test_no_log_prob_skips_sites():
+    def model():
+        a = mi.sample("a", Normal(0, 1), (3, 4))
+        with mi.no_log_prob():
+            b = mi.sample("b", Gamma(2, 2), (4, 5))
+        return a @ b
+
+    with mi.State():
+        first = model()
+        with core.LogProbTracer() as lp:
+            torch.testing.assert_close(model(), first)
+    assert "b" not in lp and "a" in lp
