@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 import mininf_amd  # noqa: E402
 from mininf_amd import engine  # noqa: E402
 from mininf_amd.distributed import all_reduce_gradients  # noqa: E402
+from mininf_amd.graph import StepGraph  # noqa: E402
 from torch.distributions import Bernoulli, Beta, Normal  # noqa: E402
 
 METRIC = "site-log_prob evals/sec + ELBO step wall-time, 1/2/4/8 MI355X"
@@ -83,7 +84,7 @@ def workload(name, device, world, rank):
         return dict(
             desc=f"{name.upper()} Beta-Bernoulli (README model), n={n}, {k_local} particles/GPU",
             k_local=k_local, n=n, module=guide, guide=lambda: {"theta": guide()},
-            conditioned=lambda step: conditioned, evals=k_local * (n + 1), lr=0.02,
+            conditioned=lambda: conditioned, evals=k_local * (n + 1), lr=0.02,
             dominant_N=n, bound="valu", flops_per_eval=2.0, bytes_per_eval=0.0,
             data=f"synthetic: x ~ Bernoulli(0.7)[{n}] fp32 (seed 0); Beta(2,2) guide init")
     if name in ("c3", "c4"):
@@ -108,11 +109,23 @@ def workload(name, device, world, rank):
             Normal, loc=1e-3 * torch.randn(p, generator=gen),
             scale=(1e-3 * torch.randn(p, generator=gen)).exp()).to(device)
         blocks = n_total // n_obs
+        if n_obs == n_total:
+            static = mininf_amd.condition(model, X=X, y=y)
 
-        def conditioned(step):
-            # Device-resident minibatch: a contiguous window (no host DataLoader, no copy).
-            start = ((step * 7919) % blocks) * n_obs
-            return mininf_amd.condition(model, X=X[start:start + n_obs], y=y[start:start + n_obs])
+            def conditioned():
+                return static
+        else:
+            # Device-resident minibatches (replaces the host DataLoader of examples/minibatch.md:78):
+            # a device counter picks the window, rows are gathered on the device, so a captured
+            # step draws a new minibatch on every replay.
+            counter = torch.zeros(1, dtype=torch.int64, device=device)
+            offsets = torch.arange(n_obs, device=device)
+
+            def conditioned():
+                rows = (counter * 7919) % blocks * n_obs + offsets
+                counter.add_(1)
+                return mininf_amd.condition(model, X=X.index_select(0, rows),
+                                            y=y.index_select(0, rows))
 
         return dict(
             desc=(f"{name.upper()} Bayesian linear regression, {n_total}x{p} (minibatch {n_obs}), "
@@ -147,7 +160,7 @@ def workload(name, device, world, rank):
         return dict(
             desc=f"C5 masked hierarchical model, n={n}, {k_local} particles/GPU",
             k_local=k_local, n=n, module=guide, guide=lambda: guide(),
-            conditioned=lambda step: conditioned,
+            conditioned=lambda: conditioned,
             evals=k_local * (1 + n + 2 * observed), lr=0.01, dominant_N=n, bound="hbm",
             flops_per_eval=0.0, bytes_per_eval=None, observed=observed,
             data=f"synthetic: y ~ N(z, 0.5), b ~ Bernoulli(logits=z), 20% masked (seed 0)")
@@ -176,10 +189,10 @@ def cpu_baseline(name, budget_s=12.0):
     optimizer = torch.optim.Adam(w["module"].parameters(), lr=w["lr"])
     steps = 0
     evals_per_particle = w["evals"] / w["k_local"]
-    cpu_port.k_particle_step(w["conditioned"](0), w["guide"], optimizer, 1)   # warm-up
+    cpu_port.k_particle_step(w["conditioned"](), w["guide"], optimizer, 1)   # warm-up
     start = time.perf_counter()
     while True:
-        cpu_port.k_particle_step(w["conditioned"](steps), w["guide"], optimizer, k_cpu)
+        cpu_port.k_particle_step(w["conditioned"](), w["guide"], optimizer, k_cpu)
         steps += 1
         elapsed = time.perf_counter() - start
         if elapsed > budget_s or steps >= 200:
@@ -206,7 +219,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="launch every step from Python instead of replaying a captured hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-host", action="store_true",
+                    help="cProfile 20 extra steps and print the hottest host functions to stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,24 +239,25 @@ def main():
 
     w = workload(args.config, device, world, rank)
     module = w["module"]
-    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"])
+    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True)
     loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(
         num_particles=w["k_local"] * world, seed=1, validate=not args.no_validate,
         process_group=group)
     timer = EventTimer()
     engine.KERNEL_TIMER = timer
 
-    def step(i):
-        optimizer.zero_grad()
-        loss = loss_fn(w["conditioned"](i), w["guide"]())
+    def forward_backward():
+        optimizer.zero_grad(set_to_none=True)
+        loss = loss_fn(w["conditioned"](), w["guide"]())
         loss.backward()
-        if world > 1:
-            all_reduce_gradients(module.parameters(), group)
-        optimizer.step()
+        if world == 1:
+            optimizer.step()
         return loss
 
-    for i in range(args.warmup):
-        step(i)
+    def finish_step():
+        if world > 1:
+            all_reduce_gradients(module.parameters(), group)
+            optimizer.step()
 
     def barrier():
         if world > 1:
@@ -247,19 +265,59 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
+    def timed(run, steps):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = run()
+        barrier()
+        seconds = time.perf_counter() - t0
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([seconds], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            seconds = float(t)
+        return seconds, out
+
+    def eager_step():
+        loss = forward_backward()
+        finish_step()
+        return loss
+
+    # Eager steps: every kernel launched from Python (the kernel timing comes from these).
+    for _ in range(args.warmup):
+        eager_step()
     timer.active = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(args.warmup + i)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    eager_steps = max(3, args.steps // 3) if args.graph else args.steps
+    eager_elapsed, loss = timed(eager_step, eager_steps)
     timer.active = False
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    eager_ms = 1e3 * eager_elapsed / eager_steps
+    elapsed, mode = eager_elapsed * args.steps / eager_steps, "eager"
+    if args.graph:
+        # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
+        captured = StepGraph(forward_backward, warmup=2)
+
+        def graph_step():
+            out = captured()
+            finish_step()
+            return out
+
+        for _ in range(args.warmup):
+            graph_step()
+        elapsed, loss = timed(graph_step, args.steps)
+        captured.check()
+        mode = "hipGraph replay"
+
+    if args.profile_host and rank == 0:
+        import cProfile
+        import pstats
+        profiler = cProfile.Profile()
+        profiler.enable()
+        for i in range(20):
+            eager_step()
+        torch.cuda.synchronize()
+        profiler.disable()
+        pstats.Stats(profiler, stream=sys.stderr).sort_stats("tottime").print_stats(30)
 
     ms = 1e3 * elapsed / args.steps
     value = w["evals"] * world * args.steps / elapsed
@@ -293,7 +351,8 @@ def main():
                    "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
                    "parallelism": f"particle-sharded x{world}" + (" + RCCL grad all-reduce"
                                                                   if world > 1 else ""),
-                   "validate": not args.no_validate, "final_loss": float(loss.detach())},
+                   "validate": not args.no_validate, "final_loss": float(loss.detach()),
+                   "step_mode": mode, "eager_ms_per_step": eager_ms},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

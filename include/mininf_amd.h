@@ -158,17 +158,20 @@ int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
 /* Counter-based Philox-4x32-10 normals: eps[k, i] is a function of (seed, step, stream_id,
  * particle_offset + k, i) only, so the union of draws is independent of how particles are sharded
  * across GPUs. z[k, i] = loc[i] + eps[k, i] * scale[i] (normal.py:83-86). If `eps` is non-NULL it is
- * used instead of the generator (parity mode: injected host noise, row-major [K, N]). */
+ * used instead of the generator (parity mode: injected host noise, row-major [K, N]).
+ * The effective step is `step + *step_device` when `step_device` (a device uint64) is non-NULL, so
+ * a captured HIP graph advances the generator by incrementing that word on the device. */
 int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
-                      int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
-                      int64_t particle_offset, const float* eps, float* z, void* stream);
+                      int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                      const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                      const float* eps, float* z, void* stream);
 
 /* Backward of mi_normal_rsample: dloc[i] = sum_k dz[k,i], dscale[i] = sum_k dz[k,i] * eps[k,i]
  * with eps regenerated from the counter (or read from `eps`). */
 int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
 int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
                                int64_t K, int64_t N, uint64_t seed, uint64_t step,
-                               uint32_t stream_id, int64_t particle_offset, const float* eps,
+                               const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset, const float* eps,
                                void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
                                void* stream);
 
@@ -176,7 +179,8 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
  * variates from the same counter-based generator (beta.py:85-86, dirichlet.py:23-36, 85-88). With
  * `x_in` non-NULL the draws are copied from it instead (parity mode). */
 int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t c0_stride,
-                    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
+                    int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                    const uint64_t* step_device, uint32_t stream_id,
                     int64_t particle_offset, const float* x_in, float* x, void* stream);
 
 /* Implicit reparameterisation gradient of the Beta draws (dirichlet.py:17-20 ->

@@ -81,16 +81,17 @@ _SIGNATURES = {
                                               ctypes.c_float, c_vp, c_vp, ctypes.c_size_t, c_vp,
                                               c_vp, c_vp]),
     "mi_normal_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
-                                         ctypes.c_uint64, ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                         ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                          c_vp]),
     "mi_normal_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_normal_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64,
-                                                  ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_uint64, c_vp,
                                                   ctypes.c_uint32, c_i64, c_vp, c_vp,
                                                   ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "mi_beta_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
-                                       ctypes.c_uint64, ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp]),
+                                       ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                       c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,

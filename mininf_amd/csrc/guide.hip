@@ -22,8 +22,10 @@ constexpr int kGuideThreads = 256;
 // -------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
     const float* __restrict__ loc, int64_t loc_s, const float* __restrict__ scale, int64_t scale_s,
-    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff,
-    const float* __restrict__ eps_in, float* __restrict__ z, int64_t rows_per_block) {
+    int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
+    uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in, float* __restrict__ z,
+    int64_t rows_per_block) {
+  if (step_dev != nullptr) step += *step_dev;
   const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   const int64_t i0 = quad * 4;
   if (i0 >= N) return;
@@ -64,9 +66,10 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
 // particles; per-block sums are combined in a fixed order through LDS and written per slice.
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
     const float* __restrict__ dz, int64_t dz_sk, int64_t dz_si, int64_t K, int64_t N,
-    uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in,
-    float* __restrict__ out_loc, float* __restrict__ out_scale, int64_t out_stride,
-    int64_t rows_per_block, int ti) {
+    uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev, uint32_t stream_id,
+    int64_t poff, const float* __restrict__ eps_in, float* __restrict__ out_loc,
+    float* __restrict__ out_scale, int64_t out_stride, int64_t rows_per_block, int ti) {
+  if (step_dev != nullptr) step += *step_dev;
   __shared__ float red[kGuideThreads][8];
   const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kGuideThreads / ti;
   const int64_t quad = (int64_t)blockIdx.x * ti + tx;
@@ -197,8 +200,8 @@ MI_DEV float sample_gamma(float alpha, Stream& rng) {
 
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
     const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
-    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id, int64_t poff,
-    const float* __restrict__ x_in, float* __restrict__ x) {
+    int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
+    uint32_t stream_id, int64_t poff, const float* __restrict__ x_in, float* __restrict__ x) {
   const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   if (t >= K * N) return;
   const int64_t k = t / N, i = t - k * N;
@@ -206,6 +209,7 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
     x[t] = x_in[t];
     return;
   }
+  if (step_dev != nullptr) step += *step_dev;
   Stream ra{seed, step, stream_id, 0u, (uint64_t)i, (uint64_t)(poff + k)};
   Stream rb{seed, step, stream_id, 1u, (uint64_t)i, (uint64_t)(poff + k)};
   const float g1 = sample_gamma(c1[i * c1_s], ra);
@@ -420,8 +424,9 @@ BwdGeometry bwd_geometry(int64_t K, int64_t units) {
 extern "C" {
 
 int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
-                      int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
-                      int64_t particle_offset, const float* eps, float* z, void* stream) {
+                      int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                      const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                      const float* eps, float* z, void* stream) {
   if (loc == nullptr || scale == nullptr || z == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
     return MI_EINVAL;
   const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
@@ -429,7 +434,8 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
   const int64_t rows = ceil_div(K, gy);
   hipLaunchKernelGGL(mi::k_normal_rsample, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
-                     scale, scale_stride, K, N, seed, step, stream_id, particle_offset, eps, z, rows);
+                     scale, scale_stride, K, N, seed, step, step_device, stream_id, particle_offset,
+                     eps, z, rows);
   return to_code(hipGetLastError());
 }
 
@@ -442,7 +448,8 @@ int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* byt
 
 int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
                                int64_t K, int64_t N, uint64_t seed, uint64_t step,
-                               uint32_t stream_id, int64_t particle_offset, const float* eps,
+                               const uint64_t* step_device, uint32_t stream_id,
+                               int64_t particle_offset, const float* eps,
                                void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
                                void* stream) {
   if (dz == nullptr || dloc == nullptr || dscale == nullptr || K < 1 || N < 1) return MI_EINVAL;
@@ -460,7 +467,8 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
   }
   hipLaunchKernelGGL(mi::k_normal_rsample_bwd, dim3((unsigned)gx, (unsigned)gy),
                      dim3(mi::kGuideThreads), 0, s, dz, dz_stride_k, dz_stride_i, K, N, seed, step,
-                     stream_id, particle_offset, eps, out_loc, out_scale, N, rows, geo.ti);
+                     step_device, stream_id, particle_offset, eps, out_loc, out_scale, N, rows,
+                     geo.ti);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
@@ -470,13 +478,15 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
 }
 
 int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t c0_stride,
-                    int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
-                    int64_t particle_offset, const float* x_in, float* x, void* stream) {
+                    int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                    const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                    const float* x_in, float* x, void* stream) {
   if (c1 == nullptr || c0 == nullptr || x == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
     return MI_EINVAL;
   hipLaunchKernelGGL(mi::k_beta_rsample, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), c1, c1_stride,
-                     c0, c0_stride, K, N, seed, step, stream_id, particle_offset, x_in, x);
+                     c0, c0_stride, K, N, seed, step, step_device, stream_id, particle_offset, x_in,
+                     x);
   return to_code(hipGetLastError());
 }
 

@@ -65,16 +65,24 @@ struct Signature {
   std::string text;
 };
 
-std::string operand_var(const mi_group& g, int o, bool row_layout) {
-  const Kind k = kind_of(g.operands[o].stride_k, g.operands[o].stride_i);
-  std::ostringstream s;
-  switch (k) {
-    case kBroadcast: s << "b" << o; break;
-    case kShared: s << (row_layout ? "s" : "sv") << o << (row_layout ? "[e]" : ""); break;
-    case kParticle: s << "p" << o; break;
-    default: s << "d" << o; break;
+// Per-element values are arrays indexed by `e` (ROW: the lane's E elements of a row segment;
+// COL: E unrolled element iterations); per-particle values are scalars.
+std::string operand_var(const mi_group& g, int o) {
+  switch (kind_of(g.operands[o].stride_k, g.operands[o].stride_i)) {
+    case kBroadcast: return "b" + std::to_string(o);
+    case kShared: return "s" + std::to_string(o) + "[e]";
+    case kParticle: return "p" + std::to_string(o);
+    default: return "d" + std::to_string(o) + "[e]";
   }
-  return s.str();
+}
+
+std::string mask_var(const mi_site& st, int s) {
+  switch (kind_of(st.mask_stride_k, st.mask_stride_i)) {
+    case kBroadcast: return "m" + std::to_string(s);
+    case kShared: return "m" + std::to_string(s) + "[e]";
+    case kParticle: return "mp" + std::to_string(s);
+    default: return "md" + std::to_string(s) + "[e]";
+  }
 }
 
 std::string mask_kind_tag(const mi_site& st) {
@@ -84,7 +92,8 @@ std::string mask_kind_tag(const mi_site& st) {
 
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
-  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << "|" << g.num_operands << ":";
+  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "|"
+    << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
     s << (int)kind_of(op.stride_k, op.stride_i) << (g.compute_grads ? op.grad_mode : 0)
@@ -102,38 +111,26 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
 
 // ---- source generation ----------------------------------------------------------------------
 
-void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, bool row_layout,
-                    const char* valid) {
+void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, const std::string& valid,
+                    const char* in) {
   const mi_site& st = g.sites[s];
   std::string r[3];
   for (int q = 0; q < 3; ++q) {
-    if (!role_used(st.family, q)) {
-      r[q] = "0.0f";
-    } else if (st.operand[q] < 0) {
-      r[q] = "c" + std::to_string(s) + "_" + std::to_string(q);
-    } else {
-      r[q] = operand_var(g, st.operand[q], row_layout);
-    }
+    if (!role_used(st.family, q)) r[q] = "0.0f";
+    else if (st.operand[q] < 0) r[q] = "c" + std::to_string(s) + "_" + std::to_string(q);
+    else r[q] = operand_var(g, st.operand[q]);
   }
-  o << "        {\n          mi::Elem el;\n";
+  o << in << "{\n" << in << "  mi::Elem el;\n";
   if (st.family == MI_BERNOULLI_LOGITS || st.family == MI_BERNOULLI_PROBS)
-    o << "          mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[2] << ", el);\n";
+    o << in << "  mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[2] << ", el);\n";
   else
-    o << "          mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[1] << ", " << r[2]
+    o << in << "  mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[1] << ", " << r[2]
       << ", el);\n";
   std::string obs = valid;
-  if (st.mask != nullptr) {
-    const Kind mk = kind_of(st.mask_stride_k, st.mask_stride_i);
-    std::string m;
-    if (mk == kBroadcast) m = "m" + std::to_string(s);
-    else if (mk == kShared) m = row_layout ? "m" + std::to_string(s) + "[e]" : "mv" + std::to_string(s);
-    else if (mk == kParticle) m = "mp" + std::to_string(s);
-    else m = "md" + std::to_string(s);
-    obs = "(" + obs + " && " + m + ")";
-  }
-  o << "          const bool obs = " << obs << ";\n";
-  o << "          lp" << s << " += obs ? el.lp : 0.0f;\n";
-  o << "          fl" << s << " |= (el.param_bad ? " << MI_FLAG_PARAM
+  if (st.mask != nullptr) obs = "(" + obs + " && " + mask_var(st, s) + ")";
+  o << in << "  const bool obs = " << obs << ";\n";
+  o << in << "  lp" << s << " += obs ? el.lp : 0.0f;\n";
+  o << in << "  fl" << s << " |= (el.param_bad ? " << MI_FLAG_PARAM
     << "u : 0u) | ((obs && el.support_bad) ? " << MI_FLAG_SUPPORT << "u : 0u);\n";
   if (g.compute_grads) {
     bool any = false;
@@ -141,24 +138,33 @@ void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, bool row_la
       const int op = st.operand[q];
       if (op >= 0 && role_used(st.family, q) && g.operands[op].grad_mode != MI_GRAD_NONE) any = true;
     }
-    if (any) o << "          const float w = obs ? scale" << s << " : 0.0f;\n";
+    if (any) o << in << "  const float w = obs ? scale" << s << " : 0.0f;\n";
     for (int q = 0; q < 3; ++q) {
       const int op = st.operand[q];
       if (op < 0 || !role_used(st.family, q)) continue;
       if (g.operands[op].grad_mode == MI_GRAD_DENSE)
-        o << "          g" << op << " = fmaf(w, el.d[" << q << "], g" << op << ");\n";
+        o << in << "  g" << op << "[e] = fmaf(w, el.d[" << q << "], g" << op << "[e]);\n";
       else if (g.operands[op].grad_mode == MI_GRAD_PARTICLE)
-        o << "          sl" << g.operands[op].slot << " = fmaf(w, el.d[" << q << "], sl"
+        o << in << "  sl" << g.operands[op].slot << " = fmaf(w, el.d[" << q << "], sl"
           << g.operands[op].slot << ");\n";
     }
   }
-  o << "        }\n";
+  o << in << "}\n";
 }
 
 std::string generate(const mi_group& g, const PlanInfo& plan) {
   const bool row = plan.row;
   const int E = plan.elems;
+  const std::string Es = std::to_string(E);
+  const int nsite_values = plan.combined ? 1 : g.num_sites;
+  const int nv = nsite_values + (g.compute_grads ? g.num_slots : 0);
   std::ostringstream o;
+  auto is = [&](int op, Kind k) { return kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == k; };
+  auto mask_is = [&](int s, Kind k) {
+    return g.sites[s].mask != nullptr && kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == k;
+  };
+  auto dense_grad = [&](int op) { return g.compute_grads && g.operands[op].grad_mode == MI_GRAD_DENSE; };
+
   o << "#include \"device_math.hpp\"\n";
   o << "extern \"C\" __global__ __launch_bounds__(256) void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
@@ -172,68 +178,82 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       if (g.sites[s].operand[q] < 0 && role_used(g.sites[s].family, q))
         o << "  const float c" << s << "_" << q << " = G.sites[" << s << "].constant[" << q << "];\n";
   }
-  // Pointers and strides as locals (scalar registers).
   for (int op = 0; op < g.num_operands; ++op) {
     o << "  const float* __restrict__ x" << op << " = G.operands[" << op << "].data;\n";
     o << "  const long sk" << op << " = G.operands[" << op << "].stride_k, si" << op
       << " = G.operands[" << op << "].stride_i;\n";
-    if (g.compute_grads && g.operands[op].grad_mode == MI_GRAD_DENSE) {
+    if (dense_grad(op)) {
       o << "  float* __restrict__ gx" << op << " = G.operands[" << op << "].grad;\n";
       o << "  const long gsk" << op << " = G.operands[" << op << "].grad_stride_k, gsi" << op
         << " = G.operands[" << op << "].grad_stride_i;\n";
     }
-    if (kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == kBroadcast)
-      o << "  const float b" << op << " = x" << op << "[0];\n";
+    if (is(op, kBroadcast)) o << "  const float b" << op << " = x" << op << "[0];\n";
   }
   for (int s = 0; s < g.num_sites; ++s) {
     if (g.sites[s].mask == nullptr) continue;
     o << "  const unsigned char* __restrict__ mk" << s << " = G.sites[" << s << "].mask;\n";
     o << "  const long msk" << s << " = G.sites[" << s << "].mask_stride_k, msi" << s
       << " = G.sites[" << s << "].mask_stride_i;\n";
-    if (kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == kBroadcast)
-      o << "  const bool m" << s << " = mk" << s << "[0] != 0;\n";
+    if (mask_is(s, kBroadcast)) o << "  const bool m" << s << " = mk" << s << "[0] != 0;\n";
   }
-  const int nv = g.num_sites + (g.compute_grads ? g.num_slots : 0);
-  auto zero_accumulators = [&](const char* indent) {
-    for (int s = 0; s < g.num_sites; ++s) o << indent << "float lp" << s << " = 0.0f;\n";
-    if (g.compute_grads)
-      for (int j = 0; j < g.num_slots; ++j) o << indent << "float sl" << j << " = 0.0f;\n";
-  };
-  auto value_name = [&](int v) {
-    return v < g.num_sites ? "lp" + std::to_string(v) : "sl" + std::to_string(v - g.num_sites);
-  };
-  auto dense_loads = [&](const char* indent, const char* kexpr, const char* iexpr) {
-    for (int op = 0; op < g.num_operands; ++op)
-      if (kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == kDense)
-        o << indent << "const float d" << op << " = x" << op << "[" << kexpr << " * sk" << op
-          << " + " << iexpr << " * si" << op << "];\n";
-    for (int s = 0; s < g.num_sites; ++s) {
-      if (g.sites[s].mask == nullptr) continue;
-      if (kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == kDense)
-        o << indent << "const bool md" << s << " = mk" << s << "[" << kexpr << " * msk" << s
-          << " + " << iexpr << " * msi" << s << "] != 0;\n";
+  auto value_expr = [&](int v) -> std::string {
+    if (v < nsite_values) {
+      if (!plan.combined) return "lp" + std::to_string(v);
+      std::string e;
+      for (int s = 0; s < g.num_sites; ++s)
+        e += (s ? " + " : "") + std::string("scale") + std::to_string(s) + " * lp" + std::to_string(s);
+      return "(" + e + ")";
     }
+    return "sl" + std::to_string(v - nsite_values);
+  };
+  auto zero_accumulators = [&](const char* in) {
+    for (int s = 0; s < g.num_sites; ++s) o << in << "float lp" << s << " = 0.0f;\n";
     if (g.compute_grads)
-      for (int op = 0; op < g.num_operands; ++op)
-        if (g.operands[op].grad_mode == MI_GRAD_DENSE) o << indent << "float g" << op << " = 0.0f;\n";
+      for (int j = 0; j < g.num_slots; ++j) o << in << "float sl" << j << " = 0.0f;\n";
   };
-  auto dense_stores = [&](const char* indent, const char* guard, const char* kexpr,
-                          const char* iexpr) {
-    if (!g.compute_grads) return;
+  auto particle_loads = [&](const char* in, const char* kexpr) {
     for (int op = 0; op < g.num_operands; ++op)
-      if (g.operands[op].grad_mode == MI_GRAD_DENSE)
-        o << indent << "if (" << guard << ") gx" << op << "[" << kexpr << " * gsk" << op << " + "
-          << iexpr << " * gsi" << op << "] = G.grad_scale * g" << op << ";\n";
-  };
-  auto particle_loads = [&](const char* indent, const char* kexpr) {
-    for (int op = 0; op < g.num_operands; ++op)
-      if (kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == kParticle)
-        o << indent << "const float p" << op << " = x" << op << "[" << kexpr << " * sk" << op << "];\n";
+      if (is(op, kParticle))
+        o << in << "const float p" << op << " = x" << op << "[" << kexpr << " * sk" << op << "];\n";
     for (int s = 0; s < g.num_sites; ++s)
-      if (g.sites[s].mask != nullptr &&
-          kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == kParticle)
-        o << indent << "const bool mp" << s << " = mk" << s << "[" << kexpr << " * msk" << s
-          << "] != 0;\n";
+      if (mask_is(s, kParticle))
+        o << in << "const bool mp" << s << " = mk" << s << "[" << kexpr << " * msk" << s << "] != 0;\n";
+  };
+  // Dense (particle x element) loads of one row / chunk into arrays `prefix`<op>[e].
+  auto dense_loads = [&](const char* in, const char* prefix, const std::string& kexpr,
+                         const char* iexpr) {
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kDense))
+        o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << Es << "; ++e) " << prefix
+          << op << "[e] = x" << op << "[" << kexpr << " * sk" << op << " + " << iexpr << " * si"
+          << op << "];\n";
+    for (int s = 0; s < g.num_sites; ++s)
+      if (mask_is(s, kDense))
+        o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << Es << "; ++e) " << prefix
+          << "m" << s << "[e] = mk" << s << "[" << kexpr << " * msk" << s << " + " << iexpr
+          << " * msi" << s << "] != 0;\n";
+  };
+  auto compute_and_store = [&](const char* in, const std::string& valid, const char* kexpr,
+                               const char* iexpr) {
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << in << "float g" << op << "[" << Es << "];\n";
+    o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << Es << "; ++e) {\n";
+    const std::string inner = std::string(in) + "  ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
+    for (int s = 0; s < g.num_sites; ++s) emit_site_eval(o, g, s, valid, inner.c_str());
+    o << in << "}\n";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op))
+        o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << Es << "; ++e) if ("
+          << valid << ") gx" << op << "[" << kexpr << " * gsk" << op << " + " << iexpr << " * gsi"
+          << op << "] = G.grad_scale * g" << op << "[e];\n";
+  };
+  auto declare_dense = [&](const char* in, const char* prefix) {
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kDense)) o << in << "float " << prefix << op << "[" << Es << "];\n";
+    for (int s = 0; s < g.num_sites; ++s)
+      if (mask_is(s, kDense)) o << in << "bool " << prefix << "m" << s << "[" << Es << "];\n";
   };
 
   if (row) {
@@ -244,36 +264,46 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << "    long idx[" << E << "]; bool ok[" << E << "];\n";
     o << "#pragma unroll\n    for (int e = 0; e < " << E << "; ++e) { const long i = base + e * 64 + lane; "
          "ok[e] = i < N; idx[e] = ok[e] ? i : N - 1; }\n";
-    // shared (per-element, particle-independent) operands and masks: loaded once per thread
     for (int op = 0; op < g.num_operands; ++op)
-      if (kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == kShared)
+      if (is(op, kShared))
         o << "    float s" << op << "[" << E << "];\n#pragma unroll\n    for (int e = 0; e < " << E
           << "; ++e) s" << op << "[e] = x" << op << "[idx[e] * si" << op << "];\n";
     for (int s = 0; s < g.num_sites; ++s)
-      if (g.sites[s].mask != nullptr &&
-          kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == kShared)
+      if (mask_is(s, kShared))
         o << "    bool m" << s << "[" << E << "];\n#pragma unroll\n    for (int e = 0; e < " << E
           << "; ++e) m" << s << "[e] = mk" << s << "[idx[e] * msi" << s << "] != 0;\n";
-    o << "    for (long kb = k_begin; kb < k_end; kb += 64) {\n";
-    for (int v = 0; v < nv; ++v) o << "      float keep" << v << " = 0.0f;\n";
-    o << "      const int rows = (int)min(64L, k_end - kb);\n";
-    o << "      for (int r = 0; r < rows; ++r) {\n";
-    o << "        const long k = kb + r;\n";
-    particle_loads("        ", "k");
-    zero_accumulators("        ");
-    o << "#pragma unroll\n        for (int e = 0; e < " << E << "; ++e) {\n";
-    o << "          const long i = idx[e];\n";
-    dense_loads("          ", "k", "i");
-    for (int s = 0; s < g.num_sites; ++s) emit_site_eval(o, g, s, true, "ok[e]");
-    dense_stores("          ", "ok[e]", "k", "i");
-    o << "        }\n";
-    for (int v = 0; v < nv; ++v)
-      o << "        { const float t = mi::wave_sum(" << value_name(v) << "); keep" << v
-        << " = (lane == r) ? t : keep" << v << "; }\n";
+    // software pipeline: the next row's dense values are in flight while this row computes
+    declare_dense("    ", "n");
+    o << "    if (k_begin < k_end) {\n";
+    dense_loads("      ", "n", "k_begin", "idx[e]");
+    o << "    }\n";
+    for (int v = 0; v < nv; ++v) o << "    float keep" << v << " = 0.0f;\n";
+    o << "    for (long k = k_begin; k < k_end; ++k) {\n";
+    o << "      const int r = (int)((k - k_begin) & 63);\n";
+    declare_dense("      ", "d");
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kDense))
+        o << "#pragma unroll\n      for (int e = 0; e < " << E << "; ++e) d" << op << "[e] = n" << op
+          << "[e];\n";
+    for (int s = 0; s < g.num_sites; ++s)
+      if (mask_is(s, kDense))
+        o << "#pragma unroll\n      for (int e = 0; e < " << E << "; ++e) dm" << s << "[e] = nm" << s
+          << "[e];\n";
+    o << "      if (k + 1 < k_end) {\n";
+    dense_loads("        ", "n", "(k + 1)", "idx[e]");
     o << "      }\n";
-    o << "      if (lane < rows) {\n";
+    particle_loads("      ", "k");
+    zero_accumulators("      ");
+    compute_and_store("      ", "ok[e]", "k", "idx[e]");
     for (int v = 0; v < nv; ++v)
-      o << "        part[((long)" << v << " * nseg + seg) * K + kb + lane] = keep" << v << ";\n";
+      o << "      { const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
+        << " = (lane == r) ? t : keep" << v << "; }\n";
+    o << "      if (r == 63 || k + 1 == k_end) {\n";
+    o << "        if (lane <= r) {\n";
+    for (int v = 0; v < nv; ++v)
+      o << "          part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
+    o << "        }\n";
+    for (int v = 0; v < nv; ++v) o << "        keep" << v << " = 0.0f;\n";
     o << "      }\n    }\n  }\n";
   } else {
     const int kw = plan.kw;
@@ -288,31 +318,42 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     particle_loads("    ", "kc");
     o << "    const long i_begin = seg * arg;\n";
     o << "    const long i_end = min(N, i_begin + arg);\n";
-    o << "#pragma unroll " << E << "\n";
-    o << "    for (long i = i_begin + isub; i < i_end; i += " << istep << ") {\n";
+    o << "    for (long i0 = i_begin + isub; i0 < i_end; i0 += " << E * istep << ") {\n";
+    o << "      long ii[" << E << "]; bool okv[" << E << "];\n";
+    o << "#pragma unroll\n      for (int e = 0; e < " << E << "; ++e) { const long i = i0 + e * "
+      << istep << "; okv[e] = kok && i < i_end; ii[e] = i < i_end ? i : i_end - 1; }\n";
     for (int op = 0; op < g.num_operands; ++op)
-      if (kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == kShared)
-        o << "      const float sv" << op << " = x" << op << "[i * si" << op << "];\n";
+      if (is(op, kShared))
+        o << "      float s" << op << "[" << E << "];\n#pragma unroll\n      for (int e = 0; e < " << E
+          << "; ++e) s" << op << "[e] = x" << op << "[ii[e] * si" << op << "];\n";
     for (int s = 0; s < g.num_sites; ++s)
-      if (g.sites[s].mask != nullptr &&
-          kind_of(g.sites[s].mask_stride_k, g.sites[s].mask_stride_i) == kShared)
-        o << "      const bool mv" << s << " = mk" << s << "[i * msi" << s << "] != 0;\n";
-    dense_loads("      ", "kc", "i");
-    for (int s = 0; s < g.num_sites; ++s) emit_site_eval(o, g, s, false, "kok");
-    dense_stores("      ", "kok", "kc", "i");
+      if (mask_is(s, kShared))
+        o << "      bool m" << s << "[" << E << "];\n#pragma unroll\n      for (int e = 0; e < " << E
+          << "; ++e) m" << s << "[e] = mk" << s << "[ii[e] * msi" << s << "] != 0;\n";
+    declare_dense("      ", "d");
+    dense_loads("      ", "d", "kc", "ii[e]");
+    compute_and_store("      ", "okv[e]", "kc", "ii[e]");
     o << "    }\n  }\n";
-    if (kw < 64)
-      for (int v = 0; v < nv; ++v)
-        o << "  " << value_name(v) << " = mi::wave_sum_strided(" << value_name(v) << ", " << kw
-          << ");\n";
+    std::vector<std::string> finals;
+    for (int v = 0; v < nv; ++v) {
+      o << "  float fin" << v << " = " << value_expr(v) << ";\n";
+      if (kw < 64) o << "  fin" << v << " = mi::wave_sum_strided(fin" << v << ", " << kw << ");\n";
+    }
     o << "  if (seg < nseg && kok && isub == 0) {\n";
     for (int v = 0; v < nv; ++v)
-      o << "    part[((long)" << v << " * nseg + seg) * K + k] = " << value_name(v) << ";\n";
+      o << "    part[((long)" << v << " * nseg + seg) * K + k] = fin" << v << ";\n";
     o << "  }\n";
   }
+  // dense masks use the names "dm<s>" inside rows; map mask_var's "md<s>[e]" onto them
   for (int s = 0; s < g.num_sites; ++s) o << "  mi::publish_flags(flags + " << s << ", fl" << s << ");\n";
   o << "}\n";
-  return o.str();
+  std::string text = o.str();
+  for (int s = 0; s < g.num_sites; ++s) {
+    const std::string from = "md" + std::to_string(s) + "[e]", to = "dm" + std::to_string(s) + "[e]";
+    for (size_t at = text.find(from); at != std::string::npos; at = text.find(from, at + to.size()))
+      text.replace(at, from.size(), to);
+  }
+  return text;
 }
 
 // ---- compile cache ---------------------------------------------------------------------------

@@ -11,6 +11,7 @@ struct PlanInfo {
   bool row;        // lanes along elements (true) or along particles (false)
   int elems;       // ROW: elements per lane per row; COL: unroll of the element loop
   int kw;          // COL: lanes per element group (power of two <= 64)
+  bool combined;   // reduce one weighted log-joint value per particle instead of one per site
   unsigned grid_x;
   unsigned grid_y;
 };

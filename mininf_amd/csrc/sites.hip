@@ -684,8 +684,9 @@ Plan make_plan(const mi_group* g) {
   return p;
 }
 
-PlanInfo plan_info(const Plan& p) {
+PlanInfo plan_info(const Plan& p, bool combined) {
   PlanInfo info{};
+  info.combined = combined;
   info.row = p.shape == kRow;
   info.elems = p.shape == kRow ? kRowElems : kColUnroll;
   info.kw = p.kw;
@@ -748,6 +749,11 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
   if (e != hipSuccess) return to_code(e);
   const mi_group G = *group;
+  // Without a per-site output the specialised kernels reduce one weighted log-joint value per
+  // particle instead of one per site.
+  const bool combined = site_lp == nullptr;
+  int reduced_lp = G.num_sites;
+  bool prescaled = false;  // partials already carry the site scales
   if (start_event != nullptr) {
     e = hipEventRecord(static_cast<hipEvent_t>(start_event), s);
     if (e != hipSuccess) return to_code(e);
@@ -776,11 +782,15 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
     }
     case kRow:
     case kCol: {
-      const PlanInfo info = plan_info(p);
+      const PlanInfo info = plan_info(p, combined);
       const int rc = mi_jit_launch(G, info, part, p.nseg,
                                    p.shape == kRow ? p.rows_per_block : p.seg_len, flags, s);
       if (rc < 0) return -rc;
-      if (rc == 0) break;
+      if (rc == 0) {
+        prescaled = combined;
+        reduced_lp = combined ? 1 : G.num_sites;
+        break;
+      }
       if (p.shape == kRow)
         hipLaunchKernelGGL((mi::k_group_row<kRowElems>), p.grid, dim3(256), 0, s, G, part, p.nseg,
                            p.rows_per_block, flags);
@@ -797,9 +807,9 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
     if (e != hipSuccess) return to_code(e);
   }
   mi::FinalizeArgs A{};
-  A.num_sites = G.num_sites;
+  A.num_sites = reduced_lp;
   A.num_slots = G.num_slots;
-  for (int i = 0; i < G.num_sites; ++i) A.scale[i] = G.sites[i].scale;
+  for (int i = 0; i < reduced_lp; ++i) A.scale[i] = prescaled ? 1.0 : G.sites[i].scale;
   hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK)),
                      dim3(mi::kFinK * mi::kFinG), 0, s, part, p.nseg, G.K, A, total, site_lp,
                      slot_grad);
@@ -811,7 +821,7 @@ int mi_group_source(const mi_group* group, char* out, size_t out_bytes, size_t* 
   const Plan p = make_plan(group);
   std::string text;
   if (p.shape == kBcast) text = "// BCAST shape: precompiled k_site_bcast\n";
-  else text = mi_jit_source(*group, plan_info(p));
+  else text = mi_jit_source(*group, plan_info(p, true));
   if (needed != nullptr) *needed = text.size() + 1;
   if (out != nullptr && out_bytes > 0) {
     const size_t n = std::min(out_bytes - 1, text.size());
@@ -826,7 +836,8 @@ int mi_group_compile_check(const mi_group* group, char* log, size_t log_bytes) {
   const Plan p = make_plan(group);
   if (p.shape == kBcast) return 0;
   std::string text;
-  const bool ok = mi_jit_compile_check(*group, plan_info(p), &text);
+  const bool ok = mi_jit_compile_check(*group, plan_info(p, true), &text) &&
+                  mi_jit_compile_check(*group, plan_info(p, false), &text);
   if (log != nullptr && log_bytes > 0) {
     const size_t n = std::min(log_bytes - 1, text.size());
     std::memcpy(log, text.data(), n);

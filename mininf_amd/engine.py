@@ -25,6 +25,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import _native as nat
+from . import particles
 from .particles import ParticleTrace, SiteRecord
 
 
@@ -139,8 +140,10 @@ class _GroupLauncher:
     """
     Owns the ctypes descriptor of one site group and launches ``mi_group_forward``.
     """
-    def __init__(self, K: int, N: int, g0: float, device: torch.device) -> None:
+    def __init__(self, K: int, N: int, g0: float, device: torch.device,
+                 per_site: bool = False) -> None:
         self.K, self.N, self.g0, self.device = K, N, g0, device
+        self.per_site = per_site  # also return each site's log density per particle (diagnostics)
         self.operands: List[_Operand] = []
         self.keys: Dict[Tuple, int] = {}
         self.sites: List[Tuple[SiteRecord, List[int], Optional[torch.Tensor]]] = []
@@ -265,7 +268,8 @@ class _GroupLauncher:
                   "mi_group_workspace_bytes")
         workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
         total = torch.empty(K, dtype=torch.float32, device=device)
-        site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device)
+        site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device) \
+            if self.per_site else None
         slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
         flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
         start = stop = None
@@ -273,7 +277,7 @@ class _GroupLauncher:
             start, stop = KERNEL_TIMER.pair(self)
         nat.check(lib.mi_group_forward_timed(
             ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
-            site_lp.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(),
+            nat.ptr(site_lp), slot_grad.data_ptr(), flags.data_ptr(),
             None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
             nat.stream_handle(device)), "mi_group_forward_timed")
         return total, site_lp, grads, slot_grad, flags
@@ -367,23 +371,30 @@ class LogJoint:
     pending: List[Tuple[str, dict, List[SiteRecord]]]
     checks: list
 
-    def raise_on_violation(self) -> None:
+    def flag_vector(self) -> Optional[torch.Tensor]:
         """
-        One host synchronisation for all validation flags of the step; raises the reference's
-        errors (core.py:186-188 for values, torch validate_args for parameters).
+        All validation results of the step as one int64 device vector: one MI_FLAG_* word per
+        kernel-evaluated site, then one 0/1 per deferred support / constraint check.
         """
         parts = []
         for _, holder, _ in self.pending:
             parts.append(holder["flags"].reshape(-1).to(torch.int64))
         for _, ok in self.checks:
             parts.append((~ok.reshape(-1).bool()).any().reshape(1).to(torch.int64))
-        if not parts:
-            return
-        flat = torch.cat(parts).cpu().tolist()
+        return torch.cat(parts) if parts else None
+
+    def flag_count(self) -> int:
+        return sum(len(sites) for _, _, sites in self.pending) + len(self.checks)
+
+    def raise_from(self, values) -> None:
+        """
+        Raise the reference's errors (core.py:186-188 for values, torch validate_args for
+        parameters) from host copies of :meth:`flag_vector`.
+        """
         cursor = 0
         for kind, holder, sites in self.pending:
             for site in sites:
-                bits = flat[cursor]
+                bits = int(values[cursor])
                 cursor += 1
                 if bits & nat.FLAG_PARAM:
                     raise ValueError(f"Expected parameters of distribution {site.description} for "
@@ -393,9 +404,20 @@ class LogJoint:
                     raise ValueError(f"Parameter '{site.name}' is not in the support of "
                                      f"{site.description}.")
         for check, _ in self.checks:
-            if flat[cursor]:
+            if int(values[cursor]):
                 raise ValueError(check.message)
             cursor += 1
+        for check, _ in self.checks:
+            if check.memo is not None:
+                particles.memo_commit(check.memo)
+
+    def raise_on_violation(self) -> None:
+        """
+        One host synchronisation for all validation flags of the step.
+        """
+        vector = self.flag_vector()
+        if vector is not None:
+            self.raise_from(vector.cpu().tolist())
 
 
 def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):

@@ -1,0 +1,171 @@
+"""
+HIP-graph capture of a whole ELBO training step.
+
+Every kernel of a step -- guide sampling, the site kernels, the finalize reductions, torch's own
+elementwise ops for the guide transforms and entropy, autograd's backward and the optimizer update
+-- is recorded once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and replayed, so a step
+costs one graph launch instead of ~100 Python-dispatched kernel launches. This is the MI355X
+substitute for a tracing compiler: the model is still traced by running its unchanged Python code
+(during warm-up and capture); replays re-execute the recorded device work on the same buffers.
+
+What makes the ELBO capturable:
+
+* the guide generator reads its step counter from device memory (``mi_*_rsample`` ``step_device``),
+  and the loss increments that word on the device, so every replay draws fresh particles;
+* inside :func:`graph_safe` the engine does not synchronise to raise validation errors: the
+  per-site flag words are gathered on the device by the graph, copied to pinned host memory after
+  each replay, and checked once that replay has finished (:meth:`StepGraph.check`, or non-blockingly before the next
+  replay) -- errors are raised with the reference's messages, at most one step late;
+* ``torch.distributions`` argument validation (a host sync per check) is off inside the captured
+  region; the site kernels' MI_FLAG_PARAM checks cover the model's parameters;
+* while capturing, ``torch.distributions``' ``broadcast_all`` turns Python numbers into device
+  tensors with a fill kernel instead of a host-to-device copy (which a capturing stream forbids).
+
+Conditioned data must keep its storage across replays (the graph records addresses), and the
+optimizer must be created with ``capturable=True`` when its step is part of the graph.
+"""
+from __future__ import annotations
+
+import contextlib
+import sys
+import threading
+from numbers import Number
+from typing import Callable, List, Optional
+
+import torch
+from torch.distributions import Distribution
+from torch.distributions import utils as distribution_utils
+from torch.overrides import is_tensor_like
+
+_STATE = threading.local()
+_ORIGINAL_BROADCAST_ALL = distribution_utils.broadcast_all
+
+
+def _capture_safe_broadcast_all(*values):
+    """
+    torch.distributions.utils.broadcast_all with Python numbers materialised by a device fill
+    (``torch.full``) instead of a host-to-device copy (``torch.tensor(v, device=...)``), which a
+    capturing stream does not permit -- e.g. the ``1`` of ``Normal(X @ theta, 1)``.
+    """
+    if not all(is_tensor_like(v) or isinstance(v, Number) for v in values):
+        return _ORIGINAL_BROADCAST_ALL(*values)
+    if all(is_tensor_like(v) for v in values):
+        return torch.broadcast_tensors(*values)
+    options = dict(dtype=torch.get_default_dtype())
+    for value in values:
+        if isinstance(value, torch.Tensor):
+            options = dict(dtype=value.dtype, device=value.device)
+            break
+    return torch.broadcast_tensors(*[v if is_tensor_like(v) else torch.full((), v, **options)
+                                     for v in values])
+
+
+@contextlib.contextmanager
+def _capture_safe_distributions():
+    patched = []
+    for name, module in list(sys.modules.items()):
+        if name.startswith("torch.distributions") and \
+                getattr(module, "broadcast_all", None) is _ORIGINAL_BROADCAST_ALL:
+            module.broadcast_all = _capture_safe_broadcast_all
+            patched.append(module)
+    try:
+        yield
+    finally:
+        for module in patched:
+            module.broadcast_all = _ORIGINAL_BROADCAST_ALL
+
+
+def deferred() -> Optional[list]:
+    """
+    The collector of deferred validations while a step is being warmed up or captured.
+    """
+    return getattr(_STATE, "collector", None)
+
+
+@contextlib.contextmanager
+def graph_safe(collector: list):
+    """
+    Run model code without host synchronisation: validation results are appended to `collector`
+    instead of being checked, and torch.distributions argument validation is disabled.
+    """
+    previous = Distribution._validate_args
+    Distribution.set_default_validate_args(False)
+    _STATE.collector = collector
+    try:
+        yield
+    finally:
+        _STATE.collector = None
+        Distribution.set_default_validate_args(previous)
+
+
+class StepGraph:
+    """
+    Capture ``step()`` (any callable running one training step on the current device) and replay
+    it. ``__call__`` returns the captured step's output tensors (updated in place by each replay).
+
+    Args:
+        step: The training step. It should call ``optimizer.zero_grad(set_to_none=True)`` first so
+            that gradient buffers are allocated inside the graph's memory pool.
+        warmup: Eager warm-up iterations on a side stream before capture (compiles the specialised
+            site programs, fills caches, initialises library handles).
+    """
+    def __init__(self, step: Callable[[], object], warmup: int = 3) -> None:
+        self.step = step
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                collector: List = []
+                with graph_safe(collector):
+                    step()
+                for joint in collector:
+                    joint.raise_on_violation()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+
+        self.graph = torch.cuda.CUDAGraph()
+        self._joints: List = []
+        with graph_safe(self._joints), _capture_safe_distributions(), \
+                torch.cuda.graph(self.graph):
+            self.output = step()
+            flags = [joint.flag_vector() for joint in self._joints]
+            flags = [f for f in flags if f is not None]
+            self._flags_device = torch.cat(flags) if flags else None
+        # Pinned host memory cannot be allocated while capturing: the copy of the flags is enqueued
+        # after each replay instead (one small asynchronous D2H copy).
+        self._flags_host = None
+        if self._flags_device is not None:
+            self._flags_host = torch.empty(self._flags_device.shape, dtype=self._flags_device.dtype,
+                                           pin_memory=True)
+        self._done = torch.cuda.Event()
+        self._pending = False
+
+    def __call__(self):
+        self._check(block=False)
+        self.graph.replay()
+        if self._flags_host is not None:
+            self._flags_host.copy_(self._flags_device, non_blocking=True)
+        self._done.record()
+        self._pending = self._flags_device is not None
+        return self.output
+
+    def check(self) -> None:
+        """
+        Wait for the last replay and raise if it found a validation error.
+        """
+        self._check(block=True)
+
+    def _check(self, block: bool) -> None:
+        if not self._pending:
+            return
+        if block:
+            self._done.synchronize()
+        elif not self._done.query():
+            return
+        self._pending = False
+        values = self._flags_host.tolist()
+        cursor = 0
+        for joint in self._joints:
+            count = joint.flag_count()
+            joint.raise_from(values[cursor:cursor + count])
+            cursor += count

@@ -31,6 +31,7 @@ class DrawConfig:
     stream_id: int
     particle_offset: int
     noise: Optional[torch.Tensor] = None
+    step_device: Optional[torch.Tensor] = None   # uint64 word added to `step` on the device
 
 
 def _flat_param(t: torch.Tensor, N: int) -> Tuple[torch.Tensor, int]:
@@ -63,8 +64,9 @@ class _NormalRsampleFn(torch.autograd.Function):
         seed, step = _philox_key(cfg)
         eps = cfg.noise
         nat.check(nat.lib().mi_normal_rsample(
-            loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step, cfg.stream_id,
-            cfg.particle_offset, nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)),
+            loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step,
+            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
+            z.data_ptr(), nat.stream_handle(loc.device)),
             "mi_normal_rsample")
         ctx.cfg = cfg
         ctx.N = N
@@ -87,8 +89,9 @@ class _NormalRsampleFn(torch.autograd.Function):
         deps_scale = torch.empty(N, dtype=torch.float32, device=device)
         seed, step = _philox_key(cfg)
         nat.check(lib.mi_normal_rsample_backward(
-            dz.data_ptr(), dz.stride(0), dz.stride(1), K, N, seed, step, cfg.stream_id,
-            cfg.particle_offset, nat.ptr(cfg.noise), workspace.data_ptr(), size.value,
+            dz.data_ptr(), dz.stride(0), dz.stride(1), K, N, seed, step,
+            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
+            workspace.data_ptr(), size.value,
             dloc.data_ptr(), deps_scale.data_ptr(), nat.stream_handle(device)),
             "mi_normal_rsample_backward")
         # dz/dscale = eps: the kernel returns sum_k dz * eps directly.
@@ -104,8 +107,9 @@ class _BetaRsampleFn(torch.autograd.Function):
         x = torch.empty((K, N), dtype=torch.float32, device=c1.device)
         seed, step = _philox_key(cfg)
         nat.check(nat.lib().mi_beta_rsample(
-            c1.data_ptr(), c1_s, c0.data_ptr(), c0_s, K, N, seed, step, cfg.stream_id,
-            cfg.particle_offset, nat.ptr(cfg.noise), x.data_ptr(), nat.stream_handle(c1.device)),
+            c1.data_ptr(), c1_s, c0.data_ptr(), c0_s, K, N, seed, step,
+            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
+            x.data_ptr(), nat.stream_handle(c1.device)),
             "mi_beta_rsample")
         ctx.save_for_backward(x, c1, c0)
         ctx.strides = (c1_s, c0_s)
@@ -165,8 +169,8 @@ def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
 
 
 def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: int,
-             particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None) \
-        -> Dict[str, torch.Tensor]:
+             particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None,
+             step_device: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """
     Draw every factor of a factorised guide (dict order = stream id order).
     """
@@ -174,6 +178,7 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
     for stream_id, (name, factor) in enumerate(approximation.items()):
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
                          particle_offset=particle_offset,
-                         noise=None if noise is None else noise.get(name))
+                         noise=None if noise is None else noise.get(name),
+                         step_device=step_device)
         samples[name] = draw(factor, cfg)
     return samples

@@ -19,7 +19,7 @@ from typing import Callable, cast, Dict, Optional, Set, Type
 import torch
 from torch import distributions, nn
 
-from . import engine, guide, particles
+from . import engine, graph, guide, particles
 from .core import condition, LogProbTracer
 from .util import _normalize_shape, maybe_as_tensor, OptionalSize, TensorDict
 
@@ -161,7 +161,7 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.seed = int(seed if seed is not None else torch.initial_seed()) & ((1 << 64) - 1)
         self.validate = validate
         self.process_group = process_group
-        self._step = 0
+        self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
 
     def _shard(self):
         """
@@ -185,10 +185,16 @@ class EvidenceLowerBoundLoss(nn.Module):
         if isinstance(approximation, Dict):
             approximation = FactorizedDistribution(approximation)
         world, _, K, offset = self._shard()
-        step = self._step
-        self._step += 1
         if isinstance(approximation, dict):
-            samples = guide.draw_all(approximation, K, self.seed, step, offset, _noise)
+            device = _guide_device(approximation)
+            if self._counter is None or self._counter.device != device:
+                self._counter = torch.zeros(1, dtype=torch.int64, device=device)
+            # The draws (and their regeneration in backward) use a snapshot of the device counter,
+            # which is then advanced on the device -- replays of a captured step draw anew.
+            step = self._counter.clone()
+            self._counter.add_(1)
+            samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
+                                     step_device=step)
         else:
             samples = approximation.rsample(torch.Size([K]))
         if not isinstance(samples, Dict):
@@ -202,11 +208,23 @@ class EvidenceLowerBoundLoss(nn.Module):
                       torch.device("cuda", torch.cuda.current_device()))
         joint = engine.log_joint(trace, g0, device)
         if self.validate:
-            joint.raise_on_violation()
+            collector = graph.deferred()
+            if collector is not None:
+                collector.append(joint)
+            else:
+                joint.raise_on_violation()
         entropy = approximation.entropy()
         if world > 1:
             entropy = entropy / world
         return (joint.total * g0).sum() - entropy
+
+
+def _guide_device(approximation: Dict[str, torch.distributions.Distribution]) -> torch.device:
+    for factor in approximation.values():
+        for item in vars(factor).values():
+            if isinstance(item, torch.Tensor):
+                return item.device
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 class LogLikelihoodLoss(nn.Module):

@@ -60,12 +60,14 @@ class SiteRecord:
 @dataclasses.dataclass
 class CheckRecord:
     """
-    A deferred support / constraint check that could not run inside vmap (a batched value).
-    ``output`` indexes a per-particle boolean output.
+    A support / constraint check evaluated on the device and resolved with the step's single
+    validation sync. ``output`` indexes a (per-particle) boolean output of the vmapped trace;
+    ``memo`` is committed to the validation memo once the check has passed.
     """
     name: str
     output: int
     message: str
+    memo: Optional[Tuple] = None
 
 
 # Unbatched (conditioned) data is validated once per tensor version instead of on every step:
@@ -79,29 +81,44 @@ def _memo_key(value: torch.Tensor, constraint: Constraint) -> Tuple:
             str(value.device), repr(constraint))
 
 
-def check_unbatched(value: torch.Tensor, constraint: Constraint) -> bool:
-    """
-    ``check_constraint(constraint, value).all()`` memoised on (storage, layout, version).
-    """
-    masked = isinstance(value, torch.masked.MaskedTensor)
+def _plain(value: torch.Tensor) -> torch.Tensor:
     # The private fields avoid MaskedTensor.get_data (an autograd.Function, not vmap-compatible);
     # the reference reads the same fields (mininf/util.py:85-89).
-    plain = value._masked_data if masked else value
-    key = _memo_key(plain, constraint)
-    hit = _VALIDATED.get(key)
-    if hit is not None and hit[0]() is plain and hit[1] == plain._version:
-        return True
+    return value._masked_data if isinstance(value, torch.masked.MaskedTensor) else value
+
+
+def device_check(constraint: Constraint, value: torch.Tensor) -> torch.Tensor:
+    """
+    ``check_constraint(constraint, value).all()`` as a 0-d device tensor (no host sync), usable
+    inside vmap; masked-out elements pass.
+    """
     with torch.no_grad():
-        passed = constraint.check(plain)
-        if masked:
+        passed = constraint.check(_plain(value))
+        if isinstance(value, torch.masked.MaskedTensor):
             mask = value._masked_mask
             for _ in range(constraint.event_dim):
                 mask = mask.all(-1)
             passed = passed | ~mask
-        ok = bool(passed.all())
-    if ok:
-        _VALIDATED[key] = (weakref.ref(plain), plain._version)
-    return ok
+        return passed.all()
+
+
+def memo_lookup(value: torch.Tensor, constraint: Constraint) -> Optional[Tuple]:
+    """
+    None if this exact tensor version already passed this check, else the memo entry to commit
+    once the (deferred) check has passed.
+    """
+    plain = _plain(value)
+    key = _memo_key(plain, constraint)
+    hit = _VALIDATED.get(key)
+    if hit is not None and hit[0]() is plain and hit[1] == plain._version:
+        return None
+    return (key, weakref.ref(plain), plain._version)
+
+
+def memo_commit(entry: Tuple) -> None:
+    key, ref, version = entry
+    if ref() is not None:
+        _VALIDATED[key] = (ref, version)
 
 
 def classify(distribution: Distribution) -> Tuple[str, List[Any]]:
@@ -143,14 +160,25 @@ class ParticleTracer(TracerMixin):
 
     def _check_support(self, name: str, value: Any, distribution: Distribution,
                        constraint: Constraint) -> None:
+        """
+        Value-support check of sites the kernels do not read (values, no_log_prob sites, torch
+        sites). Conditioned data that already passed (same storage and version) is skipped; the
+        rest is evaluated on the device and raised with the step's single validation sync.
+        """
         if not self._validate_parameters:
             return
-        if is_batched(value):
-            ok = check_constraint(constraint, value).all()
-            self.checks.append(CheckRecord(name, self._emit(ok), str(core.support_error(
-                name, type(distribution).__name__))))
-        elif not check_unbatched(value, constraint):
-            raise core.support_error(name, distribution)
+        memo = None
+        if not (is_batched(value) or is_batched(_plain(value))):
+            memo = memo_lookup(value, constraint)
+            if memo is None:
+                return
+        try:
+            described = str(distribution) if memo is not None else type(distribution).__name__
+        except Exception:  # reprs of batched parameters
+            described = type(distribution).__name__
+        ok = device_check(constraint, value)
+        self.checks.append(CheckRecord(name, self._emit(ok), str(core.support_error(
+            name, described)), memo))
 
     def sample(self, state: State, name: str, distribution: Distribution,
                sample_shape: OptionalSize = None) -> torch.Tensor:

@@ -1,0 +1,75 @@
+"""
+Particle sharding across ranks exercised with the gloo backend on the CPU
+(world size 2): rank particle ranges, the single flat all-reduce of gradients + loss, and the
+identity "sum of rank shares == single-process value" for the ELBO's linear structure.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mininf_amd.distributed import all_reduce_gradients
+from mininf_amd.nn import EvidenceLowerBoundLoss
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def worker(rank, world, port, queue):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        loss = EvidenceLowerBoundLoss(num_particles=8 * world, process_group=dist.group.WORLD)
+        shard = loss._shard()
+        # A linear "loss share" per rank, as the ELBO produces: sum over the rank's particles / K.
+        K = loss.num_particles
+        w = torch.nn.Parameter(torch.tensor([1.0, -2.0]))
+        offset, local = shard[3], shard[2]
+        particles = torch.arange(offset, offset + local, dtype=torch.float32)
+        share = (w[0] * particles.sum() + w[1] * particles.square().sum()) / K
+        share.backward()
+        total = all_reduce_gradients([w], dist.group.WORLD, loss=share)
+        queue.put((rank, shard, w.grad.tolist(), float(total)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharding_and_all_reduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    queue = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(queue.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    K = 16
+    k = torch.arange(K, dtype=torch.float32)
+    want_grad = [float(k.sum() / K), float(k.square().sum() / K)]
+    want_total = float((k.sum() - 2 * k.square().sum()) / K)
+    for rank, shard, grad, total in results:
+        assert shard == (world, rank, K // world, rank * (K // world))
+        assert grad == pytest.approx(want_grad)
+        assert total == pytest.approx(want_total)
+
+
+def test_indivisible_particles_rejected():
+    class Group:
+        pass
+
+    loss = EvidenceLowerBoundLoss(num_particles=5)
+    loss.process_group = Group()
+    import unittest.mock as um
+    with um.patch.object(dist, "get_world_size", return_value=2), \
+            um.patch.object(dist, "get_rank", return_value=0):
+        with pytest.raises(ValueError, match="not divisible"):
+            loss._shard()

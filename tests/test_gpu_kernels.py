@@ -1,0 +1,273 @@
+"""
+Kernel-level parity of the HIP path (through the C ABI / engine) against the oracle and the golden
+per-family tables produced by the reference's torch.distributions arithmetic.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+from torch.distributions import Bernoulli, Beta, Normal
+
+import mininf_amd as mi
+from mininf_amd import _native as nat, engine, guide
+from mininf_amd.particles import SiteRecord
+from oracle import build as oracle_build, elbo as oracle, logprob as lpf
+from tests.conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def launch(family, roles, value, device, mask=None, scale=1.0, K=None, N=None, g0=-1.0):
+    """
+    Run a one-site group: `roles` are [K, 1] (per-particle) or [K, N] tensors, `value` [K, N] or
+    [N] (shared). Returns (total [K], grads per role, slot grads).
+    """
+    views = []
+    for t in roles + [value]:
+        if t.dim() == 1:
+            views.append(engine._View(t.reshape(1, -1).expand(K, t.shape[0]), 0, t.stride(0)))
+        elif t.shape[1] == 1:
+            views.append(engine._View(t, t.stride(0), 0))
+        else:
+            views.append(engine._View(t, t.stride(0), t.stride(1)))
+    site = SiteRecord("s", family, [], torch.Size([N]), scale, None, family)
+    launcher = engine._GroupLauncher(K, N, g0, device, per_site=True)
+    mview = None if mask is None else engine._View(mask, 0, mask.stride(0))
+    assert launcher.try_add(site, views, mview)
+    total, site_lp, grads, slot_grad, flags = launcher.run(True)
+    torch.cuda.synchronize()
+    return total.cpu(), grads, slot_grad.cpu(), flags.cpu(), launcher
+
+
+def test_philox_device_matches_c_oracle(device):
+    lib = oracle_build.load()
+    ctrs = np.array([[0, 0, 0, 0], [0xFFFFFFFF] * 4, [0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344],
+                     [1, 2, 3, 4]], dtype=np.uint32)
+    keys = [(0, 0), (0xFFFFFFFF, 0xFFFFFFFF), (0xA4093822, 0x299F31D0), (5, 6)]
+    for ctr, (k0, k1) in zip(ctrs, keys):
+        c = torch.as_tensor(ctr.astype(np.int64)).to(torch.int32).to(device)
+        out = torch.empty(4, dtype=torch.int32, device=device)
+        nat.check(nat.lib().mi_philox4x32(c.data_ptr(), 1, k0, k1, out.data_ptr(), None), "philox")
+        want = (ctypes.c_uint32 * 4)()
+        lib.oracle_philox4x32_10((ctypes.c_uint32 * 4)(*ctr.tolist()), k0, k1, want)
+        got = out.cpu().numpy().astype(np.uint32)
+        assert got.tolist() == list(want)
+    K, N = 8, 1000
+    dev = torch.empty(K, N, device=device)
+    nat.check(nat.lib().mi_philox_normal(K, N, 1234, 7, 2, 5, dev.data_ptr(), None), "normals")
+    host = np.empty((K, N), np.float32)
+    lib.oracle_guide_normals(K, N, 1234, 7, 2, 5, host.ctypes.data)
+    np.testing.assert_allclose(dev.cpu().numpy(), host, rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("mode", ["particle", "dense"])
+def test_family_tables(device, mode):
+    f = golden("families.npz")
+
+    def rows(x):
+        t = torch.as_tensor(x, dtype=torch.float32, device=device)
+        return (t.reshape(-1, 1) if mode == "particle" else t.reshape(1, -1)).clone() \
+            .requires_grad_()
+
+    cases = [
+        ("bernoulli_probs", [f["bern_p"]], f["bern_v"], f["bern_lp"], [f["bern_dp"]]),
+        ("bernoulli_logits", [f["bernl_l"]], f["bernl_v"], f["bernl_lp"], [f["bernl_dl"]]),
+        ("normal", [f["norm_loc"], f["norm_scale"]], f["norm_v"], f["norm_lp"],
+         [f["norm_dloc"], f["norm_dscale"]]),
+        ("beta", [f["beta_a"], f["beta_b"]], f["beta_v"], f["beta_lp"],
+         [f["beta_da"], f["beta_db"]]),
+    ]
+    for family, params, value, want_lp, want_grads in cases:
+        n = len(value)
+        K, N = (n, 1) if mode == "particle" else (1, n)
+        roles = [rows(p) for p in params]
+        val = torch.as_tensor(value, dtype=torch.float32, device=device)
+        val = val.reshape(K, N).contiguous()
+        total, grads, slot_grad, flags, launcher = launch(family, roles, val, device, K=K, N=N)
+        if mode == "particle":
+            # 1e-5 relative (the north-star tolerance): Beta's lgamma(a+b) - lgamma(a) - lgamma(b)
+            # cancels in float32 in both implementations.
+            np.testing.assert_allclose(total.numpy(), want_lp, rtol=1e-5, atol=2e-6)
+            for j, want in enumerate(want_grads):
+                ok = np.isfinite(want)
+                np.testing.assert_allclose(slot_grad[j].numpy()[ok], want[ok], rtol=2e-5, atol=2e-5)
+        else:
+            np.testing.assert_allclose(total.numpy()[0], want_lp.sum(), rtol=1e-5)
+            for grad, want in zip(grads, want_grads):
+                ok = np.isfinite(want)
+                np.testing.assert_allclose(-grad.cpu().numpy()[0][ok], want[ok], rtol=2e-5,
+                                           atol=2e-5)
+        assert (flags == 0).all()
+
+
+def test_bcast_site_matches_oracle(device):
+    rng = np.random.default_rng(0)
+    K, N = 300, 5000
+    x = (rng.random(N) < 0.6).astype(np.float32)
+    p = rng.random(K).astype(np.float32) * 0.98 + 0.01
+    probs = torch.as_tensor(p, device=device).reshape(K, 1).requires_grad_()
+    total, _, slot, flags, launcher = launch("bernoulli_probs", [probs],
+                                             torch.as_tensor(x, device=device), device, K=K, N=N)
+    want_lp, want_dp = lpf.bernoulli_probs(p[:, None], x[None, :])
+    np.testing.assert_allclose(total.numpy(), want_lp.sum(1), rtol=1e-6)
+    np.testing.assert_allclose(slot[0].numpy(), want_dp.sum(1), rtol=1e-5)
+    loc = torch.as_tensor(rng.normal(size=(K, 1)).astype(np.float32), device=device).requires_grad_()
+    sd = torch.as_tensor(rng.random((K, 1)).astype(np.float32) + 0.5, device=device).requires_grad_()
+    y = rng.normal(size=N).astype(np.float32)
+    mask = torch.as_tensor(rng.random(N) > 0.3, device=device)
+    total, _, slot, flags, _ = launch("normal", [loc, sd], torch.as_tensor(y, device=device),
+                                      device, mask=mask, K=K, N=N)
+    m = mask.cpu().numpy()
+    lp, dl, ds, _ = lpf.normal(loc.detach().cpu().numpy(), sd.detach().cpu().numpy(), y[None, :])
+    np.testing.assert_allclose(total.numpy(), (lp * m).sum(1), rtol=1e-6)
+    # d/dscale = sum (z^2 - 1) / scale cancels for some particles: compare on the vector's scale.
+    for got, want in ((slot[0].numpy(), (dl * m).sum(1)), (slot[1].numpy(), (ds * m).sum(1))):
+        assert np.abs(got - want).max() <= 1e-5 * np.abs(want).max()
+
+
+def c5_case(device, n=3000, K=24):
+    rng = np.random.default_rng(1)
+    mask = torch.as_tensor(rng.random(n) > 0.2, device=device)
+    y = torch.as_tensor(rng.normal(size=n).astype(np.float32), device=device)
+    b = torch.as_tensor((rng.random(n) < 0.5).astype(np.float32), device=device)
+
+    def model():
+        mu = mi.sample("mu", Normal(0, 1))
+        z = mi.sample("z", Normal(mu, 1), sample_shape=[n])
+        mi.sample("y", Normal(z, 0.5))
+        mi.sample("b", Bernoulli(logits=z))
+
+    approx = mi.nn.ParameterizedFactorizedDistribution(
+        mu=mi.nn.ParameterizedDistribution(Normal, loc=0.2, scale=0.7),
+        z=mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n), scale=torch.ones(n) * 0.9),
+    ).to(device)
+    noise = {"mu": torch.as_tensor(rng.normal(size=K).astype(np.float32), device=device),
+             "z": torch.as_tensor(rng.normal(size=(K, n)).astype(np.float32), device=device)}
+    cond = mi.condition(model, y=torch.masked.as_masked_tensor(y, mask),
+                        b=torch.masked.as_masked_tensor(b, mask))
+    return cond, approx, noise, (y, b, mask), K
+
+
+def run_elbo(cond, approx, noise, K):
+    for p in approx.parameters():
+        p.grad = None
+    value = mi.nn.EvidenceLowerBoundLoss(num_particles=K)(cond, approx(), _noise=noise)
+    value.backward()
+    return float(value), {n: p.grad.detach().cpu().numpy().copy()
+                          for n, p in approx.named_parameters()}
+
+
+def test_specialised_and_generic_kernels_agree(device):
+    cond, approx, noise, _, K = c5_case(device)
+    jit_loss, jit_grads = run_elbo(cond, approx, noise, K)
+    os.environ["MININF_AMD_JIT"] = "0"
+    try:
+        gen_loss, gen_grads = run_elbo(cond, approx, noise, K)
+    finally:
+        del os.environ["MININF_AMD_JIT"]
+    assert abs(jit_loss - gen_loss) <= 1e-6 * abs(gen_loss)
+    for name in gen_grads:
+        np.testing.assert_allclose(jit_grads[name], gen_grads[name], rtol=1e-5, atol=1e-6)
+
+
+def test_c5_against_oracle(device):
+    cond, approx, noise, (y, b, mask), K = c5_case(device)
+    loss, grads = run_elbo(cond, approx, noise, K)
+    n = y.shape[0]
+    ref = oracle.hierarchical_masked_elbo(y.cpu(), b.cpu(), mask.cpu(), 0.2, 0.7, np.zeros(n),
+                                          np.full(n, 0.9, np.float32), noise["mu"].cpu(),
+                                          noise["z"].cpu())
+    assert abs(loss - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    np.testing.assert_allclose(grads["z.distribution_parameters.loc"], ref["grad_z_loc"],
+                               rtol=1e-5, atol=1e-5 * np.abs(ref["grad_z_loc"]).max())
+    np.testing.assert_allclose(grads["z.distribution_parameters.scale"], ref["grad_z_scale"],
+                               rtol=1e-5, atol=1e-5 * np.abs(ref["grad_z_scale"]).max())
+
+
+def test_full_size_c2_closed_form(device):
+    """
+    C2 at full size (n = 1e6, K = 4096): the oracle evaluates the Bernoulli site through its
+    sufficient statistics in float64, so it finishes instantly at this size.
+    """
+    n, K = 1_000_000, 4096
+    gen = torch.Generator().manual_seed(0)
+    x = (torch.rand(n, generator=gen) < 0.7).float()
+    draws = torch.distributions.Beta(torch.tensor(2.5), torch.tensor(1.5)).sample((K,))
+
+    def model():
+        theta = mi.sample("theta", Beta(2, 2))
+        mi.sample("x", Bernoulli(theta), sample_shape=[n])
+
+    approx = mi.nn.ParameterizedDistribution(Beta, concentration1=2.5,
+                                             concentration0=1.5).to(device)
+    value = mi.nn.EvidenceLowerBoundLoss(num_particles=K)(
+        mi.condition(model, x=x.to(device)), {"theta": approx()},
+        _noise={"theta": draws.to(device)})
+    value.backward()
+    ref = oracle.beta_bernoulli_elbo(x.numpy(), 2, 2, 2.5, 1.5, draws.numpy())
+    assert abs(float(value) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    g = approx.distribution_parameters
+    assert abs(float(g["concentration1"].grad) - ref["grad_u_concentration1"]) <= \
+        1e-5 * abs(ref["grad_u_concentration1"])
+    assert abs(float(g["concentration0"].grad) - ref["grad_u_concentration0"]) <= \
+        1e-5 * abs(ref["grad_u_concentration0"])
+
+
+def test_beta_guide_backward_against_oracle(device):
+    rng = np.random.default_rng(3)
+    K, N = 512, 7
+    c1 = torch.as_tensor(rng.random(N).astype(np.float32) * 5 + 0.3, device=device)
+    c0 = torch.as_tensor(rng.random(N).astype(np.float32) * 9 + 0.3, device=device)
+    x = torch.distributions.Beta(c1.cpu(), c0.cpu()).sample((K,)).clamp(1e-4, 1 - 1e-4)
+    c1p, c0p = c1.clone().requires_grad_(), c0.clone().requires_grad_()
+    cfg = guide.DrawConfig(K=K, seed=0, step=0, stream_id=0, particle_offset=0,
+                           noise=x.to(device))
+    draws = guide.draw(Beta(c1p, c0p), cfg)
+    weights = torch.as_tensor(rng.normal(size=(K, N)).astype(np.float32), device=device)
+    (draws * weights).sum().backward()
+    xs, w = x.double().numpy(), weights.cpu().double().numpy()
+    for i in range(N):
+        d1, d0 = lpf.beta_draw_grads(xs[:, i], float(c1[i]), float(c0[i]))
+        np.testing.assert_allclose(float(c1p.grad[i]), (w[:, i] * d1).sum(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(float(c0p.grad[i]), (w[:, i] * d0).sum(), rtol=1e-4, atol=1e-5)
+
+
+def test_guide_draws_statistics_and_sharding(device):
+    K, N = 4096, 64
+    loc = torch.linspace(-1, 1, N, device=device)
+    scale = torch.linspace(0.5, 2, N, device=device)
+    full = guide.draw(Normal(loc, scale), guide.DrawConfig(K, 9, 3, 0, 0))
+    halves = [guide.draw(Normal(loc, scale), guide.DrawConfig(K // 2, 9, 3, 0, off))
+              for off in (0, K // 2)]
+    torch.testing.assert_close(torch.cat(halves), full, rtol=0, atol=0)
+    z = (full - loc) / scale
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1) < 0.01
+    c1, c0 = torch.full((N,), 2.0, device=device), torch.full((N,), 5.0, device=device)
+    x = guide.draw(Beta(c1, c0), guide.DrawConfig(K, 9, 3, 1, 0))
+    assert abs(float(x.mean()) - 2 / 7) < 0.005
+    assert abs(float(x.var()) - 2 * 5 / (49 * 8)) < 0.002
+    assert float(x.min()) > 0 and float(x.max()) < 1
+
+
+def test_validation_errors_are_raised(device):
+    def model():
+        theta = mi.sample("theta", Beta(2, 2))
+        mi.sample("x", Bernoulli(theta), sample_shape=[5])
+
+    approx = mi.nn.ParameterizedDistribution(Beta, concentration1=2.0,
+                                             concentration0=2.0).to(device)
+    bad = torch.tensor([0.0, 1.0, 2.0, 1.0, 0.0], device=device)
+    with pytest.raises(ValueError, match="is not in the support"):
+        mi.nn.EvidenceLowerBoundLoss(num_particles=8)(mi.condition(model, x=bad),
+                                                      {"theta": approx()})
+
+    def normal_model():
+        mi.sample("y", Normal(0.0, mi.value("s")), sample_shape=[3])
+
+    with pytest.raises(ValueError, match="satisfy"):
+        loss = mi.nn.EvidenceLowerBoundLoss(num_particles=4)
+        loss(mi.condition(normal_model, y=torch.zeros(3, device=device),
+                          s=torch.tensor(-1.0, device=device)),
+             {"q": Normal(torch.zeros((), device=device), 1.0)})

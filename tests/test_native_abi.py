@@ -49,7 +49,8 @@ def test_invalid_arguments_are_rejected():
     size = ctypes.c_size_t()
     group = nat.Group()
     assert lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)) == -1
-    assert lib.mi_normal_rsample(None, 0, None, 0, 1, 1, 0, 0, 0, 0, None, None, None) == -1
+    assert lib.mi_normal_rsample(None, 0, None, 0, 1, 1, 0, 0, None, 0, 0, None, None,
+                                 None) == -1
     assert lib.mi_categorical_workspace_bytes(0, 1, ctypes.byref(size)) == -1
 
 
