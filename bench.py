@@ -282,7 +282,7 @@ def main():
     def eager_step():
         loss = forward_backward()
         finish_step()
-        return loss
+        return loss.detach()   # keep no autograd graph alive across steps (graph capture needs it)
 
     # Eager steps: every kernel launched from Python (the kernel timing comes from these).
     for _ in range(args.warmup):
@@ -292,6 +292,7 @@ def main():
     eager_elapsed, loss = timed(eager_step, eager_steps)
     timer.active = False
     eager_ms = 1e3 * eager_elapsed / eager_steps
+    torch.cuda.synchronize()
     elapsed, mode = eager_elapsed * args.steps / eager_steps, "eager"
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
