@@ -65,6 +65,24 @@ MI_DEV void publish_flags(uint32_t* flags, uint32_t mine) {
   if (mine != 0u && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, mine);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Hardware transcendentals (fp32).
+// ---------------------------------------------------------------------------------------------
+MI_DEV float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// exp(x) = 2^(x log2 e) on v_exp_f32; results below FLT_MIN flush to zero, which only drops terms
+// smaller than every sum they enter.
+MI_DEV float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
+// log1p(t), t in [0, 1]: u = 1 + t rounds, and log(u) * t / (u - 1) cancels the rounding of u
+// (Goldberg's trick); v_log_f32 is log2.
+MI_DEV float log1p_unit(float t) {
+  const float u = 1.0f + t;
+  const float d = u - 1.0f;
+  const float lg = __builtin_amdgcn_logf(u) * 0.69314718055994531f;
+  return d == 0.0f ? t : lg * (t * rcp(d));
+}
+
 // -------------------------------------------------------------------------------------------------
 // Per-element family math.  d[r] = d log p / d role_r.
 // -------------------------------------------------------------------------------------------------
@@ -78,7 +96,7 @@ struct Elem {
 // Normal(loc, scale): -(v-loc)^2 / (2 scale^2) - log(scale) - log(sqrt(2 pi))
 // torch/distributions/normal.py:88-103; support real (constraints.py: `value == value`).
 MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
-  const float inv = 1.0f / scale;
+  const float inv = rcp(scale);
   const float z = (v - loc) * inv;
   e.lp = -0.5f * z * z - logf(scale) - kHalfLog2Pi;
   e.d[0] = z * inv;
@@ -90,10 +108,15 @@ MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
 
 // Bernoulli(logits): -BCE_with_logits(l, v) = -(max(l, 0) - l v + log1p(exp(-|l|)))
 // torch/distributions/bernoulli.py:121-125; support boolean {0, 1} (constraints.py:317-325).
+// The streaming site programs evaluate this per (particle, element), so it is written with the
+// hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp each) instead of libm's
+// correctly-rounded-ish expf/log1pf/division sequences (~100 VALU ops per element on gfx950):
+// log1p(t) for t in [0, 1] uses log(u) * t / (u - 1) with u = 1 + t, exact to a few ulp.
 MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
-  const float t = expf(-fabsf(l));
-  e.lp = -(fmaxf(l, 0.0f) - l * v + log1pf(t));
-  const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
+  const float t = fast_exp(-fabsf(l));
+  e.lp = -(fmaxf(l, 0.0f) - l * v + log1p_unit(t));
+  const float r = rcp(1.0f + t);
+  const float sig = l >= 0.0f ? r : t * r;
   e.d[0] = v - sig;
   e.d[1] = 0.0f;
   e.d[2] = l;

@@ -225,8 +225,9 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
 // (1 - x). Four regimes: x near 0 (Taylor series), x near 1 (series for the mirrored variable),
 // both shapes large (Rice saddle-point expansion), otherwise a fitted rational correction of the
 // analytic approximation x (psi(total) - psi(alpha)) / beta.
-MI_DEV double beta_grad_small_alpha(double x, double a, double b) {
-  const double factor = digamma(a) - digamma(a + b) - log(x);
+// psi_a = digamma(a), psi_ab = digamma(a + b): parameter-only, hoisted out of the particle loop.
+MI_DEV double beta_grad_small_alpha(double x, double a, double b, double psi_a, double psi_ab) {
+  const double factor = psi_a - psi_ab - log(x);
   double coeff = 1.0;
   double series = coeff / a * (factor + 1.0 / a);
   for (int n = 1; n <= 10; ++n) {
@@ -238,8 +239,9 @@ MI_DEV double beta_grad_small_alpha(double x, double a, double b) {
   return r != r ? 0.0 : r;
 }
 
-MI_DEV double beta_grad_small_beta(double x, double a, double b) {
-  const double factor = digamma(a + b) - digamma(b);
+// psi_ab = digamma(a + b), psi_b = digamma(b).
+MI_DEV double beta_grad_small_beta(double x, double a, double b, double psi_ab, double psi_b) {
+  const double factor = psi_ab - psi_b;
   double coeff = 1.0, prod = 1.0, dprod = 0.0, series = factor / a;
   for (int n = 1; n <= 8; ++n) {
     coeff *= -x / n;
@@ -301,11 +303,15 @@ __constant__ double kBetaGradCoef[2][3][3][4] = {
       {0.001925008108, -0.002869809258, 0.0008000589141, -6.063713228e-05},
       {-0.0003477407336, 6.959756487e-05, 1.097287507e-05, -1.650964693e-06}}}};
 
-MI_DEV double dirichlet_grad(double x, double alpha, double total) {
+// Every regime needs only digamma(alpha) and digamma(total) of the parameters, which the caller
+// evaluates once per element rather than once per particle.
+MI_DEV double dirichlet_grad(double x, double alpha, double total, double psi_alpha,
+                             double psi_total) {
   const double beta = total - alpha;
   const double boundary = total * x * (1.0 - x);
-  if (x <= 0.5 && boundary < 2.5) return beta_grad_small_alpha(x, alpha, beta);
-  if (x >= 0.5 && boundary < 0.75) return -beta_grad_small_beta(1.0 - x, beta, alpha);
+  if (x <= 0.5 && boundary < 2.5) return beta_grad_small_alpha(x, alpha, beta, psi_alpha, psi_total);
+  if (x >= 0.5 && boundary < 0.75)
+    return -beta_grad_small_beta(1.0 - x, beta, alpha, psi_total, psi_alpha);
   if (alpha > 6.0 && beta > 6.0) return beta_grad_mid(x, alpha, beta);
   const double u = log(x);
   const double a = log(alpha) - u;
@@ -324,7 +330,7 @@ MI_DEV double dirichlet_grad(double x, double alpha, double total) {
       den += w * (d[0] + b * (d[1] + b * (d[2] + b * d[3])));
     }
   }
-  const double analytic = x * (digamma(total) - digamma(alpha)) / beta;
+  const double analytic = x * (psi_total - psi_alpha) / beta;
   return num / den * analytic;
 }
 
@@ -342,14 +348,16 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
   if (i < N) {
     const float a = c1[i * c1_s], b = c0[i * c0_s];
     const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
+    const double psi_a = digamma((double)a), psi_b = digamma((double)b);
+    const double psi_t = digamma((double)tot);
     for (int64_t k = k0 + ty; k < k1; k += tk) {
       const float g = dx[k * dx_sk + i * dx_si];
       if (g == 0.0f) continue;
       const float xv = x[k * N + i];
       const float xw = 1.0f - xv;
       // _Dirichlet_backward: grad_j * (go_j - sum(x * go)) with go = (g, 0)
-      s1 += dirichlet_grad(xv, a, tot) * (double)g * (double)(1.0f - xv);
-      s0 -= dirichlet_grad(xw, b, tot) * (double)g * (double)xv;
+      s1 += dirichlet_grad(xv, a, tot, psi_a, psi_t) * (double)g * (double)(1.0f - xv);
+      s0 -= dirichlet_grad(xw, b, tot, psi_b, psi_t) * (double)g * (double)xv;
     }
   }
   red[threadIdx.x][0] = s1;
@@ -412,7 +420,7 @@ BwdGeometry bwd_geometry(int64_t K, int64_t units) {
   const int tk = 256 / ti;
   g.gx = ceil_div(units, ti);
   int64_t slices = ceil_div(1024, g.gx);
-  slices = std::min<int64_t>(slices, ceil_div(K, (int64_t)tk * 4));
+  slices = std::min<int64_t>(slices, ceil_div(K, (int64_t)tk * 2));
   slices = std::max<int64_t>(1, slices);
   g.rows = ceil_div(K, slices);
   g.slices = ceil_div(K, g.rows);

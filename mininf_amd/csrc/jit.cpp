@@ -92,20 +92,23 @@ std::string mask_kind_tag(const mi_site& st) {
 
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
-  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "|"
+  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
+    << plan.waves_per_eu << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
     s << (int)kind_of(op.stride_k, op.stride_i) << (g.compute_grads ? op.grad_mode : 0)
-      << (op.grad_mode == MI_GRAD_PARTICLE ? op.slot : 0) << ",";
+      << (op.grad_mode == MI_GRAD_PARTICLE ? op.slot : 0) << (op.stride_i == 1 ? "u" : "")
+      << (op.grad_stride_i == 1 ? "v" : "") << ",";
   }
   s << "|" << g.num_sites << ":";
   for (int i = 0; i < g.num_sites; ++i) {
     const mi_site& st = g.sites[i];
     s << st.family << "(" << st.operand[0] << "," << st.operand[1] << "," << st.operand[2] << ","
-      << mask_kind_tag(st) << ")";
+      << mask_kind_tag(st) << (st.mask_stride_i == 1 ? "u" : "") << ")";
   }
-  s << "|" << g.num_slots << "|" << g.compute_grads;
+  s << "|" << g.num_slots << "|" << g.compute_grads
+    << (plan.row && g.N < 64L * plan.elems ? "|small" : "");
   return Signature{s.str()};
 }
 
@@ -166,7 +169,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   auto dense_grad = [&](int op) { return g.compute_grads && g.operands[op].grad_mode == MI_GRAD_DENSE; };
 
   o << "#include \"device_math.hpp\"\n";
-  o << "extern \"C\" __global__ __launch_bounds__(256) void mi_site_program(const mi_group G, "
+  o << "extern \"C\" __global__ __launch_bounds__(256) ";
+  if (plan.waves_per_eu > 0) o << "__attribute__((amdgpu_waves_per_eu(" << plan.waves_per_eu << ", 8))) ";
+  o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
   o << "  const int lane = threadIdx.x & 63;\n";
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
@@ -256,55 +261,133 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       if (mask_is(s, kDense)) o << in << "bool " << prefix << "m" << s << "[" << Es << "];\n";
   };
 
-  if (row) {
-    o << "  if (seg < nseg) {\n";
-    o << "    const long base = seg * " << 64 * E << "L;\n";
-    o << "    const long k_begin = (long)blockIdx.y * arg;\n";
-    o << "    const long k_end = min(K, k_begin + arg);\n";
-    o << "    long idx[" << E << "]; bool ok[" << E << "];\n";
-    o << "#pragma unroll\n    for (int e = 0; e < " << E << "; ++e) { const long i = base + e * 64 + lane; "
-         "ok[e] = i < N; idx[e] = ok[e] ? i : N - 1; }\n";
+  // One copy of the row loop (see below). Element e of the lane: `ie` in the clamped copy.
+  auto emit_row_loop = [&](bool full) {
+    const std::string ie = full ? "(base + e * 64 + lane)" : "idx[e]";
+    const std::string valid = "ok[e]";
+    auto unit = [&](int op) { return full && g.operands[op].stride_i == 1; };
+    auto unit_grad = [&](int op) { return full && g.operands[op].grad_stride_i == 1; };
+    auto unit_mask = [&](int s) { return full && g.sites[s].mask_stride_i == 1; };
+    const char* in = "      ";
+    if (!full)
+      o << in << "long idx[" << E << "]; bool ok[" << E << "];\n#pragma unroll\n" << in
+        << "for (int e = 0; e < " << E << "; ++e) { const long i = base + e * 64 + lane; "
+           "ok[e] = i < N; idx[e] = ok[e] ? i : N - 1; }\n";
+    else
+      o << in << "bool ok[" << E << "];\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
+        << "; ++e) ok[e] = e * 64 + lane >= shift;\n";
     for (int op = 0; op < g.num_operands; ++op)
-      if (is(op, kShared))
-        o << "    float s" << op << "[" << E << "];\n#pragma unroll\n    for (int e = 0; e < " << E
-          << "; ++e) s" << op << "[e] = x" << op << "[idx[e] * si" << op << "];\n";
+      if (is(op, kShared)) {
+        o << in << "float s" << op << "[" << E << "];\n";
+        if (unit(op))
+          o << in << "{ const float* __restrict__ r = x" << op << " + base + lane;\n#pragma unroll\n"
+            << in << "for (int e = 0; e < " << E << "; ++e) s" << op << "[e] = r[e * 64]; }\n";
+        else
+          o << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) s" << op
+            << "[e] = x" << op << "[" << ie << " * si" << op << "];\n";
+      }
     for (int s = 0; s < g.num_sites; ++s)
-      if (mask_is(s, kShared))
-        o << "    bool m" << s << "[" << E << "];\n#pragma unroll\n    for (int e = 0; e < " << E
-          << "; ++e) m" << s << "[e] = mk" << s << "[idx[e] * msi" << s << "] != 0;\n";
+      if (mask_is(s, kShared)) {
+        o << in << "bool m" << s << "[" << E << "];\n";
+        if (unit_mask(s))
+          o << in << "{ const unsigned char* __restrict__ r = mk" << s << " + base + lane;\n#pragma unroll\n"
+            << in << "for (int e = 0; e < " << E << "; ++e) m" << s << "[e] = r[e * 64] != 0; }\n";
+        else
+          o << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) m" << s
+            << "[e] = mk" << s << "[" << ie << " * msi" << s << "] != 0;\n";
+      }
+    // Dense (particle x element) loads of row `kexpr` into `prefix`<op>[e].
+    auto row_loads = [&](const char* ind, const char* prefix, const std::string& kexpr) {
+      for (int op = 0; op < g.num_operands; ++op)
+        if (is(op, kDense)) {
+          if (unit(op))
+            o << ind << "{ const float* __restrict__ r = x" << op << " + " << kexpr << " * sk" << op
+              << " + base + lane;\n#pragma unroll\n" << ind << "for (int e = 0; e < " << E << "; ++e) "
+              << prefix << op << "[e] = r[e * 64]; }\n";
+          else
+            o << "#pragma unroll\n" << ind << "for (int e = 0; e < " << E << "; ++e) " << prefix << op
+              << "[e] = x" << op << "[" << kexpr << " * sk" << op << " + " << ie << " * si" << op << "];\n";
+        }
+      for (int s = 0; s < g.num_sites; ++s)
+        if (mask_is(s, kDense))
+          o << "#pragma unroll\n" << ind << "for (int e = 0; e < " << E << "; ++e) " << prefix << "m" << s
+            << "[e] = mk" << s << "[" << kexpr << " * msk" << s << " + " << ie << " * msi" << s
+            << "] != 0;\n";
+    };
     // software pipeline: the next row's dense values are in flight while this row computes
-    declare_dense("    ", "n");
-    o << "    if (k_begin < k_end) {\n";
-    dense_loads("      ", "n", "k_begin", "idx[e]");
-    o << "    }\n";
-    for (int v = 0; v < nv; ++v) o << "    float keep" << v << " = 0.0f;\n";
-    o << "    for (long k = k_begin; k < k_end; ++k) {\n";
-    o << "      const int r = (int)((k - k_begin) & 63);\n";
-    declare_dense("      ", "d");
+    declare_dense(in, "n");
+    o << in << "if (k_begin < k_end) {\n";
+    row_loads("        ", "n", "k_begin");
+    o << in << "}\n";
+    for (int v = 0; v < nv; ++v) o << in << "float keep" << v << " = 0.0f;\n";
+    o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
+    o << in << "  const int r = (int)((k - k_begin) & 63);\n";
+    declare_dense("        ", "d");
     for (int op = 0; op < g.num_operands; ++op)
       if (is(op, kDense))
-        o << "#pragma unroll\n      for (int e = 0; e < " << E << "; ++e) d" << op << "[e] = n" << op
-          << "[e];\n";
+        o << "#pragma unroll\n" << in << "  for (int e = 0; e < " << E << "; ++e) d" << op << "[e] = n"
+          << op << "[e];\n";
     for (int s = 0; s < g.num_sites; ++s)
       if (mask_is(s, kDense))
-        o << "#pragma unroll\n      for (int e = 0; e < " << E << "; ++e) dm" << s << "[e] = nm" << s
-          << "[e];\n";
-    o << "      if (k + 1 < k_end) {\n";
-    dense_loads("        ", "n", "(k + 1)", "idx[e]");
-    o << "      }\n";
-    particle_loads("      ", "k");
-    zero_accumulators("      ");
-    compute_and_store("      ", "ok[e]", "k", "idx[e]");
+        o << "#pragma unroll\n" << in << "  for (int e = 0; e < " << E << "; ++e) dm" << s << "[e] = nm"
+          << s << "[e];\n";
+    o << in << "  if (k + 1 < k_end) {\n";
+    row_loads("          ", "n", "(k + 1)");
+    o << in << "  }\n";
+    particle_loads("        ", "k");
+    zero_accumulators("        ");
+    const char* in2 = "        ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << in2 << "float g" << op << "[" << E << "];\n";
+    o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) {\n";
+    const std::string inner = std::string(in2) + "  ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
+    for (int s = 0; s < g.num_sites; ++s) emit_site_eval(o, g, s, valid, inner.c_str());
+    o << in2 << "}\n";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) {
+        if (unit_grad(op))
+          o << in2 << "{ float* __restrict__ r = gx" << op << " + k * gsk" << op
+            << " + base + lane;\n#pragma unroll\n" << in2 << "for (int e = 0; e < " << E
+            << "; ++e) if (ok[e]) r[e * 64] = G.grad_scale * g" << op << "[e]; }\n";
+        else
+          o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) if (" << valid
+            << ") gx" << op << "[k * gsk" << op << " + " << ie << " * gsi" << op
+            << "] = G.grad_scale * g" << op << "[e];\n";
+      }
     for (int v = 0; v < nv; ++v)
-      o << "      { const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
+      o << in2 << "{ const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
         << " = (lane == r) ? t : keep" << v << "; }\n";
-    o << "      if (r == 63 || k + 1 == k_end) {\n";
-    o << "        if (lane <= r) {\n";
+    o << in2 << "if (r == 63 || k + 1 == k_end) {\n";
+    o << in2 << "  if (lane <= r) {\n";
     for (int v = 0; v < nv; ++v)
-      o << "          part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
-    o << "        }\n";
-    for (int v = 0; v < nv; ++v) o << "        keep" << v << " = 0.0f;\n";
-    o << "      }\n    }\n  }\n";
+      o << in2 << "    part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
+    o << in2 << "  }\n";
+    for (int v = 0; v < nv; ++v) o << in2 << "  keep" << v << " = 0.0f;\n";
+    o << in2 << "}\n";
+    o << in << "}\n";
+  };
+
+  if (row) {
+    // Lane `lane` owns elements base + e * 64 + lane of each row (coalesced per e). When N spans
+    // at least one whole segment, every segment is loaded as a whole one: the ragged last segment
+    // is shifted back to end at N and masks the elements its predecessor already owns (`ok`), so
+    // no load needs a bound and unit-stride operands use one row pointer with compile-time
+    // offsets e * 64 folded into the instructions. Smaller N takes the clamped-index copy.
+    o << "  if (seg < nseg) {\n";
+    o << "    const long k_begin = (long)blockIdx.y * arg;\n";
+    o << "    const long k_end = min(K, k_begin + arg);\n";
+    if (g.N >= 64L * E) {
+      o << "    const long nominal = seg * " << 64 * E << "L;\n";
+      o << "    const long shift = max(0L, nominal + " << 64 * E << "L - N);\n";
+      o << "    const long base = nominal - shift;\n";
+      emit_row_loop(true);
+    } else {
+      o << "    const long base = seg * " << 64 * E << "L;\n";
+      emit_row_loop(false);
+    }
+    o << "  }\n";
   } else {
     const int kw = plan.kw;
     const int istep = 64 / kw;

@@ -12,6 +12,7 @@ struct PlanInfo {
   int elems;       // ROW: elements per lane per row; COL: unroll of the element loop
   int kw;          // COL: lanes per element group (power of two <= 64)
   bool combined;   // reduce one weighted log-joint value per particle instead of one per site
+  int waves_per_eu;  // occupancy target handed to the compiler (0 = compiler's choice)
   unsigned grid_x;
   unsigned grid_y;
 };

@@ -22,6 +22,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -618,6 +619,17 @@ bool validate_group(const mi_group* g) {
 
 bool is_dense(const mi_operand& op) { return op.stride_k != 0 && op.stride_i != 0; }
 
+int env_int(const char* name, int fallback) {
+  const char* v = std::getenv(name);
+  return v != nullptr ? std::atoi(v) : fallback;
+}
+
+// Elements per lane per row of the ROW shape (4, 8 or 16).
+int row_elems() {
+  const int e = env_int("MININF_AMD_ROW_ELEMS", kRowElems);
+  return (e == 4 || e == 16) ? e : 8;
+}
+
 bool bcast_eligible(const mi_group* g) {
   if (g->num_sites != 1 || g->N < 1024 || g->K < 64) return false;
   const mi_site& st = g->sites[0];
@@ -660,7 +672,7 @@ Plan make_plan(const mi_group* g) {
                             llabs(g->operands[dense].stride_i) < llabs(g->operands[dense].stride_k);
   if (row || row_fallback) {
     p.shape = kRow;
-    p.nseg = ceil_div(g->N, 64 * kRowElems);
+    p.nseg = ceil_div(g->N, 64 * row_elems());
     const int64_t gx = ceil_div(p.nseg, 4);
     int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(kTargetBlocks, gx)));
     p.rows_per_block = ceil_div(g->K, gy);
@@ -688,7 +700,10 @@ PlanInfo plan_info(const Plan& p, bool combined) {
   PlanInfo info{};
   info.combined = combined;
   info.row = p.shape == kRow;
-  info.elems = p.shape == kRow ? kRowElems : kColUnroll;
+  // Tuning knobs (measured defaults; the env overrides exist for sweeps).
+  info.elems = p.shape == kRow ? row_elems() : std::max(1, env_int("MININF_AMD_COL_UNROLL",
+                                                                        kColUnroll));
+  info.waves_per_eu = env_int("MININF_AMD_WAVES_PER_EU", 0);
   info.kw = p.kw;
   info.grid_x = p.grid.x;
   info.grid_y = p.grid.y;
@@ -791,10 +806,18 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
         reduced_lp = combined ? 1 : G.num_sites;
         break;
       }
-      if (p.shape == kRow)
-        hipLaunchKernelGGL((mi::k_group_row<kRowElems>), p.grid, dim3(256), 0, s, G, part, p.nseg,
-                           p.rows_per_block, flags);
-      else
+      if (p.shape == kRow) {
+        const int e = row_elems();
+        if (e == 4)
+          hipLaunchKernelGGL((mi::k_group_row<4>), p.grid, dim3(256), 0, s, G, part, p.nseg,
+                             p.rows_per_block, flags);
+        else if (e == 16)
+          hipLaunchKernelGGL((mi::k_group_row<16>), p.grid, dim3(256), 0, s, G, part, p.nseg,
+                             p.rows_per_block, flags);
+        else
+          hipLaunchKernelGGL((mi::k_group_row<8>), p.grid, dim3(256), 0, s, G, part, p.nseg,
+                             p.rows_per_block, flags);
+      } else
         hipLaunchKernelGGL(mi::k_group_col, p.grid, dim3(256), 0, s, G, part, p.nseg, p.seg_len,
                            p.kw, flags);
       break;

@@ -172,8 +172,13 @@ def test_specialised_and_generic_kernels_agree(device):
         np.testing.assert_allclose(jit_grads[name], gen_grads[name], rtol=1e-5, atol=1e-6)
 
 
-def test_c5_against_oracle(device):
-    cond, approx, noise, (y, b, mask), K = c5_case(device)
+@pytest.mark.parametrize("n", [3000, 2048, 300, 1])
+def test_c5_against_oracle(device, n):
+    """
+    Row-layout site program at a ragged size (shifted last segment), an exact multiple of the
+    segment, and sizes below one segment (clamped-index program).
+    """
+    cond, approx, noise, (y, b, mask), K = c5_case(device, n=n)
     loss, grads = run_elbo(cond, approx, noise, K)
     n = y.shape[0]
     ref = oracle.hierarchical_masked_elbo(y.cpu(), b.cpu(), mask.cpu(), 0.2, 0.7, np.zeros(n),
