@@ -239,7 +239,7 @@ def main():
 
     w = workload(args.config, device, world, rank)
     module = w["module"]
-    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True)
+    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
     loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(
         num_particles=w["k_local"] * world, seed=1, validate=not args.no_validate,
         process_group=group)

@@ -93,7 +93,7 @@ typedef struct mi_group {
   int32_t num_operands;
   int32_t num_slots;
   int32_t compute_grads; /* 0: forward values only */
-  float grad_scale;      /* g0: upstream dL/dT_k assumed for MI_GRAD_DENSE outputs */
+  float grad_scale;      /* g0: upstream dL/dT_k assumed for MI_GRAD_DENSE / PARTICLE outputs */
   int32_t pad0;
   mi_site sites[MI_MAX_SITES];
   mi_operand operands[MI_MAX_OPERANDS];
@@ -113,7 +113,7 @@ int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);
 /* Evaluate all sites of `group` for every particle:
  *   total[k]              = sum_s scale_s * sum_i mask_si * log p_s(value_ki | params_ki)  (fp32)
  *   site_lp[s*K + k]      = scale_s * sum_i mask_si * log p_s(...)  (fp64; may be NULL)
- *   slot_grad[j*K + k]    = dT_k / d x[k] for MI_GRAD_PARTICLE operands mapped to slot j (fp32)
+ *   slot_grad[j*K + k]    = g0 * dT_k / d x[k] for MI_GRAD_PARTICLE operands in slot j (fp32)
  *   operands[o].grad      = g0 * dT_k / d x[k,i] for MI_GRAD_DENSE operands
  *   flags[s]              = OR of MI_FLAG_* found for site s (zeroed by this call)
  * Replaces LogProbTracer.sample's dist.log_prob (core.py:241, masked branch core.py:231-239),
@@ -185,13 +185,16 @@ int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t
 
 /* Implicit reparameterisation gradient of the Beta draws (dirichlet.py:17-20 ->
  * torch._dirichlet_grad, ATen/native/Distributions.h dirichlet_grad_one), reduced over particles:
- *   dc1[i] = sum_k dx[k,i] * dgrad(x, c1, c1+c0) * (1 - x)
- *   dc0[i] = -sum_k dx[k,i] * dgrad(1 - x, c0, c1+c0) * x */
+ *   dc1[i * dc1_stride] = sum_k dx[k,i] * dgrad(x, c1, c1+c0) * (1 - x)
+ *   dc0[i * dc0_stride] = -sum_k dx[k,i] * dgrad(1 - x, c0, c1+c0) * x
+ * (output strides let the gradient land directly in the interleaved [..., 2] concentration layout
+ * torch's Beta keeps, beta.py:36-40). */
 int mi_beta_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
 int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
                              const float* x, const float* c1, int64_t c1_stride, const float* c0,
                              int64_t c0_stride, int64_t K, int64_t N, void* workspace,
-                             size_t workspace_bytes, float* dc1, float* dc0, void* stream);
+                             size_t workspace_bytes, float* dc1, int64_t dc1_stride, float* dc0,
+                             int64_t dc0_stride, void* stream);
 
 /* Raw generator output for tests: out[k, i] = standard normal eps of mi_normal_rsample. */
 int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
@@ -199,6 +202,65 @@ int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_
 /* Raw Philox-4x32-10 blocks for known-answer tests: out[4*j .. 4*j+3] = philox(ctr[j], key). */
 int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t key1, uint32_t* out,
                   void* stream);
+
+/* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
+
+#define MI_MAX_TERMS 8
+#define MI_MAX_FACTORS 8
+#define MI_MAX_BUFFERS 16
+
+/* One mean-field guide factor whose entropy enters the ELBO, viewed as n elements:
+ *   MI_NORMAL: param[1] = scale (param[0], loc, is not read);   grad[1] = d loss / d scale
+ *   MI_BETA:   param[0] = concentration1, param[1] = concentration0; grad[0], grad[1]
+ * Parameters are fp32 with element stride `stride` (0 only when n == 1); grads (written by
+ * mi_elbo_backward, may be NULL) use the same element strides, e.g. both Beta parameters and both
+ * gradients interleaved in one [n, 2] concentration array. */
+typedef struct mi_factor {
+  int32_t family;
+  int32_t pad0;
+  int64_t n;
+  const float* param[2];
+  int64_t stride[2];
+  float* grad[2];
+} mi_factor;
+
+/* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f sum_i H_f(i)
+ * terms: per-particle log joints [K] (site-group totals, categorical totals, torch-evaluated sites);
+ * g0 = -1/K_total (fp32); entropy_scale = 1/world when particles are sharded over ranks.
+ * buffers: the speculative gradients of the site groups (computed for upstream g0), rescaled by
+ * mi_elbo_backward when the loss's upstream gradient is not exactly 1. */
+typedef struct mi_elbo {
+  int64_t K;
+  int32_t num_terms;
+  int32_t num_factors;
+  int32_t num_buffers;
+  int32_t pad0;
+  float g0;
+  float pad1;
+  double entropy_scale;
+  const float* terms[MI_MAX_TERMS];
+  mi_factor factors[MI_MAX_FACTORS];
+  float* buffers[MI_MAX_BUFFERS];
+  int64_t buffer_len[MI_MAX_BUFFERS];
+} mi_elbo;
+
+/* sizeof(mi_factor), sizeof(mi_elbo) as compiled. */
+int mi_elbo_struct_sizes(size_t* factor, size_t* elbo);
+
+/* Workspace of mi_elbo_forward. It holds a completion counter that must be zero before first use
+ * (mi_elbo_workspace_init) and that every forward leaves at zero, so one workspace serves every
+ * step (and captured HIP graphs) on one stream. */
+int mi_elbo_workspace_bytes(const mi_elbo* elbo, size_t* bytes);
+int mi_elbo_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
+
+/* Writes the scalar loss (fp32, reduced in fp64 in a fixed order). */
+int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes, float* loss,
+                    void* stream);
+
+/* With u = *upstream (device scalar, d out / d loss): dterm[0] = u * g0 (the gradient of every
+ * term element), factors[f].grad[j][i] = -u * entropy_scale * dH_f(i)/dparam_j, and every buffer
+ * is multiplied by u unless u == 1. One launch. */
+int mi_elbo_backward(const mi_elbo* elbo, const float* upstream, float* dterm, void* stream);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 MAX_SITES = 4
 MAX_OPERANDS = 6
 MAX_SLOTS = 4
+MAX_TERMS = 8
+MAX_FACTORS = 8
+MAX_BUFFERS = 16
 
 NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
@@ -55,6 +58,23 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("pad0", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
+    ]
+
+
+class Factor(ctypes.Structure):
+    _fields_ = [
+        ("family", ctypes.c_int32), ("pad0", ctypes.c_int32), ("n", c_i64),
+        ("param", c_vp * 2), ("stride", c_i64 * 2), ("grad", c_vp * 2),
+    ]
+
+
+class Elbo(ctypes.Structure):
+    _fields_ = [
+        ("K", c_i64), ("num_terms", ctypes.c_int32), ("num_factors", ctypes.c_int32),
+        ("num_buffers", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("g0", ctypes.c_float), ("pad1", ctypes.c_float), ("entropy_scale", ctypes.c_double),
+        ("terms", c_vp * MAX_TERMS), ("factors", Factor * MAX_FACTORS),
+        ("buffers", c_vp * MAX_BUFFERS), ("buffer_len", c_i64 * MAX_BUFFERS),
     ]
 
 
@@ -95,11 +115,17 @@ _SIGNATURES = {
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
-                                                c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp, c_vp,
-                                                c_vp]),
+                                                c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp, c_i64,
+                                                c_vp, c_i64, c_vp]),
     "mi_philox_normal": (ctypes.c_int, [c_i64, c_i64, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_uint32, c_i64, c_vp, c_vp]),
     "mi_philox4x32": (ctypes.c_int, [c_vp, c_i64, ctypes.c_uint32, ctypes.c_uint32, c_vp, c_vp]),
+    "mi_elbo_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 2),
+    "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
+                                               ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
+    "mi_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -1,7 +1,7 @@
 """
 In-tree build of ``libmininf_amd.so`` (gfx950). Used by ``__graft_entry__.build()`` and the tests.
 
-The library holds the precompiled kernels (sites.hip, guide.hip) and the host-side site-program
+The library holds the precompiled kernels (sites.hip, guide.hip, elbo.hip) and the host-side site-program
 specialiser (jit.cpp), which embeds ``include/mininf_amd.h`` and ``csrc/device_math.hpp`` verbatim
 so that kernels compiled at trace time by hiprtc share the exact device math of the precompiled
 ones.
@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
-SOURCES = [os.path.join(CSRC, name) for name in ("sites.hip", "guide.hip", "jit.cpp")]
+SOURCES = [os.path.join(CSRC, name) for name in ("sites.hip", "guide.hip", "elbo.hip", "jit.cpp")]
 HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "jit.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]
 EMBEDDED = {"embedded_header.inc": os.path.join(INCLUDE, "mininf_amd.h"),

@@ -129,15 +129,23 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
   }
 }
 
-// Sum `slices` rows of a [slices, N] partial array (fixed order, fp64).
-__global__ __launch_bounds__(kGuideThreads) void k_sum_slices(const float* __restrict__ part,
+// Sum the `slices` rows of two [slices, N] partial arrays (fixed order, fp64) into out_a[i * sa]
+// and out_b[i * sb].
+__global__ __launch_bounds__(kGuideThreads) void k_sum_slices(const float* __restrict__ part_a,
+                                                              const float* __restrict__ part_b,
                                                               int64_t slices, int64_t N,
-                                                              float* __restrict__ out) {
+                                                              float* __restrict__ out_a, int64_t sa,
+                                                              float* __restrict__ out_b,
+                                                              int64_t sb) {
   const int64_t i = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   if (i >= N) return;
-  double acc = 0.0;
-  for (int64_t s = 0; s < slices; ++s) acc += (double)part[s * N + i];
-  out[i] = (float)acc;
+  double a = 0.0, b = 0.0;
+  for (int64_t s = 0; s < slices; ++s) {
+    a += (double)part_a[s * N + i];
+    b += (double)part_b[s * N + i];
+  }
+  out_a[i * sa] = (float)a;
+  out_b[i * sb] = (float)b;
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -337,8 +345,8 @@ MI_DEV double dirichlet_grad(double x, double alpha, double total, double psi_al
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
     const float* __restrict__ dx, int64_t dx_sk, int64_t dx_si, const float* __restrict__ x,
     const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
-    int64_t K, int64_t N, float* __restrict__ out1, float* __restrict__ out0, int64_t out_stride,
-    int64_t rows_per_block, int ti) {
+    int64_t K, int64_t N, float* __restrict__ out1, int64_t o1_s, float* __restrict__ out0,
+    int64_t o0_s, int64_t out_stride, int64_t rows_per_block, int ti) {
   __shared__ double red[kGuideThreads][2];
   const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kGuideThreads / ti;
   const int64_t i = (int64_t)blockIdx.x * ti + tx;
@@ -369,8 +377,8 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
       t1 += red[r * ti + tx][0];
       t0 += red[r * ti + tx][1];
     }
-    out1[blockIdx.y * out_stride + i] = (float)t1;
-    out0[blockIdx.y * out_stride + i] = (float)t0;
+    out1[blockIdx.y * out_stride + i * o1_s] = (float)t1;
+    out0[blockIdx.y * out_stride + i * o0_s] = (float)t0;
   }
 }
 
@@ -480,8 +488,8 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
-  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, out_loc, gy, N, dloc);
-  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, out_scale, gy, N, dscale);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, out_loc, out_scale,
+                     gy, N, dloc, (int64_t)1, dscale, (int64_t)1);
   return to_code(hipGetLastError());
 }
 
@@ -508,7 +516,8 @@ int mi_beta_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes
 int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
                              const float* x, const float* c1, int64_t c1_stride, const float* c0,
                              int64_t c0_stride, int64_t K, int64_t N, void* workspace,
-                             size_t workspace_bytes, float* dc1, float* dc0, void* stream) {
+                             size_t workspace_bytes, float* dc1, int64_t dc1_stride, float* dc0,
+                             int64_t dc0_stride, void* stream) {
   if (dx == nullptr || x == nullptr || c1 == nullptr || c0 == nullptr || dc1 == nullptr ||
       dc0 == nullptr || K < 1 || N < 1)
     return MI_EINVAL;
@@ -520,18 +529,20 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
   const int64_t rows = geo.rows, gy = geo.slices;
   float* o1 = dc1;
   float* o0 = dc0;
+  int64_t s1 = dc1_stride, s0 = dc0_stride;
   if (gy > 1) {
     o1 = static_cast<float*>(workspace);
     o0 = o1 + gy * N;
+    s1 = s0 = 1;
   }
   hipLaunchKernelGGL(mi::k_beta_rsample_bwd, dim3((unsigned)geo.gx, (unsigned)gy),
                      dim3(mi::kGuideThreads), 0, s, dx, dx_stride_k, dx_stride_i, x, c1, c1_stride,
-                     c0, c0_stride, K, N, o1, o0, N, rows, geo.ti);
+                     c0, c0_stride, K, N, o1, s1, o0, s0, N, rows, geo.ti);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
-  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o1, gy, N, dc1);
-  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o0, gy, N, dc0);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o1, o0, gy, N, dc1,
+                     dc1_stride, dc0, dc0_stride);
   return to_code(hipGetLastError());
 }
 

@@ -466,6 +466,7 @@ struct FinalizeArgs {
   int32_t num_sites;
   int32_t num_slots;
   double scale[MI_MAX_SITES];
+  double slot_scale;  // the group's grad_scale: slot gradients are speculative like dense ones
 };
 
 // One block per 64 particles; its 1024 threads split the segments 16 ways (fixed assignment), each
@@ -511,7 +512,7 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restr
         if (site_lp != nullptr) site_lp[(int64_t)v * K + k] = acc;
         t += acc;
       } else {
-        slot_grad[(int64_t)(v - A.num_sites) * K + k] = (float)acc;
+        slot_grad[(int64_t)(v - A.num_sites) * K + k] = (float)(acc * A.slot_scale);
       }
     }
   }
@@ -832,6 +833,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   mi::FinalizeArgs A{};
   A.num_sites = reduced_lp;
   A.num_slots = G.num_slots;
+  A.slot_scale = (double)G.grad_scale;
   for (int i = 0; i < reduced_lp; ++i) A.scale[i] = prescaled ? 1.0 : G.sites[i].scale;
   hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK)),
                      dim3(mi::kFinK * mi::kFinG), 0, s, part, p.nseg, G.K, A, total, site_lp,

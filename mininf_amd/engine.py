@@ -309,6 +309,11 @@ class _SiteGroupFn(torch.autograd.Function):
         g = g.contiguous()
         device = g.device
         out: List[Optional[torch.Tensor]] = []
+        if launcher.num_slots:
+            # slot gradients are speculative too (pre-multiplied by g0): slot_grad[j, k] is row k
+            nat.check(nat.lib().mi_scale_rows(slot_grad.data_ptr(), 1, launcher.K, launcher.K,
+                                              launcher.num_slots, g.data_ptr(), launcher.g0,
+                                              nat.stream_handle(device)), "mi_scale_rows")
         for op, grad in zip(launcher.operands, grads):
             if op.mode == nat.GRAD_DENSE:
                 sk, si = grad.stride()
@@ -317,34 +322,43 @@ class _SiteGroupFn(torch.autograd.Function):
                                                   nat.stream_handle(device)), "mi_scale_rows")
                 out.append(grad)
             elif op.mode == nat.GRAD_PARTICLE:
-                out.append((slot_grad[op.slot] * g).reshape(launcher.K, 1))
+                out.append(slot_grad[op.slot].reshape(launcher.K, 1))
             else:
                 out.append(None)
         return (None, None, *out)
+
+
+def _run_categorical(site: SiteRecord, g0: float, logits: torch.Tensor, value: torch.Tensor,
+                     mask: Optional[torch.Tensor], need: bool):
+    """
+    Launch ``mi_categorical_forward``: (total [K], speculative dlogits or None, flags [1]).
+    """
+    K, N, C = logits.shape
+    device = logits.device
+    dlogits = torch.zeros_like(logits) if need else None
+    size = ctypes.c_size_t()
+    lib = nat.lib()
+    nat.check(lib.mi_categorical_workspace_bytes(K, N, ctypes.byref(size)),
+              "mi_categorical_workspace_bytes")
+    workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+    total = torch.empty(K, dtype=torch.float32, device=device)
+    flags = torch.empty(1, dtype=torch.int32, device=device)
+    nat.check(lib.mi_categorical_forward(
+        logits.data_ptr(), logits.stride(0), logits.stride(1), logits.stride(2), K, N, C,
+        value.data_ptr(), value.stride(0), value.stride(1),
+        None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(1),
+        site.scale, g0, None if dlogits is None else dlogits.data_ptr(), workspace.data_ptr(),
+        size.value, total.data_ptr(), flags.data_ptr(), nat.stream_handle(device)),
+        "mi_categorical_forward")
+    return total, dlogits, flags
 
 
 class _CategoricalFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, site: SiteRecord, holder: dict, g0: float, logits: torch.Tensor,
                 value: torch.Tensor, mask: Optional[torch.Tensor]):  # type: ignore[override]
-        K, N, C = logits.shape
-        device = logits.device
-        need = logits.requires_grad
-        dlogits = torch.zeros_like(logits) if need else None
-        size = ctypes.c_size_t()
-        lib = nat.lib()
-        nat.check(lib.mi_categorical_workspace_bytes(K, N, ctypes.byref(size)),
-                  "mi_categorical_workspace_bytes")
-        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
-        total = torch.empty(K, dtype=torch.float32, device=device)
-        flags = torch.empty(1, dtype=torch.int32, device=device)
-        nat.check(lib.mi_categorical_forward(
-            logits.data_ptr(), logits.stride(0), logits.stride(1), logits.stride(2), K, N, C,
-            value.data_ptr(), value.stride(0), value.stride(1),
-            None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(1),
-            site.scale, g0, None if dlogits is None else dlogits.data_ptr(), workspace.data_ptr(),
-            size.value, total.data_ptr(), flags.data_ptr(), nat.stream_handle(device)),
-            "mi_categorical_forward")
+        total, dlogits, flags = _run_categorical(site, g0, logits, value, mask,
+                                                 logits.requires_grad)
         holder["flags"] = flags
         ctx.dlogits = dlogits
         ctx.g0 = g0
@@ -494,3 +508,231 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
     else:
         total = torch.zeros(K, device=device)
     return LogJoint(total=total, pending=pending, checks=trace.checks)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fused ELBO: site groups + entropy + the scalar reduction in one autograd node.
+# ------------------------------------------------------------------------------------------------
+@dataclasses.dataclass
+class EntropyFactor:
+    """
+    A guide factor whose entropy the ELBO kernels evaluate (``mi_factor``): ``tensor`` is the
+    autograd input -- Normal: the scale as [n] (stride 1, or any stride when n == 1); Beta: the
+    interleaved [n, 2] concentration array.
+    """
+    family: int
+    n: int
+    tensor: torch.Tensor
+
+
+_ELBO_WORKSPACE: Dict[Tuple[str, int], torch.Tensor] = {}
+
+
+def _elbo_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """
+    Per-device workspace of ``mi_elbo_forward`` (its completion counter must start at zero and is
+    left at zero by every launch, so the buffer is allocated and zeroed once and reused by every
+    step, including captured graphs).
+    """
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    ws = _ELBO_WORKSPACE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 14), dtype=torch.uint8, device=device)
+        nat.check(nat.lib().mi_elbo_workspace_init(ws.data_ptr(), ws.numel(),
+                                                   nat.stream_handle(device)),
+                  "mi_elbo_workspace_init")
+        _ELBO_WORKSPACE[key] = ws
+    return ws
+
+
+class _ElboPlan:
+    """
+    Everything one ELBO evaluation launches, in the order of the autograd inputs:
+    site groups (their operand tensors), categorical sites (logits, value, mask), torch-evaluated
+    sites (their [K] log densities) and the entropy factors.
+    """
+    def __init__(self, K: int, g0: float, device: torch.device, launchers, categorical,
+                 fallback: List[torch.Tensor], factors: List[EntropyFactor],
+                 entropy_scale: float) -> None:
+        self.K, self.g0, self.device = K, g0, device
+        self.launchers = launchers
+        self.categorical = categorical
+        self.fallback = [v.to(torch.float32).reshape(K) for v in fallback]
+        self.factors = factors
+        self.entropy_scale = entropy_scale
+        self.holders = [dict() for _ in launchers]
+        self.cat_holders = [dict() for _ in categorical]
+        self.state = None
+
+    def inputs(self) -> List[Optional[torch.Tensor]]:
+        out: List[Optional[torch.Tensor]] = []
+        for launcher in self.launchers:
+            out.extend(launcher.inputs())
+        for _, lg, val, mask in self.categorical:
+            out.extend([lg, val, mask])
+        out.extend(self.fallback)
+        out.extend(f.tensor for f in self.factors)
+        return out
+
+    def _describe(self, terms: List[torch.Tensor], buffers: List[torch.Tensor]) -> nat.Elbo:
+        E = nat.Elbo()
+        E.K = self.K
+        E.g0 = self.g0
+        E.entropy_scale = self.entropy_scale
+        E.num_terms = len(terms)
+        for j, t in enumerate(terms):
+            E.terms[j] = t.data_ptr()
+        E.num_factors = len(self.factors)
+        for j, f in enumerate(self.factors):
+            d = E.factors[j]
+            d.family, d.n = f.family, f.n
+            base = f.tensor.data_ptr()
+            if f.family == nat.BETA:
+                d.param[0], d.param[1] = base, base + 4
+                d.stride[0] = d.stride[1] = 2
+            else:
+                d.param[1] = base
+                d.stride[1] = f.tensor.stride(0) if f.n > 1 else 0
+        E.num_buffers = len(buffers)
+        for j, b in enumerate(buffers):
+            E.buffers[j] = b.data_ptr()
+            E.buffer_len[j] = b.numel()
+        return E
+
+    def forward(self) -> torch.Tensor:
+        terms: List[torch.Tensor] = []
+        buffers: List[torch.Tensor] = []
+        results = []
+        for launcher, holder in zip(self.launchers, self.holders):
+            need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
+            total, site_lp, grads, slot_grad, flags = launcher.run(need)
+            holder["flags"], holder["site_lp"] = flags, site_lp
+            terms.append(total)
+            if need:
+                buffers.extend(g for g in grads if g is not None)
+                if launcher.num_slots:
+                    buffers.append(slot_grad[:launcher.num_slots])
+            results.append((grads, slot_grad))
+        cat_results = []
+        for (site, lg, val, mask), holder in zip(self.categorical, self.cat_holders):
+            total, dlogits, flags = _run_categorical(site, self.g0, lg, val, mask,
+                                                     lg.requires_grad)
+            holder["flags"] = flags
+            terms.append(total)
+            if dlogits is not None:
+                buffers.append(dlogits)
+            cat_results.append(dlogits)
+        terms.extend(t.contiguous() for t in self.fallback)
+        if len(terms) > nat.MAX_TERMS:
+            head = nat.MAX_TERMS - 1
+            terms = terms[:head] + [torch.stack(terms[head:]).sum(0)]
+        extra = buffers[nat.MAX_BUFFERS:]
+        buffers = buffers[:nat.MAX_BUFFERS]
+        E = self._describe(terms, buffers)
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
+                  "mi_elbo_workspace_bytes")
+        ws = _elbo_workspace(self.device, size.value)
+        loss = torch.empty((), dtype=torch.float32, device=self.device)
+        nat.check(lib.mi_elbo_forward(ctypes.byref(E), ws.data_ptr(), ws.numel(), loss.data_ptr(),
+                                      nat.stream_handle(self.device)), "mi_elbo_forward")
+        self.state = (E, results, cat_results, extra, terms)
+        return loss
+
+    def backward(self, u: torch.Tensor) -> List[Optional[torch.Tensor]]:
+        if self.state is None:   # a second backward through the same graph: recompute
+            self.forward()
+        E, results, cat_results, extra, _ = self.state
+        self.state = None
+        device = self.device
+        u = u.to(torch.float32).contiguous()
+        dterm = torch.empty(1, dtype=torch.float32, device=device)
+        fgrads = []
+        for j, f in enumerate(self.factors):
+            grad = torch.empty_like(f.tensor)
+            base = grad.data_ptr()
+            d = E.factors[j]
+            if f.family == nat.BETA:
+                d.grad[0], d.grad[1] = base, base + 4
+            else:
+                d.grad[1] = base
+            fgrads.append(grad)
+        nat.check(nat.lib().mi_elbo_backward(ctypes.byref(E), u.data_ptr(), dterm.data_ptr(),
+                                             nat.stream_handle(device)), "mi_elbo_backward")
+        for buffer in extra:
+            buffer.mul_(u)
+        out: List[Optional[torch.Tensor]] = []
+        for launcher, (grads, slot_grad) in zip(self.launchers, results):
+            for op, grad in zip(launcher.operands, grads):
+                if op.mode == nat.GRAD_DENSE:
+                    out.append(grad)
+                elif op.mode == nat.GRAD_PARTICLE:
+                    out.append(slot_grad[op.slot].reshape(launcher.K, 1))
+                else:
+                    out.append(None)
+        for dlogits in cat_results:
+            out.extend([dlogits, None, None])
+        out.extend(dterm.expand(self.K) for _ in self.fallback)
+        out.extend(fgrads)
+        return out
+
+
+class _ElboFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan: _ElboPlan, *inputs):  # type: ignore[override]
+        ctx.plan = plan
+        return plan.forward()
+
+    @staticmethod
+    def backward(ctx, u: torch.Tensor):  # type: ignore[override]
+        return (None, *ctx.plan.backward(u))
+
+
+def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
+    """
+    Split a factorised guide into factors whose entropy the ELBO kernels evaluate (Normal, Beta)
+    and the rest (whose entropy torch.distributions evaluates).
+    """
+    from torch.distributions import Beta, Normal
+
+    from . import guide
+    fused: List[EntropyFactor] = []
+    rest = []
+    for factor in approximation.values():
+        cls = type(factor)
+        n = max(1, int(factor.batch_shape.numel()))
+        if len(fused) < nat.MAX_FACTORS and cls is Normal and factor.scale.dtype == torch.float32 \
+                and factor.scale.is_cuda and factor.scale.numel() == n:
+            scale = factor.scale.reshape(n)
+            if n > 1 and scale.stride(0) != 1:
+                scale = scale.contiguous()
+            fused.append(EntropyFactor(nat.NORMAL, n, scale))
+        elif len(fused) < nat.MAX_FACTORS and cls is Beta:
+            conc = guide.beta_concentration(factor, n)
+            if conc.is_cuda:
+                fused.append(EntropyFactor(nat.BETA, n, conc))
+            else:
+                rest.append(factor)
+        else:
+            rest.append(factor)
+    return fused, rest
+
+
+def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[EntropyFactor],
+         entropy_scale: float) -> Tuple[torch.Tensor, LogJoint]:
+    """
+    ``g0 * sum_k log p(x, z_k) - entropy_scale * H[factors]`` as one autograd node: the site
+    kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
+    backward is one ``mi_elbo_backward`` launch (plus the guide samplers' own backward).
+    """
+    launchers, categorical = plan_groups(trace, g0, device)
+    plan = _ElboPlan(trace.K, g0, device, launchers, categorical,
+                     [value for _, value in trace.fallback], factors, entropy_scale)
+    loss = _ElboFn.apply(plan, *plan.inputs())
+    pending: List[Tuple[str, dict, List[SiteRecord]]] = []
+    for (site, _, _, _), holder in zip(categorical, plan.cat_holders):
+        pending.append(("categorical", holder, [site]))
+    for launcher, holder in zip(launchers, plan.holders):
+        pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
+    return loss, LogJoint(total=loss, pending=pending, checks=trace.checks)

@@ -98,28 +98,40 @@ class _NormalRsampleFn(torch.autograd.Function):
         return None, dloc, None, deps_scale, None
 
 
+def beta_concentration(distribution: Beta, N: int) -> torch.Tensor:
+    """
+    The [N, 2] (concentration1, concentration0) array torch's Beta keeps for its Dirichlet
+    (beta.py:36-40), as one contiguous fp32 tensor: the sampler, its backward and the entropy read
+    and write both parameters interleaved, so autograd needs no select/stack kernels.
+    """
+    dirichlet = getattr(distribution, "_dirichlet", None)
+    conc = dirichlet.concentration if dirichlet is not None else \
+        torch.stack([distribution.concentration1, distribution.concentration0], -1)
+    if conc.dtype != torch.float32:
+        raise nat.NativeError(f"guide parameters must be float32, got {conc.dtype}")
+    conc = conc.reshape(N, 2)
+    return conc if conc.is_contiguous() else conc.contiguous()
+
+
 class _BetaRsampleFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg: DrawConfig, c1: torch.Tensor, c1_s: int, c0: torch.Tensor,
-                c0_s: int):  # type: ignore[override]
-        N = c1.shape[0]
+    def forward(ctx, cfg: DrawConfig, conc: torch.Tensor):  # type: ignore[override]
+        N = conc.shape[0]
         K = cfg.K
-        x = torch.empty((K, N), dtype=torch.float32, device=c1.device)
+        x = torch.empty((K, N), dtype=torch.float32, device=conc.device)
         seed, step = _philox_key(cfg)
+        base = conc.data_ptr()
         nat.check(nat.lib().mi_beta_rsample(
-            c1.data_ptr(), c1_s, c0.data_ptr(), c0_s, K, N, seed, step,
-            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
-            x.data_ptr(), nat.stream_handle(c1.device)),
+            base, 2, base + 4, 2, K, N, seed, step, nat.ptr(cfg.step_device), cfg.stream_id,
+            cfg.particle_offset, nat.ptr(cfg.noise), x.data_ptr(), nat.stream_handle(conc.device)),
             "mi_beta_rsample")
-        ctx.save_for_backward(x, c1, c0)
-        ctx.strides = (c1_s, c0_s)
+        ctx.save_for_backward(x, conc)
         ctx.K, ctx.N = K, N
         return x
 
     @staticmethod
     def backward(ctx, dx: torch.Tensor):  # type: ignore[override]
-        x, c1, c0 = ctx.saved_tensors
-        c1_s, c0_s = ctx.strides
+        x, conc = ctx.saved_tensors
         K, N = ctx.K, ctx.N
         device = dx.device
         size = ctypes.c_size_t()
@@ -127,13 +139,13 @@ class _BetaRsampleFn(torch.autograd.Function):
         nat.check(lib.mi_beta_rsample_backward_workspace_bytes(K, N, ctypes.byref(size)),
                   "mi_beta_rsample_backward_workspace_bytes")
         workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
-        dc1 = torch.empty(N, dtype=torch.float32, device=device)
-        dc0 = torch.empty(N, dtype=torch.float32, device=device)
+        dconc = torch.empty((N, 2), dtype=torch.float32, device=device)
+        base, out = conc.data_ptr(), dconc.data_ptr()
         nat.check(lib.mi_beta_rsample_backward(
-            dx.data_ptr(), dx.stride(0), dx.stride(1), x.data_ptr(), c1.data_ptr(), c1_s,
-            c0.data_ptr(), c0_s, K, N, workspace.data_ptr(), size.value, dc1.data_ptr(),
-            dc0.data_ptr(), nat.stream_handle(device)), "mi_beta_rsample_backward")
-        return None, dc1, None, dc0, None
+            dx.data_ptr(), dx.stride(0), dx.stride(1), x.data_ptr(), base, 2, base + 4, 2, K, N,
+            workspace.data_ptr(), size.value, out, 2, out + 4, 2, nat.stream_handle(device)),
+            "mi_beta_rsample_backward")
+        return None, dconc
 
 
 def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
@@ -155,13 +167,12 @@ def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
     if cls is Beta:
         shape = distribution.batch_shape
         N = max(1, int(shape.numel()))
-        c1, c1_s = _flat_param(distribution.concentration1, N)
-        c0, c0_s = _flat_param(distribution.concentration0, N)
-        nat.require_device(c1, "guide Beta.concentration1")
+        conc = beta_concentration(distribution, N)
+        nat.require_device(conc, "guide Beta concentration")
         if cfg.noise is not None:
-            cfg.noise = cfg.noise.to(device=c1.device, dtype=torch.float32).reshape(cfg.K, N) \
+            cfg.noise = cfg.noise.to(device=conc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
-        x = _BetaRsampleFn.apply(cfg, c1, c1_s, c0, c0_s)
+        x = _BetaRsampleFn.apply(cfg, conc)
         return x.reshape((cfg.K,) + tuple(shape))
     if cfg.noise is not None:
         return cfg.noise

@@ -206,17 +206,26 @@ class EvidenceLowerBoundLoss(nn.Module):
         g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
         device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)),
                       torch.device("cuda", torch.cuda.current_device()))
-        joint = engine.log_joint(trace, g0, device)
+        if isinstance(approximation, dict):
+            # Fused path: site kernels, guide entropy and the reduction in one autograd node.
+            factors, rest = engine.entropy_factors(approximation)
+            loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world)
+            if rest:
+                extra = cast(torch.Tensor, sum(f.entropy().sum() for f in rest))
+                loss = loss - (extra / world if world > 1 else extra)
+        else:
+            joint = engine.log_joint(trace, g0, device)
+            entropy = approximation.entropy()
+            if world > 1:
+                entropy = entropy / world
+            loss = (joint.total * g0).sum() - entropy
         if self.validate:
             collector = graph.deferred()
             if collector is not None:
                 collector.append(joint)
             else:
                 joint.raise_on_violation()
-        entropy = approximation.entropy()
-        if world > 1:
-            entropy = entropy / world
-        return (joint.total * g0).sum() - entropy
+        return loss
 
 
 def _guide_device(approximation: Dict[str, torch.distributions.Distribution]) -> torch.device:

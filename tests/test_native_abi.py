@@ -42,6 +42,9 @@ def test_struct_layout_matches_header():
                                         ctypes.sizeof(nat.Group)]
     assert nat.Site.scale.offset == 56 and nat.Site.mask.offset == 32
     assert nat.Group.sites.offset == 40
+    elbo_sizes = [ctypes.c_size_t() for _ in range(2)]
+    assert nat.lib().mi_elbo_struct_sizes(*[ctypes.byref(s) for s in elbo_sizes]) == 0
+    assert [s.value for s in elbo_sizes] == [ctypes.sizeof(nat.Factor), ctypes.sizeof(nat.Elbo)]
 
 
 def test_invalid_arguments_are_rejected():
