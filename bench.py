@@ -176,6 +176,24 @@ def c5_bytes(w):
     return 8.0 * K * n + 9.0 * n
 
 
+def measured_traffic(name):
+    """
+    HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/rNN_pmc.json, written by profiles/summarize.py from separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950
+    correction). None when that config has not been profiled.
+    """
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        entry = json.load(fh).get(name)
+    if entry is None:
+        return None, None
+    return entry["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(name, budget_s=12.0):
     """
     The reference's semantics on the host cores (oracle/cpu_port.py): K_cpu single-draw losses per
@@ -195,7 +213,7 @@ def cpu_baseline(name, budget_s=12.0):
         cpu_port.k_particle_step(w["conditioned"](), w["guide"], optimizer, k_cpu)
         steps += 1
         elapsed = time.perf_counter() - start
-        if elapsed > budget_s or steps >= 200:
+        if elapsed > budget_s or steps >= 2000:
             break
     rate = evals_per_particle * k_cpu * steps / elapsed
     model_name = ""
@@ -335,15 +353,19 @@ def main():
     else:
         if w["bytes_per_eval"] is None:
             nbytes = c5_bytes(w)
-            kname = "k_group_row (z, y, b fused site group)"
+            kname = "mi_site_program (fused z, y, b site group; row layout)"
         else:
             nbytes = w["bytes_per_eval"] * w["k_local"] * w["n"] + 8.0 * w["n"]
-            kname = "k_group_col (Normal(X@theta, 1) site)"
+            kname = "mi_site_program (Normal(X@theta, 1) site; column layout)"
         achieved = nbytes / kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,
                 "kernel_ms": kernel_ms, "launches_timed": launches,
                 "algorithmic_per_launch": f"{nbytes:.4g} B"}
+    traffic, source = measured_traffic(args.config)
+    roof["traffic"] = traffic
+    if traffic is not None:
+        roof["traffic_source"] = f"{source} (rocprofv3 --pmc, bytes per launch)"
     out = {
         "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",

@@ -12,10 +12,12 @@
 // finish (device-scope counter, reset by that block) adds the partials in block order.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace mi {
 
 constexpr int kElboThreads = 256;
-constexpr int kElboMaxBlocks = 512;
+constexpr int kElboMaxBlocks = 1024;
 
 // Trigamma psi'(x), x > 0: recurrence up to x >= 6, then the asymptotic series
 // 1/x + 1/(2x^2) + sum_k B_2k / x^(2k+1).
@@ -35,19 +37,20 @@ MI_DEV double trigamma(double x) {
 // Entropy of element i of factor f, and its partial derivatives w.r.t. the factor's parameters.
 MI_DEV double factor_entropy(const mi_factor& f, int64_t i, double* d0, double* d1) {
   if (f.family == MI_NORMAL) {
-    // 0.5 + 0.5 log(2 pi) + log(scale)   (normal.py:112-113)
-    const double s = (double)f.param[1][i * f.stride[1]];
+    // 0.5 + 0.5 log(2 pi) + log(scale) in fp32 as torch evaluates it (normal.py:112-113); the
+    // sum over elements is carried in fp64.
+    const float s = f.param[1][i * f.stride[1]];
     if (d0 != nullptr) {
       *d0 = 0.0;
-      *d1 = 1.0 / s;
+      *d1 = (double)(1.0f / s);
     }
-    return 0.5 + 0.91893853320467274178 + log(s);
+    return (double)(1.4189385332046727f + logf(s));
   }
   // Beta(a, b) = Dirichlet([a, b]) (dirichlet.py:122-130 with k = 2, a0 = a + b):
   //   lgamma(a) + lgamma(b) - lgamma(a0) - (2 - a0) psi(a0) - (a - 1) psi(a) - (b - 1) psi(b)
-  const double a = (double)f.param[0][i * f.stride[0]];
-  const double b = (double)f.param[1][i * f.stride[1]];
-  const double t = (double)((float)f.param[0][i * f.stride[0]] + f.param[1][i * f.stride[1]]);
+  const float af = f.param[0][i * f.stride[0]], bf = f.param[1][i * f.stride[1]];
+  const double a = (double)af, b = (double)bf;
+  const double t = (double)(af + bf);  // concentration.sum(-1) in fp32
   if (d0 != nullptr) {
     const double tt = (t - 2.0) * trigamma(t);
     *d0 = -(a - 1.0) * trigamma(a) + tt;
@@ -55,16 +58,6 @@ MI_DEV double factor_entropy(const mi_factor& f, int64_t i, double* d0, double* 
   }
   return lgamma(a) + lgamma(b) - lgamma(t) - (2.0 - t) * digamma(t) - (a - 1.0) * digamma(a) -
          (b - 1.0) * digamma(b);
-}
-
-// Factor index and element of unit u (u counts the elements of all factors in order).
-MI_DEV int locate(const mi_elbo& E, int64_t& u) {
-  int f = 0;
-  while (f + 1 < E.num_factors && u >= E.factors[f].n) {
-    u -= E.factors[f].n;
-    ++f;
-  }
-  return f;
 }
 
 MI_DEV double block_sum(double v, double* red) {
@@ -78,26 +71,21 @@ MI_DEV double block_sum(double v, double* red) {
   return s;
 }
 
-__global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, int64_t term_units,
-                                                               int64_t units,
-                                                               double* partial,
+__global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, double* partial,
                                                                unsigned* __restrict__ counter,
                                                                float* __restrict__ loss) {
   __shared__ double red[kElboThreads / kWave];
   __shared__ bool last;
-  double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * kElboThreads;
-  for (int64_t u = (int64_t)blockIdx.x * kElboThreads + threadIdx.x; u < units; u += stride) {
-    if (u < term_units) {
-      const int64_t t = u / E.K, k = u - t * E.K;
-      acc += (double)E.g0 * (double)E.terms[t][k];
-    } else {
-      int64_t i = u - term_units;
-      const int f = locate(E, i);
-      acc -= E.entropy_scale * factor_entropy(E.factors[f], i, nullptr, nullptr);
-    }
+  const int64_t first = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
+  double lp = 0.0, h = 0.0;
+  for (int t = 0; t < E.num_terms; ++t)
+    for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
+  for (int f = 0; f < E.num_factors; ++f) {
+    const mi_factor& F = E.factors[f];
+    for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i, nullptr, nullptr);
   }
-  const double s = block_sum(acc, red);
+  const double s = block_sum((double)E.g0 * lp - E.entropy_scale * h, red);
   if (threadIdx.x == 0) {
     partial[blockIdx.x] = s;
     __threadfence();
@@ -114,7 +102,6 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, 
 }
 
 __global__ __launch_bounds__(kElboThreads) void k_elbo_backward(const mi_elbo E,
-                                                                int64_t factor_units,
                                                                 const float* __restrict__ upstream,
                                                                 float* __restrict__ dterm) {
   const float u = *upstream;
@@ -123,14 +110,14 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_backward(const mi_elbo E,
   if (first == 0) dterm[0] = u * E.g0;
   // d loss / d param = -u * entropy_scale * dH / d param
   const double w = -(double)u * E.entropy_scale;
-  for (int64_t v = first; v < factor_units; v += stride) {
-    int64_t i = v;
-    const int f = locate(E, i);
+  for (int f = 0; f < E.num_factors; ++f) {
     const mi_factor& F = E.factors[f];
-    double d0, d1;
-    factor_entropy(F, i, &d0, &d1);
-    if (F.grad[0] != nullptr) F.grad[0][i * F.stride[0]] = (float)(w * d0);
-    if (F.grad[1] != nullptr) F.grad[1][i * F.stride[1]] = (float)(w * d1);
+    for (int64_t i = first; i < F.n; i += stride) {
+      double d0, d1;
+      factor_entropy(F, i, &d0, &d1);
+      if (F.grad[0] != nullptr) F.grad[0][i * F.stride[0]] = (float)(w * d0);
+      if (F.grad[1] != nullptr) F.grad[1][i * F.stride[1]] = (float)(w * d1);
+    }
   }
   if (u == 1.0f) return;  // the site groups' gradients were computed for exactly this upstream
   for (int b = 0; b < E.num_buffers; ++b) {
@@ -164,16 +151,20 @@ bool valid(const mi_elbo* e) {
   return true;
 }
 
-int64_t factor_units(const mi_elbo* e) {
-  int64_t n = 0;
-  for (int f = 0; f < e->num_factors; ++f) n += e->factors[f].n;
+// Enough blocks that each thread handles about four elements of the longest term or factor.
+unsigned blocks_for(int64_t longest, int64_t cap) {
+  return (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(cap, ceil_div(longest, 4 * mi::kElboThreads)));
+}
+
+int64_t longest_factor(const mi_elbo* e) {
+  int64_t n = 1;
+  for (int f = 0; f < e->num_factors; ++f) n = std::max(n, e->factors[f].n);
   return n;
 }
 
 unsigned forward_blocks(const mi_elbo* e) {
-  const int64_t units = (int64_t)e->num_terms * e->K + factor_units(e);
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(mi::kElboMaxBlocks,
-                                                          ceil_div(units, 4 * mi::kElboThreads)));
+  return blocks_for(std::max(e->K, longest_factor(e)), mi::kElboMaxBlocks);
 }
 
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
@@ -206,25 +197,20 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
   size_t need = 0;
   mi_elbo_workspace_bytes(elbo, &need);
   if (workspace_bytes < need) return MI_EWORKSPACE;
-  const unsigned blocks = forward_blocks(elbo);
-  const int64_t term_units = (int64_t)elbo->num_terms * elbo->K;
-  const int64_t units = term_units + factor_units(elbo);
   auto* counter = static_cast<unsigned*>(workspace);
   auto* partial = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256);
-  hipLaunchKernelGGL(mi::k_elbo_forward, dim3(blocks), dim3(mi::kElboThreads), 0,
-                     static_cast<hipStream_t>(stream), *elbo, term_units, units, partial, counter,
-                     loss);
+  hipLaunchKernelGGL(mi::k_elbo_forward, dim3(forward_blocks(elbo)), dim3(mi::kElboThreads), 0,
+                     static_cast<hipStream_t>(stream), *elbo, partial, counter, loss);
   return to_code(hipGetLastError());
 }
 
 int mi_elbo_backward(const mi_elbo* elbo, const float* upstream, float* dterm, void* stream) {
   if (!valid(elbo) || upstream == nullptr || dterm == nullptr) return MI_EINVAL;
-  int64_t longest = factor_units(elbo);
+  int64_t longest = longest_factor(elbo);
   for (int b = 0; b < elbo->num_buffers; ++b) longest = std::max(longest, elbo->buffer_len[b]);
-  const unsigned blocks = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>(2048, ceil_div(longest, 4 * mi::kElboThreads)));
-  hipLaunchKernelGGL(mi::k_elbo_backward, dim3(blocks), dim3(mi::kElboThreads), 0,
-                     static_cast<hipStream_t>(stream), *elbo, factor_units(elbo), upstream, dterm);
+  hipLaunchKernelGGL(mi::k_elbo_backward, dim3(blocks_for(longest, 2048)),
+                     dim3(mi::kElboThreads), 0, static_cast<hipStream_t>(stream), *elbo, upstream,
+                     dterm);
   return to_code(hipGetLastError());
 }
 
