@@ -212,6 +212,8 @@ __global__ __launch_bounds__(256) void k_group_col(const mi_group G, float* __re
 // -------------------------------------------------------------------------------------------------
 // BCAST: one site, parameters are per-particle scalars (or constants), the value is shared data.
 // -------------------------------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 constexpr int kBcastThreads = 256;
 constexpr int kBcastP = 8;          // particles per lane
 constexpr int kBcastChunk = 2048;   // elements staged per block
@@ -235,14 +237,69 @@ MI_DEV float block_sum(float v, float* scratch) {
   return out;
 }
 
+// Per-particle constants of a BCAST site, computed once per particle (not once per element chunk):
+//   Bernoulli: l, dl/dparam, softplus(l), sigmoid(l)
+//   Normal:    loc, scale, log(scale) + log sqrt(2 pi)
+//   Beta:      a - 1, b - 1, lgamma(a + b) - lgamma(a) - lgamma(b), psi(a+b) - psi(a), psi(a+b) - psi(b)
+// laid out as prep[j * K + k]; parameter-constraint violations are flagged here.
+constexpr int kPrep = 5;
+
+template <int FAMILY>
+__global__ __launch_bounds__(256) void k_bcast_prep(const mi_group G, float* __restrict__ prep,
+                                                    uint32_t* __restrict__ flags) {
+  const mi_site& st = G.sites[0];
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t fl = 0u;
+  if (k < G.K) {
+    const float a = role_scalar(G, st, 0, k), b = role_scalar(G, st, 1, k);
+    float c[kPrep] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    bool bad;
+    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+      float l = a, dl = 1.0f;
+      if (FAMILY == MI_BERNOULLI_PROBS) {
+        bad = !(a >= 0.0f && a <= 1.0f);
+        bernoulli_probs_to_logits(a, l, dl);
+      } else {
+        bad = l != l;
+      }
+      // log p(x | l) = x l - softplus(l);  d/dl = x - sigmoid(l)   (bernoulli.py:121-125)
+      const float t = expf(-fabsf(l));
+      c[0] = l;
+      c[1] = dl;
+      c[2] = fmaxf(l, 0.0f) + log1pf(t);
+      c[3] = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
+    } else if (FAMILY == MI_NORMAL) {
+      bad = !(b > 0.0f) || (a != a);
+      c[0] = a;
+      c[1] = b;
+      c[2] = (float)((double)logf(b) + (double)kHalfLog2Pi);
+    } else {
+      bad = !(a > 0.0f) || !(b > 0.0f);
+      const double psi_ab = digamma((double)a + (double)b);
+      c[0] = a - 1.0f;
+      c[1] = b - 1.0f;
+      c[2] = (float)((double)lgammaf(a + b) - (double)lgammaf(a) - (double)lgammaf(b));
+      c[3] = (float)(psi_ab - digamma((double)a));
+      c[4] = (float)(psi_ab - digamma((double)b));
+    }
+    fl = bad ? MI_FLAG_PARAM : 0u;
+#pragma unroll
+    for (int j = 0; j < kPrep; ++j) prep[j * G.K + k] = c[j];
+  }
+  publish_flags(flags, fl);
+}
+
 // FAMILY in {MI_BERNOULLI_LOGITS, MI_BERNOULLI_PROBS, MI_NORMAL, MI_BETA}
 template <int FAMILY, bool MASKED>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
+                                                              const float* __restrict__ prep,
                                                               float* __restrict__ part,
                                                               int64_t nchunk,
                                                               uint32_t* __restrict__ flags) {
-  constexpr int NF = (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) ? 1 : 2;
-  __shared__ float4 feat[NF][kBcastChunk / 4];
+  constexpr bool BERN = FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS;
+  constexpr int NF = BERN ? 1 : 2;
+  // Bernoulli stages each value twice, (x, x), so a 16-byte LDS read feeds packed FMAs directly.
+  __shared__ float4 feat[NF][BERN ? kBcastChunk / 2 : kBcastChunk / 4];
   __shared__ float scratch[kBcastThreads / 64];
   __shared__ float sums[4];
 
@@ -269,7 +326,8 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
     if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
       fl |= (obs && !(v == 0.0f || v == 1.0f)) ? MI_FLAG_SUPPORT : 0u;
       const float f = obs ? v : 0.0f;
-      f0[j] = f;
+      f0[2 * j] = f;
+      f0[2 * j + 1] = f;
       s_a += f;
     } else if (FAMILY == MI_NORMAL) {
       fl |= (obs && v != v) ? MI_FLAG_SUPPORT : 0u;
@@ -301,37 +359,14 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
 
   // ---- per-particle element loop -------------------------------------------------------------
   const int64_t kbase = (int64_t)blockIdx.y * (kBcastThreads * kBcastP) + threadIdx.x;
-  float pa[kBcastP], pb[kBcastP];
-  uint32_t pbad = 0u;
-#pragma unroll
-  for (int p = 0; p < kBcastP; ++p) {
-    const int64_t k = min(kbase + p * kBcastThreads, G.K - 1);
-    pa[p] = role_scalar(G, st, 0, k);
-    pb[p] = role_scalar(G, st, 1, k);
-  }
-  // Hoisted per-particle coefficients of the element loop.
+  // Hoisted per-particle coefficients of the element loop (k_bcast_prep).
+  const int64_t K = G.K;
   float ca[kBcastP], cb[kBcastP];
 #pragma unroll
   for (int p = 0; p < kBcastP; ++p) {
-    if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
-      float l = pa[p], dl = 1.0f;
-      if (FAMILY == MI_BERNOULLI_PROBS) {
-        pbad |= !(pa[p] >= 0.0f && pa[p] <= 1.0f);
-        bernoulli_probs_to_logits(pa[p], l, dl);
-      } else {
-        pbad |= (l != l);
-      }
-      ca[p] = l;
-      cb[p] = dl;
-    } else if (FAMILY == MI_NORMAL) {
-      pbad |= !(pb[p] > 0.0f) || (pa[p] != pa[p]);
-      ca[p] = pa[p];
-      cb[p] = 0.0f;
-    } else {
-      pbad |= !(pa[p] > 0.0f) || !(pb[p] > 0.0f);
-      ca[p] = pa[p] - 1.0f;
-      cb[p] = pb[p] - 1.0f;
-    }
+    const int64_t k = min(kbase + p * kBcastThreads, K - 1);
+    ca[p] = prep[k];
+    cb[p] = prep[K + k];
   }
 
   double acc1[kBcastP], acc2[kBcastP];
@@ -376,6 +411,55 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
 
   const int nq = (int)((len + 3) / 4);
   const int full = (int)(len / 4) & ~15;
+  if constexpr (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
+    // x l summed over the chunk for 8 particles: packed FMAs (v_pk_fma_f32) on particle pairs,
+    // two evals per lane per instruction. The zero padding of the last quad is neutral.
+    f32x2 cav[kBcastP / 2];
+#pragma unroll
+    for (int j = 0; j < kBcastP / 2; ++j) cav[j] = f32x2{ca[2 * j], ca[2 * j + 1]};
+    // feat[0][j] = (x_2j, x_2j, x_2j+1, x_2j+1); the chunk's zero padding is neutral.
+    const int npair = (int)((len + 1) / 2);
+    for (int j0 = 0; j0 < npair; j0 += 64) {
+      // two accumulator sets (even / odd elements): 8 independent FMA chains per lane, flushed to
+      // fp64 every 128 elements
+      f32x2 in[2][kBcastP / 2];
+#pragma unroll
+      for (int j = 0; j < kBcastP / 2; ++j) in[0][j] = in[1][j] = f32x2{0.0f, 0.0f};
+      if (j0 + 64 <= npair) {
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          float4 xs[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xs[j] = feat[0][j0 + 8 * h + j];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x2 xa = f32x2{xs[j].x, xs[j].y}, xb = f32x2{xs[j].z, xs[j].w};
+#pragma unroll
+            for (int pp = 0; pp < kBcastP / 2; ++pp) {
+              in[0][pp] = __builtin_elementwise_fma(xa, cav[pp], in[0][pp]);
+              in[1][pp] = __builtin_elementwise_fma(xb, cav[pp], in[1][pp]);
+            }
+          }
+        }
+      } else {
+        for (int j = j0; j < npair; ++j) {
+          const float4 x = feat[0][j];
+          const f32x2 xa = f32x2{x.x, x.y}, xb = f32x2{x.z, x.w};
+#pragma unroll
+          for (int pp = 0; pp < kBcastP / 2; ++pp) {
+            in[0][pp] = __builtin_elementwise_fma(xa, cav[pp], in[0][pp]);
+            in[1][pp] = __builtin_elementwise_fma(xb, cav[pp], in[1][pp]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kBcastP / 2; ++j) {
+        const f32x2 t = in[0][j] + in[1][j];
+        acc1[2 * j] += (double)t.x;
+        acc1[2 * j + 1] += (double)t.y;
+      }
+    }
+  } else {
   for (int q0 = 0; q0 < full; q0 += 16) {
     float in1[kBcastP], in2[kBcastP];
 #pragma unroll
@@ -412,6 +496,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
       acc2[p] += (double)in2[p];
     }
   }
+  }
 
   // ---- epilogue: constant parts, gradients, partial writes -------------------------------------
   const int o_a = st.operand[0], o_b = st.operand[1];
@@ -425,29 +510,27 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
     const int64_t k = kbase + p * kBcastThreads;
     double lp = 0.0;
     float ga = 0.0f, gb = 0.0f;
+    const int64_t kc = min(k, K - 1);
     if (FAMILY == MI_BERNOULLI_LOGITS || FAMILY == MI_BERNOULLI_PROBS) {
-      const float l = ca[p];
-      const float t = expf(-fabsf(l));
-      const float softplus = fmaxf(l, 0.0f) + log1pf(t);
-      const float sig = l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t);
-      lp = acc1[p] - M * (double)softplus;
-      ga = (float)(((double)s_a - M * (double)sig) * (double)cb[p]);
+      const double softplus = prep[2 * K + kc], sig = prep[3 * K + kc];
+      lp = acc1[p] - M * softplus;
+      ga = (float)(((double)s_a - M * sig) * (double)cb[p]);
     } else if (FAMILY == MI_NORMAL) {
-      const double sigma = pb[p];
+      const double sigma = cb[p];
       const double inv2 = 1.0 / (sigma * sigma);
-      lp = -0.5 * acc2[p] * inv2 - M * ((double)logf(pb[p]) + (double)kHalfLog2Pi);
+      lp = -0.5 * acc2[p] * inv2 - M * (double)prep[2 * K + kc];
       ga = (float)(acc1[p] * inv2);
       gb = (float)(acc2[p] * inv2 / sigma - M / sigma);
     } else {
-      const double a = pa[p], b = pb[p];
-      const double psi_ab = digamma(a + b);
-      double base = acc1[p] + M * ((double)lgammaf(pa[p] + pb[p]) - (double)lgammaf(pa[p]) - (double)lgammaf(pb[p]));
+      double base = acc1[p] + M * (double)prep[2 * K + kc];
       // xlogy semantics for exact 0 / 1 values (dirichlet.py:94)
       if (s_zero > 0.0f && ca[p] != 0.0f) base += ca[p] > 0.0f ? -__builtin_inf() : __builtin_inf();
       if (s_one > 0.0f && cb[p] != 0.0f) base += cb[p] > 0.0f ? -__builtin_inf() : __builtin_inf();
       lp = base;
-      ga = (float)((double)s_a + M * (psi_ab - digamma(a)) - (s_zero > 0.0f ? __builtin_inf() : 0.0));
-      gb = (float)((double)s_b + M * (psi_ab - digamma(b)) - (s_one > 0.0f ? __builtin_inf() : 0.0));
+      ga = (float)((double)s_a + M * (double)prep[3 * K + kc] -
+                   (s_zero > 0.0f ? __builtin_inf() : 0.0));
+      gb = (float)((double)s_b + M * (double)prep[4 * K + kc] -
+                   (s_one > 0.0f ? __builtin_inf() : 0.0));
     }
     if (k < G.K) {
       part[((int64_t)0 * nchunk + c) * G.K + k] = (float)lp;
@@ -455,7 +538,6 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
       if (slot_b >= 0) part[((int64_t)(1 + slot_b) * nchunk + c) * G.K + k] = w * gb;
     }
   }
-  fl |= pbad ? MI_FLAG_PARAM : 0u;
   publish_flags(flags, fl);
 }
 
@@ -716,6 +798,16 @@ size_t partial_bytes(const mi_group* g, const Plan& p) {
   return (size_t)nv * (size_t)p.nseg * (size_t)g->K * sizeof(float);
 }
 
+// BCAST groups also hold the per-particle constants after the (256-byte aligned) partials.
+size_t prep_offset(const mi_group* g, const Plan& p) {
+  return (partial_bytes(g, p) + 255) / 256 * 256;
+}
+
+size_t workspace_bytes(const mi_group* g, const Plan& p) {
+  if (p.shape != kBcast) return partial_bytes(g, p);
+  return prep_offset(g, p) + (size_t)mi::kPrep * (size_t)g->K * sizeof(float);
+}
+
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 }  // namespace
@@ -743,7 +835,7 @@ int mi_struct_sizes(size_t* operand, size_t* site, size_t* group) {
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
   if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
-  *bytes = partial_bytes(group, p);
+  *bytes = workspace_bytes(group, p);
   return 0;
 }
 
@@ -759,7 +851,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   if (!validate_group(group) || total == nullptr || flags == nullptr) return MI_EINVAL;
   if (group->num_slots > 0 && slot_grad == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
-  if (workspace_bytes < partial_bytes(group, p) || workspace == nullptr) return MI_EWORKSPACE;
+  if (workspace_bytes < ::workspace_bytes(group, p) || workspace == nullptr) return MI_EWORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(workspace);
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
@@ -770,6 +862,25 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   const bool combined = site_lp == nullptr;
   int reduced_lp = G.num_sites;
   bool prescaled = false;  // partials already carry the site scales
+  float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
+  if (p.shape == kBcast) {
+    const dim3 pg((unsigned)ceil_div(G.K, 256));
+    switch (G.sites[0].family) {
+      case MI_BERNOULLI_LOGITS:
+        hipLaunchKernelGGL((mi::k_bcast_prep<MI_BERNOULLI_LOGITS>), pg, dim3(256), 0, s, G, prep, flags);
+        break;
+      case MI_BERNOULLI_PROBS:
+        hipLaunchKernelGGL((mi::k_bcast_prep<MI_BERNOULLI_PROBS>), pg, dim3(256), 0, s, G, prep, flags);
+        break;
+      case MI_NORMAL:
+        hipLaunchKernelGGL((mi::k_bcast_prep<MI_NORMAL>), pg, dim3(256), 0, s, G, prep, flags);
+        break;
+      case MI_BETA:
+        hipLaunchKernelGGL((mi::k_bcast_prep<MI_BETA>), pg, dim3(256), 0, s, G, prep, flags);
+        break;
+      default: return MI_EUNSUPPORTED;
+    }
+  }
   if (start_event != nullptr) {
     e = hipEventRecord(static_cast<hipEvent_t>(start_event), s);
     if (e != hipSuccess) return to_code(e);
@@ -782,10 +893,10 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   case FAM:                                                                                    \
     if (masked)                                                                                \
       hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), 0, s, \
-                         G, part, p.nseg, flags);                                              \
+                         G, prep, part, p.nseg, flags);                                        \
     else                                                                                       \
       hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), 0,   \
-                         s, G, part, p.nseg, flags);                                           \
+                         s, G, prep, part, p.nseg, flags);                                     \
     break;
         MI_LAUNCH_BCAST(MI_BERNOULLI_LOGITS)
         MI_LAUNCH_BCAST(MI_BERNOULLI_PROBS)
