@@ -58,6 +58,10 @@ enum mi_grad_mode {
 };
 
 /* flag bits reported per site */
+/* mi_group.options: the caller has zeroed `flags` (e.g. one buffer for every group of a step),
+ * so mi_group_forward does not reset them. */
+#define MI_GROUP_FLAGS_ZEROED 1
+
 #define MI_FLAG_SUPPORT 1u  /* a (non-masked) value lies outside the family's support */
 #define MI_FLAG_PARAM 2u    /* a parameter violates its constraint (e.g. scale <= 0) */
 
@@ -94,7 +98,7 @@ typedef struct mi_group {
   int32_t num_slots;
   int32_t compute_grads; /* 0: forward values only */
   float grad_scale;      /* g0: upstream dL/dT_k assumed for MI_GRAD_DENSE / PARTICLE outputs */
-  int32_t pad0;
+  int32_t options;       /* MI_GROUP_* bits */
   mi_site sites[MI_MAX_SITES];
   mi_operand operands[MI_MAX_OPERANDS];
 } mi_group;
@@ -115,7 +119,8 @@ int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);
  *   site_lp[s*K + k]      = scale_s * sum_i mask_si * log p_s(...)  (fp64; may be NULL)
  *   slot_grad[j*K + k]    = g0 * dT_k / d x[k] for MI_GRAD_PARTICLE operands in slot j (fp32)
  *   operands[o].grad      = g0 * dT_k / d x[k,i] for MI_GRAD_DENSE operands
- *   flags[s]              = OR of MI_FLAG_* found for site s (zeroed by this call)
+ *   flags[s]              = OR of MI_FLAG_* found for site s (zeroed by this call unless
+ *                           options has MI_GROUP_FLAGS_ZEROED)
  * Replaces LogProbTracer.sample's dist.log_prob (core.py:241, masked branch core.py:231-239),
  * LogProbTracer.total/contribution (core.py:247-273) and the autograd backward of the same ops. */
 int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,

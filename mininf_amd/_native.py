@@ -27,6 +27,7 @@ MAX_BUFFERS = 16
 
 NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
+GROUP_FLAGS_ZEROED = 1
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -56,7 +57,7 @@ class Group(ctypes.Structure):
         ("K", c_i64), ("N", c_i64),
         ("num_sites", ctypes.c_int32), ("num_operands", ctypes.c_int32),
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
-        ("grad_scale", ctypes.c_float), ("pad0", ctypes.c_int32),
+        ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
     ]
 

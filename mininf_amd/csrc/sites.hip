@@ -854,8 +854,11 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   if (workspace_bytes < ::workspace_bytes(group, p) || workspace == nullptr) return MI_EWORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(workspace);
-  hipError_t e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
-  if (e != hipSuccess) return to_code(e);
+  hipError_t e = hipSuccess;
+  if (!(group->options & MI_GROUP_FLAGS_ZEROED)) {
+    e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
+    if (e != hipSuccess) return to_code(e);
+  }
   const mi_group G = *group;
   // Without a per-site output the specialised kernels reduce one weighted log-joint value per
   // particle instead of one per site.

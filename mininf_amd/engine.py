@@ -258,7 +258,11 @@ class _GroupLauncher:
             raise nat.NativeError("site program failed to compile:\n" + log.value.decode())
         return log.value.decode()
 
-    def run(self, compute_grads: bool):
+    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None):
+        """
+        Launch the group. ``flags``: an already-zeroed int32 slice (one word per site) to write the
+        validation flags into, e.g. part of one buffer for every group of a step.
+        """
         device = self.device
         K, N = self.K, self.N
         group, grads = self.describe(compute_grads)
@@ -271,7 +275,10 @@ class _GroupLauncher:
         site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device) \
             if self.per_site else None
         slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
-        flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
+        if flags is None:
+            flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
+        else:
+            group.options |= nat.GROUP_FLAGS_ZEROED
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
@@ -329,7 +336,8 @@ class _SiteGroupFn(torch.autograd.Function):
 
 
 def _run_categorical(site: SiteRecord, g0: float, logits: torch.Tensor, value: torch.Tensor,
-                     mask: Optional[torch.Tensor], need: bool):
+                     mask: Optional[torch.Tensor], need: bool,
+                     flags: Optional[torch.Tensor] = None):
     """
     Launch ``mi_categorical_forward``: (total [K], speculative dlogits or None, flags [1]).
     """
@@ -342,7 +350,8 @@ def _run_categorical(site: SiteRecord, g0: float, logits: torch.Tensor, value: t
               "mi_categorical_workspace_bytes")
     workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
     total = torch.empty(K, dtype=torch.float32, device=device)
-    flags = torch.empty(1, dtype=torch.int32, device=device)
+    if flags is None:
+        flags = torch.empty(1, dtype=torch.int32, device=device)
     nat.check(lib.mi_categorical_forward(
         logits.data_ptr(), logits.stride(0), logits.stride(1), logits.stride(2), K, N, C,
         value.data_ptr(), value.stride(0), value.stride(1),
@@ -384,15 +393,21 @@ class LogJoint:
     total: torch.Tensor                       # [K] fp32, differentiable
     pending: List[Tuple[str, dict, List[SiteRecord]]]
     checks: list
+    flags: Optional[torch.Tensor] = None      # int32, one word per pending site, in order
 
     def flag_vector(self) -> Optional[torch.Tensor]:
         """
         All validation results of the step as one int64 device vector: one MI_FLAG_* word per
         kernel-evaluated site, then one 0/1 per deferred support / constraint check.
         """
+        if self.flags is not None and not self.checks:
+            return self.flags
         parts = []
-        for _, holder, _ in self.pending:
-            parts.append(holder["flags"].reshape(-1).to(torch.int64))
+        if self.flags is not None:
+            parts.append(self.flags.to(torch.int64))
+        else:
+            for _, holder, _ in self.pending:
+                parts.append(holder["flags"].reshape(-1).to(torch.int64))
         for _, ok in self.checks:
             parts.append((~ok.reshape(-1).bool()).any().reshape(1).to(torch.int64))
         return torch.cat(parts) if parts else None
@@ -562,6 +577,7 @@ class _ElboPlan:
         self.entropy_scale = entropy_scale
         self.holders = [dict() for _ in launchers]
         self.cat_holders = [dict() for _ in categorical]
+        self.flags: Optional[torch.Tensor] = None
         self.state = None
 
     def inputs(self) -> List[Optional[torch.Tensor]]:
@@ -603,9 +619,15 @@ class _ElboPlan:
         terms: List[torch.Tensor] = []
         buffers: List[torch.Tensor] = []
         results = []
+        # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
+        sizes = [1] * len(self.categorical) + [len(l.sites) for l in self.launchers]
+        self.flags = torch.zeros(max(1, sum(sizes)), dtype=torch.int32, device=self.device)
+        cursor = len(self.categorical)
         for launcher, holder in zip(self.launchers, self.holders):
             need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
-            total, site_lp, grads, slot_grad, flags = launcher.run(need)
+            part = self.flags[cursor:cursor + len(launcher.sites)]
+            cursor += len(launcher.sites)
+            total, site_lp, grads, slot_grad, flags = launcher.run(need, part)
             holder["flags"], holder["site_lp"] = flags, site_lp
             terms.append(total)
             if need:
@@ -614,9 +636,10 @@ class _ElboPlan:
                     buffers.append(slot_grad[:launcher.num_slots])
             results.append((grads, slot_grad))
         cat_results = []
-        for (site, lg, val, mask), holder in zip(self.categorical, self.cat_holders):
+        for j, ((site, lg, val, mask), holder) in enumerate(zip(self.categorical,
+                                                                 self.cat_holders)):
             total, dlogits, flags = _run_categorical(site, self.g0, lg, val, mask,
-                                                     lg.requires_grad)
+                                                     lg.requires_grad, self.flags[j:j + 1])
             holder["flags"] = flags
             terms.append(total)
             if dlogits is not None:
@@ -735,4 +758,4 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         pending.append(("categorical", holder, [site]))
     for launcher, holder in zip(launchers, plan.holders):
         pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
-    return loss, LogJoint(total=loss, pending=pending, checks=trace.checks)
+    return loss, LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)

@@ -130,7 +130,9 @@ class StepGraph:
             self.output = step()
             flags = [joint.flag_vector() for joint in self._joints]
             flags = [f for f in flags if f is not None]
-            self._flags_device = torch.cat(flags) if flags else None
+            if len(flags) > 1:
+                flags = [torch.cat([f.to(torch.int64) for f in flags])]
+            self._flags_device = flags[0] if flags else None
         # Pinned host memory cannot be allocated while capturing: the copy of the flags is enqueued
         # after each replay instead (one small asynchronous D2H copy).
         self._flags_host = None

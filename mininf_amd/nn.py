@@ -35,6 +35,23 @@ def _is_identity_transform(transform: distributions.Transform) -> bool:
     return isinstance(transform, torch.distributions.ComposeTransform) and not transform.parts
 
 
+def _forward_transform(transform: distributions.Transform) -> distributions.Transform:
+    """
+    The transform to apply in ``forward``: ``transform_to(positive)`` is
+    ``ComposeTransform([ExpTransform(), AffineTransform(0., 1)])`` and ``0 + 1 * exp(u)`` is
+    ``exp(u)`` exactly (same values and gradients), so the affine no-op -- two kernels forward and
+    one backward per parameter -- is dropped.
+    """
+    if isinstance(transform, distributions.ComposeTransform) and len(transform.parts) == 2:
+        first, second = transform.parts
+        if isinstance(first, distributions.ExpTransform) and \
+                isinstance(second, distributions.AffineTransform) and \
+                isinstance(second.loc, (int, float)) and second.loc == 0 and \
+                isinstance(second.scale, (int, float)) and second.scale == 1:
+            return first
+    return transform
+
+
 class ParameterizedDistribution(nn.Module):
     """
     Distribution whose (constrained) parameters are learnable; they are stored unconstrained via
@@ -80,9 +97,11 @@ class ParameterizedDistribution(nn.Module):
         arguments = {}
         for name, unconstrained in self.distribution_parameters.items():
             transform = distributions.transform_to(constraints[name])
-            # `1 *` so the distribution never exposes the nn.Parameter itself.
-            arguments[name] = 1 * unconstrained if _is_identity_transform(transform) \
-                else transform(unconstrained)
+            # The reference exposes `1 * value` so the distribution never holds the nn.Parameter
+            # itself (nn.py:92-94); a view is likewise a distinct tensor and costs no kernel.
+            arguments[name] = unconstrained.view_as(unconstrained) \
+                if _is_identity_transform(transform) \
+                else _forward_transform(transform)(unconstrained)
         return self.distribution_cls(**arguments, **self.distribution_constants)  # type: ignore
 
 
