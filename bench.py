@@ -240,6 +240,9 @@ def main():
     ap.add_argument("--eager", dest="graph", action="store_false",
                     help="launch every step from Python instead of replaying a captured hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo lets "
+                         "several ranks share one GPU to exercise the sharded path)")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile 20 extra steps and print the hottest host functions to stderr")
     args = ap.parse_args()
@@ -247,12 +250,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(device)
     group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
         group = dist.group.WORLD
 
     w = workload(args.config, device, world, rank)
@@ -372,8 +378,9 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": w["data"],
         "config": {"workload": w["desc"], "particles_per_gpu": w["k_local"],
                    "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
-                   "parallelism": f"particle-sharded x{world}" + (" + RCCL grad all-reduce"
-                                                                  if world > 1 else ""),
+                   "parallelism": f"particle-sharded x{world}" + (
+                       (" + RCCL grad all-reduce" if args.dist_backend == "nccl" else
+                        f" + {args.dist_backend} grad all-reduce") if world > 1 else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms},
         "roofline": roof,

@@ -257,11 +257,41 @@ def _guide_device(approximation: Dict[str, torch.distributions.Distribution]) ->
 
 class LogLikelihoodLoss(nn.Module):
     """
-    Negative log likelihood at fixed parameter values (reference ``nn.py:231-257``), evaluated by
-    the reference-semantics :class:`~mininf_amd.core.LogProbTracer`.
+    Negative log likelihood at fixed parameter values (reference ``nn.py:231-257``).
+
+    When the parameters live on a ROCm device, the model is traced with the particle tracer at
+    K = 1 and every kernel-family site is evaluated by the same HIP site kernels as the ELBO
+    (``mi_group_forward``; speculative gradients for the upstream -1). Host (CPU) parameters keep
+    the reference's torch-CPU evaluation through :class:`~mininf_amd.core.LogProbTracer`.
+
+    Example:
+
+        >>> from mininf_amd import sample
+        >>> from mininf_amd.nn import LogLikelihoodLoss
+        >>> from torch.distributions import Normal
+        >>> def model() -> None:
+        ...     sample("x", Normal(0, 1))
+        >>> LogLikelihoodLoss()(model, {"x": 0.1})
+        tensor(0.9239)
     """
     def forward(self, model: Callable, parameters: TensorDict) -> torch.Tensor:
         """"""
-        with LogProbTracer() as log_prob:
-            condition(model, **parameters)()
-        return - log_prob.total
+        device = next((v.device for v in parameters.values()
+                       if isinstance(v, torch.Tensor) and v.is_cuda), None)
+        if device is None:
+            with LogProbTracer() as log_prob:
+                condition(model, **parameters)()
+            return - log_prob.total
+        samples = {}
+        for name, value in parameters.items():
+            if not isinstance(value, torch.Tensor):
+                value = torch.as_tensor(value, dtype=torch.get_default_dtype(), device=device)
+            samples[name] = value.unsqueeze(0)
+        trace = particles.trace_particles(model, samples, 1)
+        joint = engine.log_joint(trace, -1.0, device)
+        collector = graph.deferred()
+        if collector is not None:
+            collector.append(joint)
+        else:
+            joint.raise_on_violation()
+        return - joint.total[0]

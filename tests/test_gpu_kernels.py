@@ -338,3 +338,39 @@ def test_fused_elbo_scales_with_upstream(device):
     (2.5 * loss_fn(cond, approx(), _noise=noise)).backward()
     for name, p in approx.named_parameters():
         torch.testing.assert_close(p.grad, 2.5 * base[name], rtol=1e-5, atol=1e-6)
+
+
+def test_log_likelihood_loss_on_device(device):
+    """
+    LogLikelihoodLoss with device parameters runs the site kernels (K = 1); it must match the
+    reference-semantics host evaluation (LogProbTracer on the CPU) in value and gradients.
+    """
+    rng = np.random.default_rng(9)
+    n, p = 2000, 4
+    X = torch.as_tensor(rng.normal(size=(n, p)).astype(np.float32))
+    y = torch.as_tensor(rng.normal(size=n).astype(np.float32))
+    b = torch.as_tensor((rng.random(n) < 0.4).astype(np.float32))
+
+    def make_model(Xd):
+        def model():
+            theta = mi.sample("theta", Normal(0.0, 1.0), sample_shape=p)
+            q = mi.sample("q", Beta(2.0, 3.0))
+            mi.sample("X", Normal(0.0, 1.0), sample_shape=(n, p))
+            mi.sample("y", Normal(Xd @ theta, 1.5))
+            mi.sample("b", Bernoulli(q), sample_shape=[n])
+        return model
+
+    def evaluate(dev):
+        theta = torch.tensor([0.3, -0.2, 0.5, 1.0], device=dev, requires_grad=True)
+        q = torch.tensor(0.35, device=dev, requires_grad=True)
+        loss = mi.nn.LogLikelihoodLoss()(
+            make_model(X.to(dev)),
+            {"theta": theta, "q": q, "X": X.to(dev), "y": y.to(dev), "b": b.to(dev)})
+        loss.backward()
+        return float(loss), theta.grad.cpu(), q.grad.cpu()
+
+    host = evaluate(torch.device("cpu"))
+    dev = evaluate(device)
+    assert abs(dev[0] - host[0]) <= 1e-5 * abs(host[0])
+    torch.testing.assert_close(dev[1], host[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dev[2], host[2], rtol=1e-5, atol=1e-5)
