@@ -86,6 +86,8 @@ def workload(name, device, world, rank):
             k_local=k_local, n=n, module=guide, guide=lambda: {"theta": guide()},
             conditioned=lambda: conditioned, evals=k_local * (n + 1), lr=0.02,
             dominant_N=n, bound="valu", flops_per_eval=2.0, bytes_per_eval=0.0,
+            kernel="k_site_bcast<Bernoulli-probs> (per-particle logits x shared data, LDS-staged)",
+            flop_note="2 FLOP/eval (one FMA) x K x n",
             data=f"synthetic: x ~ Bernoulli(0.7)[{n}] fp32 (seed 0); Beta(2,2) guide init")
     if name in ("c3", "c4"):
         p = 32
@@ -132,7 +134,10 @@ def workload(name, device, world, rank):
                   f"MF Normal guide, {k_local} particles/GPU"),
             k_local=k_local, n=n_obs, module=guide, guide=lambda: {"theta": guide()},
             conditioned=conditioned, evals=k_local * (n_obs + p), lr=0.01,
-            dominant_N=n_obs, bound="hbm", flops_per_eval=0.0, bytes_per_eval=8.0,
+            dominant_N=n_obs, bound="valu", flops_per_eval=4.0 * p, bytes_per_eval=0.0,
+            kernel=("k_linear<Normal, 32> (X @ theta evaluated in the site kernel: dot product "
+                    "and gradient, 2 FMA per feature per eval)"),
+            flop_note=f"{4 * p} FLOP/eval (2 x {p} FMA) x K x n",
             data=f"synthetic: X ~ N(0,1)[{n_total},{p}], y = X theta* + N(0,1) (seed 0)")
     if name == "c5":
         n, k_local = 1_000_000, 128
@@ -353,16 +358,11 @@ def main():
         achieved = flops / kernel_s / 1e12
         roof = {"bound": "valu", "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
-                "kernel": "k_site_bcast<Bernoulli-probs>", "kernel_ms": kernel_ms,
-                "launches_timed": launches,
-                "algorithmic_per_launch": f"{flops:.4g} FLOP (2 FLOP/eval x K x n)"}
+                "kernel": w["kernel"], "kernel_ms": kernel_ms, "launches_timed": launches,
+                "algorithmic_per_launch": f"{flops:.4g} FLOP ({w['flop_note']})"}
     else:
-        if w["bytes_per_eval"] is None:
-            nbytes = c5_bytes(w)
-            kname = "mi_site_program (fused z, y, b site group; row layout)"
-        else:
-            nbytes = w["bytes_per_eval"] * w["k_local"] * w["n"] + 8.0 * w["n"]
-            kname = "mi_site_program (Normal(X@theta, 1) site; column layout)"
+        nbytes = c5_bytes(w)
+        kname = "mi_site_program (fused z, y, b site group; row layout)"
         achieved = nbytes / kernel_s / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": kname,

@@ -208,6 +208,55 @@ int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_
 int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t key1, uint32_t* out,
                   void* stream);
 
+/* ---- linear-predictor sites (Normal(X @ theta, sigma), Bernoulli(logits = X @ theta)) --------- */
+
+/* A site whose location / logits is the model's own product X @ theta of an observed design matrix
+ * X [N, P] and a per-particle coefficient vector theta [K, P] (the reference's regression models:
+ * tests/test_mininf.py:13-18, examples/minibatch.md:24-33). The product is evaluated inside the
+ * site kernel, so the [K, N] predictor and its gradient never exist in memory:
+ *   total[k]        = site_scale * sum_i mask_i * log p(value_i | (X theta_k)_i, sigma_k)
+ *   dslots[j*K + k] = g0 * d total[k] / d theta[k, j]   for j < P (slot-major: row j holds all k)
+ *   dslots[P*K + k] = g0 * d total[k] / d sigma_k       (Normal with per-particle sigma only)
+ *   flags[0]        = OR of MI_FLAG_* (value support; sigma > 0; finite predictor)
+ * family: MI_NORMAL (sigma = scale[k * scale_stride_k], or scale_constant when scale == NULL) or
+ * MI_BERNOULLI_LOGITS (scale unused). P <= MI_LINEAR_MAX_P. */
+#define MI_LINEAR_MAX_P 64
+
+typedef struct mi_linear {
+  int64_t K;
+  int64_t N;
+  int64_t P;
+  int32_t family;
+  int32_t options;        /* MI_GROUP_FLAGS_ZEROED */
+  const float* x;         /* X[i, j] at x[i * x_stride_i + j * x_stride_j] */
+  int64_t x_stride_i;
+  int64_t x_stride_j;
+  const float* theta;     /* theta[k, j] at theta[k * theta_stride_k + j * theta_stride_j] */
+  int64_t theta_stride_k;
+  int64_t theta_stride_j;
+  const float* value;     /* value[i * value_stride_i] */
+  int64_t value_stride_i;
+  const uint8_t* mask;    /* NULL or mask[i * mask_stride_i] */
+  int64_t mask_stride_i;
+  const float* scale;     /* Normal sigma per particle, or NULL */
+  int64_t scale_stride_k;
+  float scale_constant;
+  float grad_scale;       /* g0 */
+  double site_scale;      /* minibatch scale (core.py:267-271) */
+  int32_t compute_grads;  /* write dtheta (and dsigma when `scale` is non-NULL) */
+  int32_t pad0;
+} mi_linear;
+
+int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes);
+int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,
+                      float* dslots, uint32_t* flags, void* stream);
+/* Same, recording the hipEvent_t start_event / stop_event (when non-NULL) around the site kernel
+ * alone (not the fp64 finalize reduction). */
+int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t workspace_bytes,
+                            float* total, float* dslots, uint32_t* flags, void* start_event,
+                            void* stop_event, void* stream);
+int mi_linear_struct_size(size_t* bytes);
+
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 
 #define MI_MAX_TERMS 8

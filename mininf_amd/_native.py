@@ -24,6 +24,7 @@ MAX_SLOTS = 4
 MAX_TERMS = 8
 MAX_FACTORS = 8
 MAX_BUFFERS = 16
+LINEAR_MAX_P = 64
 
 NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
@@ -59,6 +60,21 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
+    ]
+
+
+class Linear(ctypes.Structure):
+    _fields_ = [
+        ("K", c_i64), ("N", c_i64), ("P", c_i64),
+        ("family", ctypes.c_int32), ("options", ctypes.c_int32),
+        ("x", c_vp), ("x_stride_i", c_i64), ("x_stride_j", c_i64),
+        ("theta", c_vp), ("theta_stride_k", c_i64), ("theta_stride_j", c_i64),
+        ("value", c_vp), ("value_stride_i", c_i64),
+        ("mask", c_vp), ("mask_stride_i", c_i64),
+        ("scale", c_vp), ("scale_stride_k", c_i64),
+        ("scale_constant", ctypes.c_float), ("grad_scale", ctypes.c_float),
+        ("site_scale", ctypes.c_double),
+        ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
     ]
 
 
@@ -122,6 +138,13 @@ _SIGNATURES = {
                                         ctypes.c_uint32, c_i64, c_vp, c_vp]),
     "mi_philox4x32": (ctypes.c_int, [c_vp, c_i64, ctypes.c_uint32, ctypes.c_uint32, c_vp, c_vp]),
     "mi_elbo_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 2),
+    "mi_linear_struct_size": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_linear_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Linear),
+                                                 ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_linear_forward": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t, c_vp, c_vp,
+                                         c_vp, c_vp]),
+    "mi_linear_forward_timed": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t, c_vp,
+                                               c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

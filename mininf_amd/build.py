@@ -1,7 +1,7 @@
 """
 In-tree build of ``libmininf_amd.so`` (gfx950). Used by ``__graft_entry__.build()`` and the tests.
 
-The library holds the precompiled kernels (sites.hip, guide.hip, elbo.hip) and the host-side site-program
+The library holds the precompiled kernels (sites.hip, guide.hip, elbo.hip, linear.hip) and the host-side site-program
 specialiser (jit.cpp), which embeds ``include/mininf_amd.h`` and ``csrc/device_math.hpp`` verbatim
 so that kernels compiled at trace time by hiprtc share the exact device math of the precompiled
 ones.
@@ -16,8 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
-SOURCES = [os.path.join(CSRC, name) for name in ("sites.hip", "guide.hip", "elbo.hip", "jit.cpp")]
-HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "jit.hpp")] + \
+SOURCES = [os.path.join(CSRC, name)
+           for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "jit.cpp")]
+HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "jit.hpp",
+                                                 "internal.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]
 EMBEDDED = {"embedded_header.inc": os.path.join(INCLUDE, "mininf_amd.h"),
             "embedded_math.inc": os.path.join(CSRC, "device_math.hpp")}
@@ -25,6 +27,7 @@ TARGET = os.path.join(HERE, "libmininf_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}",
+         "-fno-slp-vectorize",  # SLP packing of independent fp32 chains into v_pk_* only adds moves
          f"-I{INCLUDE}", f"-I{CSRC}"]
 LIBS = ["-lhiprtc"]
 

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <string>
 
+#include "internal.hpp"
 #include "jit.hpp"
 
 namespace mi {
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
 struct FinalizeArgs {
   int32_t num_sites;
   int32_t num_slots;
-  double scale[MI_MAX_SITES];
+  double scale[MI_MAX_SITES];  // num_sites <= MI_MAX_SITES
   double slot_scale;  // the group's grad_scale: slot gradients are speculative like dense ones
 };
 
@@ -571,7 +572,12 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restr
   const int64_t kc = k < K ? k : K - 1;
   double t = 0.0;
   const int nv = A.num_sites + A.num_slots;
-  for (int v = 0; v < nv; ++v) {
+  // With one (combined) site value, blockIdx.y selects the value: many-slot groups (linear sites:
+  // one slot per coefficient) reduce in parallel instead of one value after another.
+  const bool split = gridDim.y > 1;
+  const int v_begin = split ? (int)blockIdx.y : 0;
+  const int v_end = split ? v_begin + 1 : nv;
+  for (int v = v_begin; v < v_end; ++v) {
     const float* p = part + (int64_t)v * nseg * K + kc;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     int64_t g = gl;
@@ -598,7 +604,7 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restr
       }
     }
   }
-  if (gl == 0 && k < K) total[k] = (float)t;
+  if (gl == 0 && k < K && v_begin == 0) total[k] = (float)t;
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -812,6 +818,22 @@ int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 }  // namespace
 
+int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
+                       const double* scale, double slot_scale, float* total, double* site_lp,
+                       float* slot_grad, hipStream_t stream) {
+  if (num_sites > MI_MAX_SITES) return MI_EINVAL;
+  mi::FinalizeArgs A{};
+  A.num_sites = num_sites;
+  A.num_slots = num_slots;
+  A.slot_scale = slot_scale;
+  for (int i = 0; i < num_sites; ++i) A.scale[i] = scale[i];
+  const unsigned gy = num_sites == 1 ? (unsigned)(1 + num_slots) : 1u;
+  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(K, mi::kFinK), gy),
+                     dim3(mi::kFinK * mi::kFinG), 0, stream, part, nseg, K, A, total, site_lp,
+                     slot_grad);
+  return to_code(hipGetLastError());
+}
+
 extern "C" {
 
 int mi_abi_version(char* target, size_t target_bytes) {
@@ -949,7 +971,8 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   A.num_slots = G.num_slots;
   A.slot_scale = (double)G.grad_scale;
   for (int i = 0; i < reduced_lp; ++i) A.scale[i] = prescaled ? 1.0 : G.sites[i].scale;
-  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK)),
+  const unsigned gy = reduced_lp == 1 ? (unsigned)(1 + A.num_slots) : 1u;
+  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK), gy),
                      dim3(mi::kFinK * mi::kFinG), 0, s, part, p.nseg, G.K, A, total, site_lp,
                      slot_grad);
   return to_code(hipGetLastError());

@@ -385,6 +385,164 @@ class _CategoricalFn(torch.autograd.Function):
         return None, None, None, dlogits, None, None
 
 
+# ------------------------------------------------------------------------------------------------
+# Linear-predictor sites: Normal(X @ theta, sigma) / Bernoulli(logits = X @ theta), fused.
+# ------------------------------------------------------------------------------------------------
+class _LinearLauncher:
+    """
+    One ``mi_linear_forward`` site: the predictor ``X @ theta_k`` is evaluated inside the kernel
+    (the model's matmul was deferred by :mod:`mininf_amd.linear`).
+    """
+    def __init__(self, site: SiteRecord, K: int, g0: float, device: torch.device,
+                 theta: torch.Tensor, sigma: Optional[_View], value: _View,
+                 mask: Optional[torch.Tensor]) -> None:
+        self.site, self.K, self.g0, self.device = site, K, g0, device
+        self.X = site.linear_X
+        self.N, self.P = self.X.shape
+        self.theta = theta
+        self.sigma = sigma
+        self.sigma_input = None
+        if sigma is not None and sigma.constant is None:
+            self.sigma_input = sigma.tensor[:, :1]
+        self.value = value
+        self.mask = mask
+        self.sites = [(site, None, mask)]   # flag layout: one word
+        # decided here, outside the autograd Function (whose forward runs with grad disabled)
+        grad_on = torch.is_grad_enabled()
+        self.theta_grad = grad_on and theta.requires_grad
+        self.sigma_grad = grad_on and self.sigma_input is not None and \
+            self.sigma_input.requires_grad
+
+    def needs_grads(self) -> bool:
+        return self.theta_grad or self.sigma_grad
+
+    def inputs(self) -> List[Optional[torch.Tensor]]:
+        return [self.theta, self.sigma_input]
+
+    def describe(self, compute_grads: bool) -> nat.Linear:
+        L = nat.Linear()
+        L.K, L.N, L.P = self.K, self.N, self.P
+        L.family = FAMILY_CODES[self.site.family]
+        L.x = self.X.data_ptr()
+        L.x_stride_i, L.x_stride_j = self.X.stride()
+        L.theta = self.theta.data_ptr()
+        L.theta_stride_k, L.theta_stride_j = self.theta.stride()
+        L.value = self.value.tensor.data_ptr()
+        L.value_stride_i = self.value.si
+        if self.mask is not None:
+            L.mask = self.mask.data_ptr()
+            L.mask_stride_i = self.mask.stride(0) if self.N > 1 else 1
+        if self.sigma is not None:
+            if self.sigma.constant is not None:
+                L.scale_constant = self.sigma.constant
+            else:
+                L.scale = self.sigma_input.data_ptr()
+                L.scale_stride_k = self.sigma_input.stride(0)
+        L.grad_scale = self.g0
+        L.site_scale = self.site.scale
+        L.compute_grads = int(compute_grads)
+        return L
+
+    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None):
+        device = self.device
+        L = self.describe(compute_grads)
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_linear_workspace_bytes(ctypes.byref(L), ctypes.byref(size)),
+                  "mi_linear_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        total = torch.empty(self.K, dtype=torch.float32, device=device)
+        nslots = self.P + (1 if L.scale else 0)
+        dslots = torch.empty((nslots, self.K), dtype=torch.float32, device=device) \
+            if compute_grads else None
+        if flags is None:
+            flags = torch.empty(1, dtype=torch.int32, device=device)
+        else:
+            L.options |= nat.GROUP_FLAGS_ZEROED
+        start = stop = None
+        if KERNEL_TIMER is not None:
+            start, stop = KERNEL_TIMER.pair(self)
+        nat.check(lib.mi_linear_forward_timed(
+            ctypes.byref(L), workspace.data_ptr(), size.value, total.data_ptr(), nat.ptr(dslots),
+            flags.data_ptr(), None if start is None else start.cuda_event,
+            None if stop is None else stop.cuda_event, nat.stream_handle(device)),
+            "mi_linear_forward_timed")
+        return total, dslots, flags
+
+    def grads(self, dslots: Optional[torch.Tensor]) -> List[Optional[torch.Tensor]]:
+        if dslots is None:
+            return [None, None]
+        dtheta = dslots[:self.P].t() if self.theta_grad else None
+        dsigma = dslots[self.P].reshape(self.K, 1) if self.sigma_grad else None
+        return [dtheta, dsigma]
+
+
+class _LinearSiteFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, launcher: _LinearLauncher, holder: dict, theta, sigma):  # type: ignore
+        total, dslots, flags = launcher.run(launcher.needs_grads())
+        holder["flags"] = flags
+        ctx.launcher, ctx.dslots = launcher, dslots
+        return total
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):  # type: ignore[override]
+        launcher: _LinearLauncher = ctx.launcher
+        dslots = ctx.dslots
+        if dslots is None:
+            return None, None, None, None
+        ctx.dslots = None
+        g = g.contiguous()
+        # dslots[j, k] is row k of a [K, slots] view: rescale by g[k] / g0 unless equal
+        nat.check(nat.lib().mi_scale_rows(dslots.data_ptr(), 1, launcher.K, launcher.K,
+                                          dslots.shape[0], g.data_ptr(), launcher.g0,
+                                          nat.stream_handle(g.device)), "mi_scale_rows")
+        return (None, None, *launcher.grads(dslots))
+
+
+def plan_linear(trace: ParticleTrace, g0: float, device: torch.device) -> List[_LinearLauncher]:
+    """
+    Launchers for the fused linear-predictor sites of a trace. A site whose operands the kernel
+    cannot take (per-element sigma, particle-dependent values, non-float32) gets its predictor
+    materialised here as ``theta @ X.T`` and is planned like any other site.
+    """
+    K = trace.K
+    out: List[_LinearLauncher] = []
+    for site in trace.sites:
+        if site.linear_X is None:
+            continue
+        theta = site.linear_theta
+        shape = site.site_shape
+        launcher = None
+        ok = theta is not None and theta.dtype == torch.float32 and theta.dim() == 2 and \
+            theta.device == device and site.linear_X.device == device
+        if ok:
+            value_t, const = _to_device(_float(site.tensors[-1], site.name), K, device,
+                                        f"site '{site.name}'", allow_constant=False)
+            value = _collapse(value_t, K, shape)
+            sigma = None
+            if site.family == "normal":
+                t, c = _to_device(_float(site.tensors[1], site.name), K, device,
+                                  f"site '{site.name}'")
+                sigma = _View(None, 0, 0, c) if c is not None else _collapse(t, K, shape)
+                if sigma.constant is None and sigma.si != 0:
+                    ok = False
+            if value.sk != 0:
+                ok = False
+            mask = None
+            if site.mask is not None:
+                mask = site.mask.to(device).bool().expand(shape).reshape(-1)
+            if ok:
+                launcher = _LinearLauncher(site, K, g0, device, theta, sigma, value, mask)
+        if launcher is None:
+            # materialise the predictor as the model would have: [K, N] = theta @ X^T
+            site.tensors[0] = theta @ site.linear_X.t()
+            site.linear_X = None
+            continue
+        out.append(launcher)
+    return out
+
+
 @dataclasses.dataclass
 class LogJoint:
     """
@@ -410,7 +568,11 @@ class LogJoint:
                 parts.append(holder["flags"].reshape(-1).to(torch.int64))
         for _, ok in self.checks:
             parts.append((~ok.reshape(-1).bool()).any().reshape(1).to(torch.int64))
-        return torch.cat(parts) if parts else None
+        if not parts:
+            return None
+        # host-evaluated checks (host values) join the device flags
+        device = next((p.device for p in parts if p.device.type != "cpu"), parts[0].device)
+        return torch.cat([p.to(device) for p in parts])
 
     def flag_count(self) -> int:
         return sum(len(sites) for _, _, sites in self.pending) + len(self.checks)
@@ -458,6 +620,8 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
     groups: List[Tuple[torch.Size, _GroupLauncher]] = []
     categorical = []
     for site in trace.sites:
+        if site.linear_X is not None:
+            continue   # planned by plan_linear
         if site.family == "categorical":
             logits, value = (_to_device(t, K, device, f"site '{site.name}'", False)[0]
                              for t in site.tensors)
@@ -503,6 +667,7 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
     Launch the site kernels for every recorded site and return the per-particle log joint.
     """
     K = trace.K
+    linears = plan_linear(trace, g0, device)
     launchers, categorical = plan_groups(trace, g0, device)
     totals: List[torch.Tensor] = []
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
@@ -510,12 +675,16 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
         holder: dict = {}
         totals.append(_CategoricalFn.apply(site, holder, g0, lg, val, mask))
         pending.append(("categorical", holder, [site]))
+    for linear in linears:
+        holder = {}
+        totals.append(_LinearSiteFn.apply(linear, holder, *linear.inputs()))
+        pending.append(("linear", holder, [linear.site]))
     for launcher in launchers:
         holder = {}
         totals.append(_SiteGroupFn.apply(launcher, holder, *launcher.inputs()))
         pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
     for _, value in trace.fallback:
-        totals.append(value.to(torch.float32))
+        totals.append(value.to(device=device, dtype=torch.float32))
     if totals:
         total = totals[0]
         for extra in totals[1:]:
@@ -568,11 +737,13 @@ class _ElboPlan:
     """
     def __init__(self, K: int, g0: float, device: torch.device, launchers, categorical,
                  fallback: List[torch.Tensor], factors: List[EntropyFactor],
-                 entropy_scale: float) -> None:
+                 entropy_scale: float, linears: Optional[List[_LinearLauncher]] = None) -> None:
         self.K, self.g0, self.device = K, g0, device
         self.launchers = launchers
         self.categorical = categorical
-        self.fallback = [v.to(torch.float32).reshape(K) for v in fallback]
+        self.linears = linears or []
+        self.lin_holders = [dict() for _ in self.linears]
+        self.fallback = [v.to(device=device, dtype=torch.float32).reshape(K) for v in fallback]
         self.factors = factors
         self.entropy_scale = entropy_scale
         self.holders = [dict() for _ in launchers]
@@ -586,6 +757,8 @@ class _ElboPlan:
             out.extend(launcher.inputs())
         for _, lg, val, mask in self.categorical:
             out.extend([lg, val, mask])
+        for linear in self.linears:
+            out.extend(linear.inputs())
         out.extend(self.fallback)
         out.extend(f.tensor for f in self.factors)
         return out
@@ -620,9 +793,10 @@ class _ElboPlan:
         buffers: List[torch.Tensor] = []
         results = []
         # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
-        sizes = [1] * len(self.categorical) + [len(l.sites) for l in self.launchers]
+        sizes = [1] * (len(self.categorical) + len(self.linears)) + \
+            [len(l.sites) for l in self.launchers]
         self.flags = torch.zeros(max(1, sum(sizes)), dtype=torch.int32, device=self.device)
-        cursor = len(self.categorical)
+        cursor = len(self.categorical) + len(self.linears)
         for launcher, holder in zip(self.launchers, self.holders):
             need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
             part = self.flags[cursor:cursor + len(launcher.sites)]
@@ -645,6 +819,16 @@ class _ElboPlan:
             if dlogits is not None:
                 buffers.append(dlogits)
             cat_results.append(dlogits)
+        lin_results = []
+        base = len(self.categorical)
+        for j, (linear, holder) in enumerate(zip(self.linears, self.lin_holders)):
+            total, dslots, flags = linear.run(linear.needs_grads(),
+                                              self.flags[base + j:base + j + 1])
+            holder["flags"] = flags
+            terms.append(total)
+            if dslots is not None:
+                buffers.append(dslots)
+            lin_results.append(dslots)
         terms.extend(t.contiguous() for t in self.fallback)
         if len(terms) > nat.MAX_TERMS:
             head = nat.MAX_TERMS - 1
@@ -660,13 +844,13 @@ class _ElboPlan:
         loss = torch.empty((), dtype=torch.float32, device=self.device)
         nat.check(lib.mi_elbo_forward(ctypes.byref(E), ws.data_ptr(), ws.numel(), loss.data_ptr(),
                                       nat.stream_handle(self.device)), "mi_elbo_forward")
-        self.state = (E, results, cat_results, extra, terms)
+        self.state = (E, results, cat_results, lin_results, extra, terms)
         return loss
 
     def backward(self, u: torch.Tensor) -> List[Optional[torch.Tensor]]:
         if self.state is None:   # a second backward through the same graph: recompute
             self.forward()
-        E, results, cat_results, extra, _ = self.state
+        E, results, cat_results, lin_results, extra, _ = self.state
         self.state = None
         device = self.device
         u = u.to(torch.float32).contiguous()
@@ -696,6 +880,8 @@ class _ElboPlan:
                     out.append(None)
         for dlogits in cat_results:
             out.extend([dlogits, None, None])
+        for linear, dslots in zip(self.linears, lin_results):
+            out.extend(linear.grads(dslots))
         out.extend(dterm.expand(self.K) for _ in self.fallback)
         out.extend(fgrads)
         return out
@@ -749,13 +935,16 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
     backward is one ``mi_elbo_backward`` launch (plus the guide samplers' own backward).
     """
+    linears = plan_linear(trace, g0, device)
     launchers, categorical = plan_groups(trace, g0, device)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical,
-                     [value for _, value in trace.fallback], factors, entropy_scale)
+                     [value for _, value in trace.fallback], factors, entropy_scale, linears)
     loss = _ElboFn.apply(plan, *plan.inputs())
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):
         pending.append(("categorical", holder, [site]))
+    for linear, holder in zip(linears, plan.lin_holders):
+        pending.append(("linear", holder, [linear.site]))
     for launcher, holder in zip(launchers, plan.holders):
         pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
     return loss, LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)

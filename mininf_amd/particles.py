@@ -17,7 +17,10 @@ per-particle sum; they are outside the north-star families and listed in DESIGN.
 """
 from __future__ import annotations
 
+import collections
+import copy
 import dataclasses
+import os
 import weakref
 from typing import Any, Callable, Dict, List, Optional, Tuple, cast
 
@@ -55,6 +58,11 @@ class SiteRecord:
     mask: Optional[torch.Tensor]
     description: str
     tensors: List[torch.Tensor] = dataclasses.field(default_factory=list)
+    # Linear-predictor site (loc / logits = X @ theta deferred by mininf_amd.linear): the observed
+    # design matrix, the output index of theta and, after tracing, theta as [K, P].
+    linear_X: Optional[torch.Tensor] = None
+    linear_theta_index: int = -1
+    linear_theta: Optional[torch.Tensor] = None
 
 
 @dataclasses.dataclass
@@ -121,6 +129,59 @@ def memo_commit(entry: Tuple) -> None:
         _VALIDATED[key] = (ref, version)
 
 
+_HOST_COPIES: "collections.OrderedDict[Tuple, Tuple[torch.Tensor, torch.Tensor]]" = \
+    collections.OrderedDict()
+
+
+def device_copy(t: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """
+    A cached device copy of an unbatched host tensor (keyed on storage, layout and version), so a
+    constant such as the 2.0 of ``Gamma(2.0, 2.0)`` is copied once, not on every step (and not
+    inside a captured graph).
+    """
+    key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t._version, str(device))
+    hit = _HOST_COPIES.get(key)
+    if hit is None:
+        hit = (t, t.to(device))
+        _HOST_COPIES[key] = hit
+        while len(_HOST_COPIES) > 64:
+            _HOST_COPIES.popitem(last=False)
+    else:
+        _HOST_COPIES.move_to_end(key)
+    return hit[1]
+
+
+def _on_device(obj: Any, device: torch.device) -> Any:
+    """
+    A shallow copy of a distribution (or transform) whose unbatched host tensors -- and those of
+    nested distributions and transforms -- are replaced by device copies: torch-evaluated sites
+    then compute on the device. (Under vmap, torch evaluates e.g. Gamma(2., 2.).log_prob of a
+    device value on the HOST when the parameters are host tensors.)
+    """
+    from torch.distributions import Transform
+    changes = {}
+    for key, item in vars(obj).items():
+        if isinstance(item, torch.Tensor):
+            if item.device.type == "cpu" and not is_batched(item) and not item.requires_grad:
+                changes[key] = device_copy(item, device)
+        elif isinstance(item, (Distribution, Transform)):
+            moved = _on_device(item, device)
+            if moved is not item:
+                changes[key] = moved
+        elif isinstance(item, (list, tuple)) and any(isinstance(x, (Distribution, Transform))
+                                                      for x in item):
+            moved_items = [_on_device(x, device) if isinstance(x, (Distribution, Transform))
+                           else x for x in item]
+            if any(a is not b for a, b in zip(moved_items, item)):
+                changes[key] = type(item)(moved_items)
+    if not changes:
+        return obj
+    out = copy.copy(obj)
+    for key, item in changes.items():
+        setattr(out, key, item)
+    return out
+
+
 def classify(distribution: Distribution) -> Tuple[str, List[Any]]:
     """
     Map a distribution onto a HIP site family and its role tensors, or ``("torch", [])``.
@@ -153,6 +214,7 @@ class ParticleTracer(TracerMixin):
         self.outputs: List[torch.Tensor] = []
         self.checks: List[CheckRecord] = []
         self.fallback_outputs: List[Tuple[str, int]] = []
+        self.deferred = None   # the DeferredMatmul mode of the trace, if any
 
     def _emit(self, tensor: torch.Tensor) -> int:
         self.outputs.append(tensor)
@@ -231,16 +293,35 @@ class ParticleTracer(TracerMixin):
             self._record_torch_site(name, distribution, value, data, mask, scale)
             return value
 
+        # A deferred `X @ theta` as the location / logits of a Normal / Bernoulli-logits site over
+        # shared data becomes a fused linear site; every other deferred parameter is materialised.
+        linear = None
+        mode = self.deferred
+        if mode is not None:
+            info = mode.lookup(params[0]) if params else None
+            if info is not None and family in ("normal", "bernoulli_logits") and \
+                    not is_batched(data) and tuple(shape) == (info.X.shape[0],) and \
+                    tuple(data.shape) == tuple(shape) and \
+                    all(mode.lookup(p) is None for p in params[1:]):
+                linear = info.root or info
+            params = [p if (linear is not None and j == 0) else mode.materialize(p)
+                      for j, p in enumerate(params)]
+
         # Value support is checked by the site kernels (fused flag); constraint checks on the
         # parameters as well (MI_FLAG_PARAM), replacing torch's validate_args at construction.
         roles = [self._emit(p) for p in params] + [self._emit(data)]
-        self.sites.append(SiteRecord(name=name, family=family, roles=roles, site_shape=shape,
-                                     scale=scale, mask=mask,
-                                     description=type(distribution).__name__))
+        record = SiteRecord(name=name, family=family, roles=roles, site_shape=shape, scale=scale,
+                            mask=mask, description=type(distribution).__name__)
+        if linear is not None:
+            record.linear_X = linear.X
+            record.linear_theta_index = self._emit(linear.theta)
+        self.sites.append(record)
         return value
 
     def _record_torch_site(self, name: str, distribution: Distribution, value: Any,
                            data: torch.Tensor, mask: Optional[torch.Tensor], scale: float) -> None:
+        if isinstance(data, torch.Tensor) and data.device.type != "cpu":
+            distribution = _on_device(distribution, data.device)
         if self._validate_parameters:
             self._check_support(name, value, distribution, cast(Constraint, distribution.support))
             for param, constraint in distribution.arg_constraints.items():
@@ -276,17 +357,30 @@ _NO_VALIDATE = object()
 
 
 def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
-                    validate: bool = True) -> ParticleTrace:
+                    validate: bool = True, defer_matmul: Optional[bool] = None) -> ParticleTrace:
     """
     Run ``condition(model, **samples)`` once under ``vmap`` over the leading (particle) dimension of
-    every sample and return the recorded sites with [K, ...] tensors.
+    every sample and return the recorded sites with [K, ...] tensors. With ``defer_matmul``,
+    ``X @ theta`` predictors of Normal / Bernoulli-logits sites are evaluated inside the site
+    kernels instead of by the model (:mod:`mininf_amd.linear`).
     """
+    from .linear import DeferredMatmul
+
+    if defer_matmul is None:
+        defer_matmul = os.environ.get("MININF_AMD_DEFER_MATMUL", "1") != "0"
     names = list(samples)
     tracer = ParticleTracer(validate=validate)
 
     def per_particle(*values):
+        mode = DeferredMatmul(K) if defer_matmul else None
+        tracer.deferred = mode
         with tracer:
-            core.condition(model, **dict(zip(names, values)))()
+            if mode is not None:
+                with mode:
+                    core.condition(model, **dict(zip(names, values)))()
+            else:
+                core.condition(model, **dict(zip(names, values)))()
+        tracer.deferred = None
         return tuple(tracer.outputs)
 
     previous = Distribution._validate_args
@@ -304,6 +398,8 @@ def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
 
     for site in tracer.sites:
         site.tensors = [outputs[index] for index in site.roles]
+        if site.linear_theta_index >= 0:
+            site.linear_theta = outputs[site.linear_theta_index]
     checks = [(check, outputs[check.output]) for check in tracer.checks]
     fallback = [(name, outputs[index]) for name, index in tracer.fallback_outputs]
     return ParticleTrace(sites=tracer.sites, checks=checks, fallback=fallback, K=K)

@@ -25,7 +25,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 DOMINANT = {
     "c2": r"k_site_bcast",
-    "c3": r"mi_site_program|k_group_col",
+    "c3": r"k_linear",
     "c5": r"mi_site_program|k_group_row",
 }
 
