@@ -9,7 +9,7 @@
 // plus every autograd kernel of those expressions (~50 small launches per step for a Beta guide).
 //
 // Reductions are deterministic: fixed grid, fp64 per-block partial sums, and the last block to
-// finish (device-scope counter, reset by that block) adds the partials in block order.
+// finish (device-scope counter, reset by that block) adds the partials in a fixed order.
 #include "common.hpp"
 
 #include <algorithm>
@@ -74,7 +74,7 @@ MI_DEV double block_sum(double v, double* red) {
 __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, double* partial,
                                                                unsigned* __restrict__ counter,
                                                                float* __restrict__ loss) {
-  __shared__ double red[kElboThreads / kWave];
+  __shared__ double red[2 * (kElboThreads / kWave)];
   __shared__ bool last;
   const int64_t stride = (int64_t)gridDim.x * kElboThreads;
   const int64_t first = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
@@ -92,12 +92,17 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, 
     last = atomicAdd(counter, 1u) == gridDim.x - 1;
   }
   __syncthreads();
-  if (last && threadIdx.x == 0) {
+  if (last) {
+    // the last block adds the partials: each thread a fixed strided subset, then a fixed-order
+    // block sum -- deterministic, and no serial chain of dependent loads
     __threadfence();
-    double total = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) total += partial[b];
-    *loss = (float)total;
-    *counter = 0u;
+    double t = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += kElboThreads) t += partial[b];
+    const double total = block_sum(t, red + kElboThreads / kWave);
+    if (threadIdx.x == 0) {
+      *loss = (float)total;
+      *counter = 0u;
+    }
   }
 }
 
