@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 1
+#define MI_ABI_VERSION 2
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -87,6 +87,33 @@ typedef struct mi_site {
   double scale;          /* minibatch scale: declared batch numel / observed numel (core.py:267-271) */
 } mi_site;
 
+/* A guide draw evaluated inside a site group instead of being read from memory: the operand
+ * `operand - 1` of the group is z[k, i] = loc[i] + eps[k, i] * scale[i] with eps the counter-based
+ * normals of mi_normal_rsample (same seed, step, stream and particle numbering, so the values are
+ * bit-identical). The [K, N] draw and its [K, N] gradient never exist in memory: with
+ * compute_grads the group writes
+ *   dloc[i]   = sum_k g0 * dT_k / dz[k, i]
+ *   dscale[i] = sum_k g0 * dT_k / dz[k, i] * eps[k, i]
+ * (the gradients mi_normal_rsample_backward would produce from the dense dz). Requirements: the
+ * group's other dense operands are row-major [K, N] with unit element stride, N % 4 == 0 and
+ * N >= 512; otherwise mi_group_forward returns MI_EUNSUPPORTED and the caller materialises the
+ * draw with mi_normal_rsample. */
+typedef struct mi_draw {
+  int32_t operand;          /* 1 + index of the operand replaced by the draw; 0 = no draw (so a
+                               zero-initialised descriptor has none) */
+  uint32_t stream_id;
+  const float* loc;
+  int64_t loc_stride;       /* element strides (0: one value for all elements) */
+  const float* scale;
+  int64_t scale_stride;
+  uint64_t seed;
+  uint64_t step;
+  const uint64_t* step_device;  /* may be NULL; added to step */
+  int64_t particle_offset;
+  float* dloc;              /* [N] outputs (compute_grads) */
+  float* dscale;
+} mi_draw;
+
 /* A group of sites evaluated over one shared [K, N] element space in a single pass, so that an
  * operand read by several sites (e.g. a latent z that is the value of one site and the loc of
  * another) is loaded once and its gradient accumulated in registers. */
@@ -101,6 +128,7 @@ typedef struct mi_group {
   int32_t options;       /* MI_GROUP_* bits */
   mi_site sites[MI_MAX_SITES];
   mi_operand operands[MI_MAX_OPERANDS];
+  mi_draw draw;          /* draw.operand == 0: no operand is a fused guide draw */
 } mi_group;
 
 /* Library identification: returns MI_ABI_VERSION and writes the offload target ("gfx950"). */

@@ -53,6 +53,15 @@ class Site(ctypes.Structure):
     ]
 
 
+class Draw(ctypes.Structure):
+    _fields_ = [
+        ("operand", ctypes.c_int32), ("stream_id", ctypes.c_uint32),
+        ("loc", c_vp), ("loc_stride", c_i64), ("scale", c_vp), ("scale_stride", c_i64),
+        ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
+        ("particle_offset", c_i64), ("dloc", c_vp), ("dscale", c_vp),
+    ]
+
+
 class Group(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("N", c_i64),
@@ -60,6 +69,7 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
+        ("draw", Draw),
     ]
 
 

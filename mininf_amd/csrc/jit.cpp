@@ -108,7 +108,8 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
       << mask_kind_tag(st) << (st.mask_stride_i == 1 ? "u" : "") << ")";
   }
   s << "|" << g.num_slots << "|" << g.compute_grads
-    << (plan.row && g.N < 64L * plan.elems ? "|small" : "");
+    << (plan.row && g.N < 64L * plan.elems ? "|small" : "") << "|draw" << g.draw.operand
+    << (g.draw.loc_stride == 0 ? "b" : "") << (g.draw.scale_stride == 0 ? "b" : "");
   return Signature{s.str()};
 }
 
@@ -369,7 +370,108 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << in << "}\n";
   };
 
-  if (row) {
+
+  // Row loop with a fused guide draw (mi_draw): lane `lane` owns the element quads
+  // base/4 + qq * 64 + lane (qq < E / 4), i.e. elements base + qq * 256 + lane * 4 + j, so that one
+  // Philox call yields the lane's four normals of a quad -- exactly the eps of mi_normal_rsample for
+  // (quad, particle). z = loc + eps * scale is formed in registers and d/dz is reduced over the
+  // block's particles into dloc / dscale, so neither z nor dz touches memory.
+  const int draw = g.draw.operand - 1;
+  auto emit_draw_loop = [&]() {
+    const char* in = "    ";
+    auto elem = [&](const char* e) {
+      return std::string("((") + e + " >> 2) * 256 + lane * 4 + (" + e + " & 3))";
+    };
+    o << in << "const long nominal = seg * " << 64 * E << "L;\n";
+    o << in << "const long shift = max(0L, nominal + " << 64 * E << "L - N);\n";
+    o << in << "const long base = nominal - shift;\n";
+    o << in << "bool ok[" << E << "];\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
+      << "; ++e) ok[e] = " << elem("e") << " >= shift;\n";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kShared))
+        o << in << "float s" << op << "[" << E << "];\n" << in << "{ const float* __restrict__ r = x"
+          << op << " + base + lane * 4;\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
+          << "; ++e) s" << op << "[e] = r[(e >> 2) * 256 + (e & 3)]; }\n";
+    for (int st = 0; st < g.num_sites; ++st)
+      if (mask_is(st, kShared))
+        o << in << "bool m" << st << "[" << E << "];\n" << in
+          << "{ const unsigned char* __restrict__ r = mk" << st
+          << " + base + lane * 4;\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
+          << "; ++e) m" << st << "[e] = r[(e >> 2) * 256 + (e & 3)] != 0; }\n";
+    o << in << "float dwl[" << E << "], dws[" << E << "];\n#pragma unroll\n" << in
+      << "for (int e = 0; e < " << E << "; ++e) { const long i = base + " << elem("e")
+      << "; dwl[e] = G.draw.loc[i * G.draw.loc_stride]; dws[e] = G.draw.scale[i * "
+         "G.draw.scale_stride]; }\n";
+    const bool dgrad = g.compute_grads != 0;
+    if (dgrad)
+      o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
+        << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
+    for (int v = 0; v < nv; ++v) o << in << "float keep" << v << " = 0.0f;\n";
+    o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
+    o << in << "  const int r = (int)((k - k_begin) & 63);\n";
+    o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
+      << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
+         "+ qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
+    o << in << "  float d" << draw << "[" << E << "];\n#pragma unroll\n" << in
+      << "  for (int e = 0; e < " << E << "; ++e) d" << draw << "[e] = fmaf(ep[e], dws[e], dwl[e]);\n";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (op != draw && is(op, kDense))
+        o << in << "  float d" << op << "[" << E << "];\n" << in
+          << "  { const float* __restrict__ r = x" << op << " + k * sk" << op
+          << " + base + lane * 4;\n#pragma unroll\n" << in << "  for (int e = 0; e < " << E
+          << "; ++e) d" << op << "[e] = r[(e >> 2) * 256 + (e & 3)]; }\n";
+    particle_loads("      ", "k");
+    zero_accumulators("      ");
+    const char* in2 = "      ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << in2 << "float g" << op << "[" << E << "];\n";
+    o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) {\n";
+    const std::string inner = std::string(in2) + "  ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
+    for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, "ok[e]", inner.c_str());
+    o << in2 << "}\n";
+    for (int op = 0; op < g.num_operands; ++op) {
+      if (!dense_grad(op)) continue;
+      if (op == draw)
+        o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) { dal[e] += g"
+          << op << "[e]; das[e] = fmaf(g" << op << "[e], ep[e], das[e]); }\n";
+      else
+        o << in2 << "{ float* __restrict__ r = gx" << op << " + k * gsk" << op
+          << " + base + lane * 4;\n#pragma unroll\n" << in2 << "for (int e = 0; e < " << E
+          << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * g" << op << "[e]; }\n";
+    }
+    for (int v = 0; v < nv; ++v)
+      o << in2 << "{ const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
+        << " = (lane == r) ? t : keep" << v << "; }\n";
+    o << in2 << "if (r == 63 || k + 1 == k_end) {\n";
+    o << in2 << "  if (lane <= r) {\n";
+    for (int v = 0; v < nv; ++v)
+      o << in2 << "    part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
+    o << in2 << "  }\n";
+    for (int v = 0; v < nv; ++v) o << in2 << "  keep" << v << " = 0.0f;\n";
+    o << in2 << "}\n";
+    o << in << "}\n";
+    if (dgrad)
+      o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) if (ok[e]) {\n"
+        << in << "  const long i = (long)blockIdx.y * N + base + " << elem("e") << ";\n"
+        << in << "  G.draw.dloc[i] = G.grad_scale * dal[e];\n"
+        << in << "  G.draw.dscale[i] = G.grad_scale * das[e];\n"
+        << in << "}\n";
+  };
+
+  if (row && draw >= 0) {
+    o << "  const unsigned long long dseed = G.draw.seed;\n";
+    o << "  const unsigned long long dstep = G.draw.step + (G.draw.step_device != nullptr ? "
+         "*G.draw.step_device : 0ull);\n";
+    o << "  const unsigned dstream = G.draw.stream_id;\n";
+    o << "  const long dpoff = G.draw.particle_offset;\n";
+    o << "  if (seg < nseg) {\n";
+    o << "    const long k_begin = (long)blockIdx.y * arg;\n";
+    o << "    const long k_end = min(K, k_begin + arg);\n";
+    emit_draw_loop();
+    o << "  }\n";
+  } else if (row) {
     // Lane `lane` owns elements base + e * 64 + lane of each row (coalesced per e). When N spans
     // at least one whole segment, every segment is loaded as a whole one: the ragged last segment
     // is shifted back to end at N and masks the elements its predecessor already owns (`ok`), so

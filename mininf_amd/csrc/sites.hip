@@ -608,6 +608,23 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restr
 }
 
 // -------------------------------------------------------------------------------------------------
+// Fused guide draws: sum the per-K-block dloc / dscale partials (fixed order, fp64).
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_draw_reduce(const float* __restrict__ part, int64_t slices,
+                                                     int64_t N, float* __restrict__ dloc,
+                                                     float* __restrict__ dscale) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  double a = 0.0, b = 0.0;
+  for (int64_t y = 0; y < slices; ++y) {
+    a += (double)part[y * N + i];
+    b += (double)part[(slices + y) * N + i];
+  }
+  dloc[i] = (float)a;
+  dscale[i] = (float)b;
+}
+
+// -------------------------------------------------------------------------------------------------
 // Backward rescale of speculative dense gradients.
 // -------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ x, int64_t sk, int64_t si,
@@ -697,11 +714,36 @@ bool validate_group(const mi_group* g) {
     for (int q = 0; q < 3; ++q)
       if (st.operand[q] >= g->num_operands) return false;
   }
+  const int draw = g->draw.operand - 1;
+  if (draw >= g->num_operands || draw < -1) return false;
+  if (draw >= 0 && (g->draw.loc == nullptr || g->draw.scale == nullptr ||
+                    (g->compute_grads && (g->draw.dloc == nullptr || g->draw.dscale == nullptr))))
+    return false;
   for (int o = 0; o < g->num_operands; ++o) {
     const mi_operand& op = g->operands[o];
+    if (o == draw) continue;  // computed in the kernel
     if (op.data == nullptr) return false;
     if (op.grad_mode == MI_GRAD_DENSE && op.grad == nullptr) return false;
     if (op.grad_mode == MI_GRAD_PARTICLE && (op.slot < 0 || op.slot >= g->num_slots)) return false;
+  }
+  return true;
+}
+
+// A fused guide draw (mi_draw) needs the row layout with whole element quads per lane and plain
+// row-major [K, N] companions (see include/mininf_amd.h).
+bool draw_supported(const mi_group* g) {
+  const int draw = g->draw.operand - 1;
+  if (draw < 0) return true;
+  if (g->N % 4 != 0 || g->N < 64 * 8) return false;
+  for (int o = 0; o < g->num_operands; ++o) {
+    const mi_operand& op = g->operands[o];
+    if (o == draw) continue;
+    if (op.stride_k != 0 && op.stride_i != 0 && op.stride_i != 1) return false;
+    if (op.stride_k == 0 && op.stride_i != 0 && op.stride_i != 1) return false;
+  }
+  for (int s = 0; s < g->num_sites; ++s) {
+    const mi_site& st = g->sites[s];
+    if (st.mask != nullptr && st.mask_stride_k != 0) return false;
   }
   return true;
 }
@@ -747,7 +789,7 @@ Plan make_plan(const mi_group* g) {
   Plan p{};
   const int nv = g->num_sites + g->num_slots;
   (void)nv;
-  if (bcast_eligible(g)) {
+  if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     p.nseg = ceil_div(g->N, mi::kBcastChunk);
     p.grid = dim3((unsigned)p.nseg, (unsigned)ceil_div(g->K, mi::kBcastThreads * mi::kBcastP));
@@ -809,8 +851,15 @@ size_t prep_offset(const mi_group* g, const Plan& p) {
   return (partial_bytes(g, p) + 255) / 256 * 256;
 }
 
+// Per-K-block partial dloc / dscale of a fused draw (when the grid splits the particles).
+size_t draw_partial_floats(const mi_group* g, const Plan& p) {
+  if (g->draw.operand == 0 || !g->compute_grads || p.grid.y <= 1) return 0;
+  return 2 * (size_t)p.grid.y * (size_t)g->N;
+}
+
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
-  if (p.shape != kBcast) return partial_bytes(g, p);
+  if (p.shape != kBcast)
+    return prep_offset(g, p) + draw_partial_floats(g, p) * sizeof(float);
   return prep_offset(g, p) + (size_t)mi::kPrep * (size_t)g->K * sizeof(float);
 }
 
@@ -888,6 +937,8 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   int reduced_lp = G.num_sites;
   bool prescaled = false;  // partials already carry the site scales
   float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
+  if (group->draw.operand != 0 && (p.shape != kRow || !draw_supported(group))) return MI_EUNSUPPORTED;
+  float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
   if (p.shape == kBcast) {
     const dim3 pg((unsigned)ceil_div(G.K, 256));
     switch (G.sites[0].family) {
@@ -935,7 +986,12 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
     case kRow:
     case kCol: {
       const PlanInfo info = plan_info(p, combined);
-      const int rc = mi_jit_launch(G, info, part, p.nseg,
+      mi_group GK = G;
+      if (draw_partials != nullptr) {  // per-K-block partials, summed below
+        GK.draw.dloc = draw_partials;
+        GK.draw.dscale = draw_partials + (size_t)p.grid.y * G.N;
+      }
+      const int rc = mi_jit_launch(GK, info, part, p.nseg,
                                    p.shape == kRow ? p.rows_per_block : p.seg_len, flags, s);
       if (rc < 0) return -rc;
       if (rc == 0) {
@@ -943,6 +999,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
         reduced_lp = combined ? 1 : G.num_sites;
         break;
       }
+      if (G.draw.operand != 0) return MI_EUNSUPPORTED;  // fused draws need the specialised kernel
       if (p.shape == kRow) {
         const int e = row_elems();
         if (e == 4)
@@ -964,6 +1021,12 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   if (e != hipSuccess) return to_code(e);
   if (stop_event != nullptr) {
     e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s);
+    if (e != hipSuccess) return to_code(e);
+  }
+  if (draw_partials != nullptr) {
+    hipLaunchKernelGGL(mi::k_draw_reduce, dim3((unsigned)ceil_div(G.N, 256)), dim3(256), 0, s,
+                       draw_partials, (int64_t)p.grid.y, G.N, G.draw.dloc, G.draw.dscale);
+    e = hipGetLastError();
     if (e != hipSuccess) return to_code(e);
   }
   mi::FinalizeArgs A{};

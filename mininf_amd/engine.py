@@ -20,12 +20,13 @@ from __future__ import annotations
 import collections
 import ctypes
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from . import _native as nat
-from . import particles
+from . import guide, particles
 from .particles import ParticleTrace, SiteRecord
 
 
@@ -110,11 +111,14 @@ class _View:
     sk: int                         # element strides over the logical [K, N] space
     si: int
     constant: Optional[float] = None  # host scalar (e.g. the 2.0 of `Beta(2, 2)`): no operand
+    draw: Optional[guide.LazyDraw] = None  # a guide draw computed inside the kernel (mi_draw)
 
     @property
     def key(self) -> Tuple:
         if self.constant is not None:
             return ("constant", self.constant)
+        if self.draw is not None:
+            return ("draw", id(self.draw))
         t = self.tensor
         return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), self.sk, self.si,
                 t.requires_grad)
@@ -126,7 +130,14 @@ class _View:
     @property
     def per_particle(self) -> bool:
         """One scalar per particle: the gradient is reduced over elements inside the kernel."""
-        return self.constant is None and self.tensor.shape[1] == 1 and self.si == 0
+        return self.constant is None and self.draw is None and self.tensor.shape[1] == 1 and \
+            self.si == 0
+
+    @property
+    def requires_grad(self) -> bool:
+        if self.draw is not None:
+            return self.draw.loc.requires_grad or self.draw.scale.requires_grad
+        return self.tensor.requires_grad
 
 
 @dataclasses.dataclass
@@ -156,16 +167,20 @@ class _GroupLauncher:
         new = {v.key for v in views if v.key not in self.keys}
         if len(self.sites) >= nat.MAX_SITES or len(self.operands) + len(new) > nat.MAX_OPERANDS:
             return False
+        draws = {id(op.view.draw) for op in self.operands if op.view.draw is not None} | \
+            {id(v.draw) for v in views if v.draw is not None}
+        if len(draws) > 1:   # one fused draw per group
+            return False
         grad_on = torch.is_grad_enabled()
         slots = len({v.key for v in views if v.key not in self.keys and v.per_particle
-                     and v.tensor.requires_grad and grad_on})
+                     and v.requires_grad and grad_on})
         if self.num_slots + slots > nat.MAX_SLOTS:
             return False
         indices = []
         for v in views:
             if v.key not in self.keys:
                 mode, slot = nat.GRAD_NONE, -1
-                if v.tensor.requires_grad and grad_on:
+                if v.requires_grad and grad_on:
                     if v.per_particle:
                         mode, slot = nat.GRAD_PARTICLE, self.num_slots
                         self.num_slots += 1
@@ -184,7 +199,38 @@ class _GroupLauncher:
         return any(v.key in self.keys and v.dense for v in views)
 
     def inputs(self) -> List[torch.Tensor]:
-        return [op.view.tensor for op in self.operands]
+        """Autograd inputs: one per operand, two (loc, scale) for a fused draw."""
+        out: List[torch.Tensor] = []
+        for op in self.operands:
+            if op.view.draw is not None:
+                out.extend([op.view.draw.loc, op.view.draw.scale])
+            else:
+                out.append(op.view.tensor)
+        return out
+
+    @property
+    def draw(self) -> Optional["guide.LazyDraw"]:
+        return next((op.view.draw for op in self.operands if op.view.draw is not None), None)
+
+    def draw_supported(self) -> bool:
+        """
+        Python mirror of sites.hip draw_supported (plus the specialiser being enabled): whether
+        the group's fused draw can run, or has to be materialised before launching.
+        """
+        if self.draw is None:
+            return True
+        if os.environ.get("MININF_AMD_JIT", "1") == "0" or self.N % 4 or self.N < 512:
+            return False
+        for op in self.operands:
+            v = op.view
+            if v.draw is not None or v.constant is not None:
+                continue
+            if v.si != 0 and v.si != 1:
+                return False
+        for _, _, mask in self.sites:
+            if mask is not None and (mask.sk != 0 or mask.si not in (0, 1)):
+                return False
+        return True
 
     def describe(self, compute_grads: bool):
         """
@@ -204,10 +250,30 @@ class _GroupLauncher:
         for index, op in enumerate(self.operands):
             desc = group.operands[index]
             view = op.view
-            desc.data = view.tensor.data_ptr()
-            desc.stride_k, desc.stride_i = view.sk, view.si
             grad = None
             mode = op.mode if compute_grads else nat.GRAD_NONE
+            if view.draw is not None:
+                d = view.draw
+                desc.data = None
+                desc.stride_k, desc.stride_i = N, 1
+                desc.grad_mode = mode
+                dw = group.draw
+                dw.operand = index + 1
+                dw.stream_id = d.cfg.stream_id
+                dw.loc, dw.loc_stride = d.loc.data_ptr(), d.loc_s
+                dw.scale, dw.scale_stride = d.scale.data_ptr(), d.scale_s
+                dw.seed, dw.step = guide._philox_key(d.cfg)
+                dw.step_device = nat.ptr(d.cfg.step_device)
+                dw.particle_offset = d.cfg.particle_offset
+                if mode == nat.GRAD_DENSE:
+                    dloc = torch.empty(N, dtype=torch.float32, device=device)
+                    dscale = torch.empty(N, dtype=torch.float32, device=device)
+                    dw.dloc, dw.dscale = dloc.data_ptr(), dscale.data_ptr()
+                    grad = (dloc, dscale)
+                grads.append(grad)
+                continue
+            desc.data = view.tensor.data_ptr()
+            desc.stride_k, desc.stride_i = view.sk, view.si
             if mode == nat.GRAD_DENSE:
                 sk, si = view.sk, view.si
                 if (sk, si) in ((N, 1), (1, K)):
@@ -641,6 +707,10 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
         views = []
         for role, t in enumerate(site.tensors):
             is_value = role == len(site.tensors) - 1
+            lazy = guide.lazy_of(t)
+            if lazy is not None:   # exact-shape use, checked by _lazy_uses
+                views.append(_View(None, N, 1, None, lazy))
+                continue
             moved, constant = _to_device(_float(t, site.name), K, device, f"site '{site.name}'",
                                          allow_constant=not is_value)
             views.append(_View(None, 0, 0, constant) if constant is not None
@@ -667,6 +737,9 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
     Launch the site kernels for every recorded site and return the per-particle log joint.
     """
     K = trace.K
+    lazy, _ = _lazy_uses(trace)
+    if lazy:   # per-particle upstream gradients need the draws themselves
+        _materialize_draws(trace, lazy)
     linears = plan_linear(trace, g0, device)
     launchers, categorical = plan_groups(trace, g0, device)
     totals: List[torch.Tensor] = []
@@ -805,7 +878,11 @@ class _ElboPlan:
             holder["flags"], holder["site_lp"] = flags, site_lp
             terms.append(total)
             if need:
-                buffers.extend(g for g in grads if g is not None)
+                for g in grads:
+                    if isinstance(g, tuple):
+                        buffers.extend(g)
+                    elif g is not None:
+                        buffers.append(g)
                 if launcher.num_slots:
                     buffers.append(slot_grad[:launcher.num_slots])
             results.append((grads, slot_grad))
@@ -872,7 +949,9 @@ class _ElboPlan:
         out: List[Optional[torch.Tensor]] = []
         for launcher, (grads, slot_grad) in zip(self.launchers, results):
             for op, grad in zip(launcher.operands, grads):
-                if op.mode == nat.GRAD_DENSE:
+                if op.view.draw is not None:
+                    out.extend(grad if grad is not None else (None, None))
+                elif op.mode == nat.GRAD_DENSE:
                     out.append(grad)
                 elif op.mode == nat.GRAD_PARTICLE:
                     out.append(slot_grad[op.slot].reshape(launcher.K, 1))
@@ -896,6 +975,35 @@ class _ElboFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, u: torch.Tensor):  # type: ignore[override]
         return (None, *ctx.plan.backward(u))
+
+
+def _materialize_draws(trace: ParticleTrace, draws) -> None:
+    """
+    Replace the placeholders of the given lazy draws in the trace's site tensors by the real
+    draws (mi_normal_rsample), broadcast like the placeholders were.
+    """
+    for site in trace.sites:
+        site.tensors = [t if guide.lazy_of(t) not in draws else
+                        guide.lazy_of(t).materialize().expand(t.shape) for t in site.tensors]
+
+
+def _lazy_uses(trace: ParticleTrace) -> Tuple[set, set]:
+    """
+    (all lazy draws in the trace's site tensors, those used where the kernels cannot compute
+    them: linear / categorical sites, or broadcast beyond the draw's own shape).
+    """
+    seen, bad = set(), set()
+    for site in trace.sites:
+        for t in site.tensors:
+            lazy = guide.lazy_of(t)
+            if lazy is None:
+                continue
+            seen.add(lazy)
+            if site.linear_X is not None or site.family == "categorical" or \
+                    tuple(t.shape[1:]) != tuple(site.site_shape) or \
+                    int(site.site_shape.numel()) != lazy.N:
+                bad.add(lazy)
+    return seen, bad
 
 
 def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
@@ -935,8 +1043,16 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
     backward is one ``mi_elbo_backward`` launch (plus the guide samplers' own backward).
     """
+    _, bad = _lazy_uses(trace)
+    if bad:
+        _materialize_draws(trace, bad)
     linears = plan_linear(trace, g0, device)
-    launchers, categorical = plan_groups(trace, g0, device)
+    while True:
+        launchers, categorical = plan_groups(trace, g0, device)
+        bad = {l.draw for l in launchers if l.draw is not None and not l.draw_supported()}
+        if not bad:
+            break
+        _materialize_draws(trace, bad)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical,
                      [value for _, value in trace.fallback], factors, entropy_scale, linears)
     loss = _ElboFn.apply(plan, *plan.inputs())

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -148,7 +149,65 @@ class _BetaRsampleFn(torch.autograd.Function):
         return None, dconc
 
 
-def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
+@dataclasses.dataclass(eq=False)   # identity semantics: used in sets
+class LazyDraw:
+    """
+    A Normal factor's K draws left to the site kernels (``mi_draw``): the model is traced with
+    ``placeholder`` -- a [K, *shape] zero-stride view of a private one-element buffer, recognised
+    by its data pointer -- and site groups that read it compute ``loc + eps * scale`` in registers
+    (the same Philox eps as :class:`_NormalRsampleFn`). Any other use of the draw in the model
+    makes the loss re-trace with :meth:`materialize`\ d draws.
+    """
+    cfg: DrawConfig
+    loc: torch.Tensor
+    loc_s: int
+    scale: torch.Tensor
+    scale_s: int
+    N: int
+    shape: torch.Size
+    placeholder: torch.Tensor
+    real: Optional[torch.Tensor] = None
+
+    def materialize(self) -> torch.Tensor:
+        if self.real is None:
+            z = _NormalRsampleFn.apply(self.cfg, self.loc, self.loc_s, self.scale, self.scale_s)
+            self.real = z.reshape((self.cfg.K,) + tuple(self.shape))
+        return self.real
+
+
+# data pointer of a live placeholder -> its draw (reset by every lazy draw_all)
+_LAZY: Dict[int, LazyDraw] = {}
+
+
+def release_lazy() -> None:
+    """Forget the placeholders of the last lazy draw_all (the loss has planned its kernels)."""
+    _LAZY.clear()
+
+
+def lazy_of(tensor) -> Optional[LazyDraw]:
+    """
+    The lazy draw a tensor (a placeholder, a broadcast view of one, or a batched view inside the
+    particle vmap) stands for, or None.
+    """
+    if not _LAZY or not isinstance(tensor, torch.Tensor):
+        return None
+    functorch = torch._C._functorch
+    base = tensor
+    while functorch.is_batchedtensor(base):
+        base = functorch.get_unwrapped(base)
+    try:
+        return _LAZY.get(base.data_ptr())
+    except RuntimeError:  # tensors without storage
+        return None
+
+
+def _fusable_normal(distribution: Normal, N: int) -> bool:
+    return (N >= 512 and N % 4 == 0 and distribution.loc.is_cuda and
+            distribution.loc.dtype == torch.float32 and distribution.scale.dtype == torch.float32
+            and os.environ.get("MININF_AMD_FUSE_DRAWS", "1") != "0")
+
+
+def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> torch.Tensor:
     """
     K reparameterised draws of one guide factor: shape [K, *batch_shape, *event_shape].
     """
@@ -162,6 +221,12 @@ def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
         if cfg.noise is not None:
             cfg.noise = cfg.noise.to(device=loc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
+        elif lazy and _fusable_normal(distribution, N):
+            buffer = torch.zeros(1, dtype=torch.float32, device=loc.device)
+            placeholder = buffer.expand((cfg.K,) + tuple(shape))
+            _LAZY[buffer.data_ptr()] = LazyDraw(cfg, loc, loc_s, scale, scale_s, N,
+                                                torch.Size(shape), placeholder)
+            return placeholder
         z = _NormalRsampleFn.apply(cfg, loc, loc_s, scale, scale_s)
         return z.reshape((cfg.K,) + tuple(shape))
     if cls is Beta:
@@ -181,15 +246,18 @@ def draw(distribution: Distribution, cfg: DrawConfig) -> torch.Tensor:
 
 def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: int,
              particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None,
-             step_device: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+             step_device: Optional[torch.Tensor] = None,
+             lazy: bool = False) -> Dict[str, torch.Tensor]:
     """
-    Draw every factor of a factorised guide (dict order = stream id order).
+    Draw every factor of a factorised guide (dict order = stream id order). With ``lazy``, large
+    Normal factors become :class:`LazyDraw` placeholders evaluated inside the site kernels.
     """
+    _LAZY.clear()
     samples = {}
     for stream_id, (name, factor) in enumerate(approximation.items()):
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
                          particle_offset=particle_offset,
                          noise=None if noise is None else noise.get(name),
                          step_device=step_device)
-        samples[name] = draw(factor, cfg)
+        samples[name] = draw(factor, cfg, lazy)
     return samples

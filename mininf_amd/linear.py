@@ -24,6 +24,8 @@ import torch
 from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_map
 
+from .guide import lazy_of
+
 _functorch = torch._C._functorch
 
 _MATMULS = {torch.matmul, torch.Tensor.matmul, torch.Tensor.__matmul__, torch.mv, torch.Tensor.mv}
@@ -42,6 +44,13 @@ _METADATA = {
 # Broadcasting views of a placeholder are placeholders of the broadcast shape.
 _BROADCASTS = {torch.broadcast_tensors, torch.Tensor.expand, torch.Tensor.expand_as,
                torch.Tensor.broadcast_to, torch.broadcast_to}
+
+
+class NeedsDraws(Exception):
+    """
+    Raised while tracing when the model uses a lazy guide draw (:class:`mininf_amd.guide.LazyDraw`)
+    in an operation other than a site parameter / value: the loss then re-traces with real draws.
+    """
 
 
 @dataclasses.dataclass
@@ -63,9 +72,10 @@ class DeferredMatmul(TorchFunctionMode):
     """
     require_device = True   # defer only device matmuls (the fused kernel's operands)
 
-    def __init__(self, K: int) -> None:
+    def __init__(self, K: int, defer_matmul: bool = True) -> None:
         super().__init__()
         self.K = K
+        self.defer_matmul = defer_matmul
         self.deferred: Dict[int, Deferred] = {}
         self._keep: List[torch.Tensor] = []   # placeholders stay alive: ids are never reused
         self._bypass = False
@@ -83,6 +93,8 @@ class DeferredMatmul(TorchFunctionMode):
         if not (isinstance(X, torch.Tensor) and isinstance(theta, torch.Tensor)):
             return False
         if self.lookup(X) is not None or self.lookup(theta) is not None:
+            return False
+        if not self.defer_matmul or lazy_of(X) is not None or lazy_of(theta) is not None:
             return False
         return (not _functorch.is_batchedtensor(X) and X.dim() == 2 and
                 (X.is_cuda or not self.require_device) and
@@ -134,16 +146,23 @@ class DeferredMatmul(TorchFunctionMode):
             info = Deferred(X=X, theta=theta, shape=torch.Size([X.shape[0]]))
             return self._placeholder(theta, info.shape, info)
         touched = []
+        lazy = []
 
         def scan(x):
             info = self.lookup(x)
             if info is not None:
                 touched.append(info)
+            elif lazy_of(x) is not None:
+                lazy.append(x)
             return x
         tree_map(scan, (args, kwargs))
-        if not touched:
+        if not touched and not lazy:
             return func(*args, **kwargs)
         if func in _METADATA:
+            return func(*args, **kwargs)
+        if lazy and func not in _BROADCASTS:
+            raise NeedsDraws(getattr(func, "__name__", str(func)))
+        if not touched:
             return func(*args, **kwargs)
         if func in _BROADCASTS:
             out = func(*args, **kwargs)

@@ -19,7 +19,7 @@ from typing import Callable, cast, Dict, Optional, Set, Type
 import torch
 from torch import distributions, nn
 
-from . import engine, graph, guide, particles
+from . import engine, graph, guide, linear, particles
 from .core import condition, LogProbTracer
 from .util import _normalize_shape, maybe_as_tensor, OptionalSize, TensorDict
 
@@ -212,15 +212,24 @@ class EvidenceLowerBoundLoss(nn.Module):
             # which is then advanced on the device -- replays of a captured step draw anew.
             step = self._counter.clone()
             self._counter.add_(1)
+            # Large Normal factors are drawn lazily: the site kernels compute them in registers
+            # (mi_draw). If the model uses a draw in any other operation, the trace is repeated
+            # with real draws (same counter, same values).
             samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
-                                     step_device=step)
+                                     step_device=step, lazy=True)
+            try:
+                trace = particles.trace_particles(model, samples, K, validate=self.validate)
+            except linear.NeedsDraws:
+                guide.release_lazy()
+                samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
+                                         step_device=step)
+                trace = particles.trace_particles(model, samples, K, validate=self.validate)
         else:
             samples = approximation.rsample(torch.Size([K]))
-        if not isinstance(samples, Dict):
-            raise TypeError("Expected a distribution which samples dictionaries of tensors but got "
-                            f"a sample of type {type(samples)}")
-
-        trace = particles.trace_particles(model, samples, K, validate=self.validate)
+            if not isinstance(samples, Dict):
+                raise TypeError("Expected a distribution which samples dictionaries of tensors "
+                                f"but got a sample of type {type(samples)}")
+            trace = particles.trace_particles(model, samples, K, validate=self.validate)
         # d loss / d T_k = -1 / K exactly (fp32), matching the `mul(-1/K)` below.
         g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
         device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)),
@@ -228,7 +237,12 @@ class EvidenceLowerBoundLoss(nn.Module):
         if isinstance(approximation, dict):
             # Fused path: site kernels, guide entropy and the reduction in one autograd node.
             factors, rest = engine.entropy_factors(approximation)
-            loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world)
+            try:
+                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world)
+            finally:
+                # The placeholder registry is only needed while tracing and planning; holding it
+                # would keep this step's autograd graph (and its AccumulateGrad streams) alive.
+                guide.release_lazy()
             if rest:
                 extra = cast(torch.Tensor, sum(f.entropy().sum() for f in rest))
                 loss = loss - (extra / world if world > 1 else extra)

@@ -371,8 +371,11 @@ def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
     names = list(samples)
     tracer = ParticleTracer(validate=validate)
 
+    from .guide import _LAZY
+    use_mode = defer_matmul or bool(_LAZY)
+
     def per_particle(*values):
-        mode = DeferredMatmul(K) if defer_matmul else None
+        mode = DeferredMatmul(K, defer_matmul) if use_mode else None
         tracer.deferred = mode
         with tracer:
             if mode is not None:

@@ -106,3 +106,46 @@ def test_graph_regression_minibatch_window(device):
     assert float(captured()) < first      # it learns across replays
     assert int(counter) == 2 + 202         # warm-up steps and replays advanced the window (capture
     #                                        records the increment without executing it)
+
+
+def test_graph_replays_fused_guide_draws(device):
+    """
+    A hierarchical model whose latent vector is drawn inside the site kernel (mi_draw, the step
+    read from the device counter): graph replays must reproduce eager steps.
+    """
+    n, K = 4096, 16
+
+    def setup():
+        gen = torch.Generator().manual_seed(2)
+        y = torch.randn(n, generator=gen).to(device)
+
+        def model():
+            mu = mi.sample("mu", Normal(0.0, 1.0))
+            z = mi.sample("z", Normal(mu, 1.0), sample_shape=[n])
+            mi.sample("y", Normal(z, 0.5))
+
+        approx = mi.nn.ParameterizedFactorizedDistribution(
+            mu=mi.nn.ParameterizedDistribution(Normal, loc=0.0, scale=1.0),
+            z=mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n), scale=torch.ones(n)),
+        ).to(device)
+        optimizer = torch.optim.Adam(approx.parameters(), lr=0.01, capturable=True)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=9)
+        cond = mi.condition(model, y=y)
+
+        def step():
+            optimizer.zero_grad(set_to_none=True)
+            loss = loss_fn(cond, approx())
+            loss.backward()
+            optimizer.step()
+            return loss.detach()
+        return step, approx
+
+    eager_step, eager_approx = setup()
+    graph_body, graph_approx = setup()
+    eager = [float(eager_step()) for _ in range(6)]
+    captured = StepGraph(graph_body, warmup=2)
+    replays = [float(captured()) for _ in range(4)]
+    captured.check()
+    torch.testing.assert_close(torch.tensor(replays), torch.tensor(eager[2:]), rtol=1e-6, atol=0)
+    for a, b in zip(eager_approx.parameters(), graph_approx.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
