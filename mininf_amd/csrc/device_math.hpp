@@ -48,10 +48,11 @@ struct U4 {
 MI_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int round = 0; round < 10; ++round) {
-    const uint32_t lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one 32x32->64 multiply per word (v_mad_u64_u32) instead of separate low / high halves
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -62,13 +63,15 @@ MI_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 // Uniform in the open interval (0, 1) from the top 24 bits (exactly representable in fp32).
 MI_DEV float u01(uint32_t bits) { return ((float)(bits >> 8) + 0.5f) * 5.9604644775390625e-08f; }
 
-// Two standard normals from two uniforms (Box-Muller).
+// Two standard normals from two uniforms (Box-Muller) on the hardware transcendentals:
+// v_log_f32 (log2), v_sqrt_f32 and v_sin_f32 / v_cos_f32, which take their argument in
+// revolutions (sin(2 pi u) for u in (0, 1), no range reduction needed). Each is accurate to a few
+// ulp; the oracle (oracle/philox.c) restates the same transform in double precision.
 MI_DEV void box_muller(uint32_t a, uint32_t b, float& n0, float& n1) {
-  const float r = sqrtf(-2.0f * logf(u01(a)));
-  float s, c;
-  sincospif(2.0f * u01(b), &s, &c);
-  n0 = r * c;
-  n1 = r * s;
+  const float r = __builtin_amdgcn_sqrtf(-1.38629436111989061883f * __builtin_amdgcn_logf(u01(a)));
+  const float t = u01(b);
+  n0 = r * __builtin_amdgcn_cosf(t);
+  n1 = r * __builtin_amdgcn_sinf(t);
 }
 
 // Counter layout of the guide generator (see include/mininf_amd.h, mi_normal_rsample):

@@ -564,8 +564,8 @@ bool compile_only(const std::string& source, std::vector<char>* code, std::strin
   if (hiprtcCreateProgram(&prog, source.c_str(), "mi_site_program.hip", 3, headers, names) !=
       HIPRTC_SUCCESS)
     return false;
-  const char* options[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, options);
+  const char* options[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, options);
   if (log != nullptr) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);

@@ -778,6 +778,7 @@ bool bcast_eligible(const mi_group* g) {
 
 struct Plan {
   Shape shape;
+  int elems;               // ROW: elements per lane per row
   int64_t nseg;
   int64_t rows_per_block;  // ROW
   int64_t seg_len;         // COL
@@ -803,7 +804,10 @@ Plan make_plan(const mi_group* g) {
                             llabs(g->operands[dense].stride_i) < llabs(g->operands[dense].stride_k);
   if (row || row_fallback) {
     p.shape = kRow;
-    p.nseg = ceil_div(g->N, 64 * row_elems());
+    // fused draws: one Philox quad per lane and row keeps the register footprint at 4 waves/SIMD
+    p.elems = g->draw.operand != 0 ? (env_int("MININF_AMD_DRAW_ELEMS", 4) == 8 ? 8 : 4)
+                                   : row_elems();
+    p.nseg = ceil_div(g->N, 64 * p.elems);
     const int64_t gx = ceil_div(p.nseg, 4);
     int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(kTargetBlocks, gx)));
     p.rows_per_block = ceil_div(g->K, gy);
@@ -832,8 +836,8 @@ PlanInfo plan_info(const Plan& p, bool combined) {
   info.combined = combined;
   info.row = p.shape == kRow;
   // Tuning knobs (measured defaults; the env overrides exist for sweeps).
-  info.elems = p.shape == kRow ? row_elems() : std::max(1, env_int("MININF_AMD_COL_UNROLL",
-                                                                        kColUnroll));
+  info.elems = p.shape == kRow ? p.elems : std::max(1, env_int("MININF_AMD_COL_UNROLL",
+                                                                     kColUnroll));
   info.waves_per_eu = env_int("MININF_AMD_WAVES_PER_EU", 0);
   info.kw = p.kw;
   info.grid_x = p.grid.x;
@@ -1001,7 +1005,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
       }
       if (G.draw.operand != 0) return MI_EUNSUPPORTED;  // fused draws need the specialised kernel
       if (p.shape == kRow) {
-        const int e = row_elems();
+        const int e = p.elems;
         if (e == 4)
           hipLaunchKernelGGL((mi::k_group_row<4>), p.grid, dim3(256), 0, s, G, part, p.nseg,
                              p.rows_per_block, flags);
