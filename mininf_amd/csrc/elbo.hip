@@ -71,6 +71,9 @@ MI_DEV double block_sum(double v, double* red) {
   return s;
 }
 
+// HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
+// of the common large-factor case small (the Beta path carries fp64 lgamma / digamma).
+template <bool HAS_BETA>
 __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, double* partial,
                                                                unsigned* __restrict__ counter,
                                                                float* __restrict__ loss) {
@@ -83,7 +86,16 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E, 
     for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
   for (int f = 0; f < E.num_factors; ++f) {
     const mi_factor& F = E.factors[f];
-    for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i, nullptr, nullptr);
+    if (!HAS_BETA || F.family == MI_NORMAL) {
+      const float* __restrict__ sc = F.param[1];
+      const int64_t ss = F.stride[1];
+      float hf = 0.0f;   // per-thread partial of <= a few hundred terms, then fp64
+      for (int64_t i = first; i < F.n; i += stride) hf += logf(sc[i * ss]);
+      h += (double)hf + 1.4189385332046727 * (double)((F.n - first + stride - 1) / stride > 0 ?
+                                                        (F.n - first + stride - 1) / stride : 0);
+    } else {
+      for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i, nullptr, nullptr);
+    }
   }
   const double s = block_sum((double)E.g0 * lp - E.entropy_scale * h, red);
   if (threadIdx.x == 0) {
@@ -204,8 +216,16 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
   if (workspace_bytes < need) return MI_EWORKSPACE;
   auto* counter = static_cast<unsigned*>(workspace);
   auto* partial = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256);
-  hipLaunchKernelGGL(mi::k_elbo_forward, dim3(forward_blocks(elbo)), dim3(mi::kElboThreads), 0,
-                     static_cast<hipStream_t>(stream), *elbo, partial, counter, loss);
+  bool has_beta = false;
+  for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family == MI_BETA;
+  if (has_beta)
+    hipLaunchKernelGGL(mi::k_elbo_forward<true>, dim3(forward_blocks(elbo)),
+                       dim3(mi::kElboThreads), 0, static_cast<hipStream_t>(stream), *elbo, partial,
+                       counter, loss);
+  else
+    hipLaunchKernelGGL(mi::k_elbo_forward<false>, dim3(forward_blocks(elbo)),
+                       dim3(mi::kElboThreads), 0, static_cast<hipStream_t>(stream), *elbo, partial,
+                       counter, loss);
   return to_code(hipGetLastError());
 }
 

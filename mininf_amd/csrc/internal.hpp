@@ -3,12 +3,16 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 // Fixed-order fp64 reduction of per-(segment, particle) partials part[v][nseg][K] (sites.hip
 // k_finalize): values v < num_sites are multiplied by scale[v] and summed into total[k] (and
 // written to site_lp[v*K + k] when non-NULL); the remaining num_slots values are multiplied by
 // slot_scale and written to slot_grad[(v - num_sites)*K + k].
+// With long segment lists (> 512) and a `scratch` of mi_finalize_scratch_bytes, the reduction
+// runs in two launches (segment chunks in parallel, then the chunk sums); otherwise in one.
+size_t mi_finalize_scratch_bytes(int64_t nseg, int64_t K, int nv);
 int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
                        const double* scale, double slot_scale, float* total, double* site_lp,
-                       float* slot_grad, hipStream_t stream);
+                       float* slot_grad, double* scratch, hipStream_t stream);

@@ -198,6 +198,11 @@ Geometry geometry(const mi_linear* L) {
 
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
+// per-(tile, particle) partials, 256-byte aligned so the finalize scratch behind them is too
+size_t partial_bytes(const mi_linear* site, const Geometry& g) {
+  return ((size_t)g.nv * (size_t)g.ntile * (size_t)site->K * sizeof(float) + 255) / 256 * 256;
+}
+
 template <int FAMILY>
 void launch(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 grid((unsigned)g.ntile, (unsigned)g.gy);
@@ -228,7 +233,7 @@ int mi_linear_struct_size(size_t* bytes) {
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes) {
   if (!valid(site) || bytes == nullptr) return MI_EINVAL;
   const Geometry g = geometry(site);
-  *bytes = (size_t)g.nv * (size_t)g.ntile * (size_t)site->K * sizeof(float);
+  *bytes = partial_bytes(site, g) + mi_finalize_scratch_bytes(g.ntile, site->K, g.nv);
   return 0;
 }
 
@@ -260,8 +265,9 @@ int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t works
   if (stop_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s)) != hipSuccess)
     return to_code(e);
   const double scale = site->site_scale;
+  double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) + partial_bytes(site, g));
   return mi_launch_finalize(part, g.ntile, site->K, 1, site->compute_grads ? g.nv - 1 : 0, &scale,
-                            (double)site->grad_scale, total, nullptr, dslots, s);
+                            (double)site->grad_scale, total, nullptr, dslots, scratch, s);
 }
 
 int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,

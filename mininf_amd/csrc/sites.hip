@@ -559,7 +559,40 @@ struct FinalizeArgs {
 constexpr int kFinK = 64;
 constexpr int kFinG = 16;
 
-__global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restrict__ part,
+// Stage 1 of the two-stage finalize for long segment lists: block (k-block, v, chunk) sums the
+// chunk's segments of value v for 64 particles (fixed order) into stage[v][chunk][k] (fp64).
+constexpr int64_t kFinChunk = 256;
+
+__global__ __launch_bounds__(kFinK * kFinG) void k_finalize_chunks(const float* __restrict__ part,
+                                                                  int64_t nseg, int64_t K,
+                                                                  double* __restrict__ stage) {
+  __shared__ double red[kFinG][kFinK];
+  const int kl = threadIdx.x % kFinK;
+  const int gl = threadIdx.x / kFinK;
+  const int64_t k = (int64_t)blockIdx.x * kFinK + kl;
+  const int64_t kc = k < K ? k : K - 1;
+  const int64_t v = blockIdx.y, c = blockIdx.z, nchunk = gridDim.z;
+  const int64_t g0 = c * kFinChunk, g1 = min(nseg, g0 + kFinChunk);
+  const float* p = part + v * nseg * K + kc;
+  double a0 = 0.0, a1 = 0.0;
+  int64_t g = g0 + gl;
+  for (; g + kFinG < g1; g += 2 * kFinG) {
+    a0 += (double)p[g * K];
+    a1 += (double)p[(g + kFinG) * K];
+  }
+  for (; g < g1; g += kFinG) a0 += (double)p[g * K];
+  red[gl][kl] = a0 + a1;
+  __syncthreads();
+  if (gl == 0 && k < K) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kFinG; ++j) acc += red[j][kl];
+    stage[(v * nchunk + c) * K + k] = acc;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const T* __restrict__ part,
                                                            int64_t nseg, int64_t K,
                                                            const FinalizeArgs A,
                                                            float* __restrict__ total,
@@ -578,7 +611,7 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const float* __restr
   const int v_begin = split ? (int)blockIdx.y : 0;
   const int v_end = split ? v_begin + 1 : nv;
   for (int v = v_begin; v < v_end; ++v) {
-    const float* p = part + (int64_t)v * nseg * K + kc;
+    const T* p = part + (int64_t)v * nseg * K + kc;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     int64_t g = gl;
     for (; g + 3 * kFinG < nseg; g += 4 * kFinG) {
@@ -802,7 +835,11 @@ Plan make_plan(const mi_group* g) {
   const bool row = dense >= 0 && g->operands[dense].stride_i == 1 && g->operands[dense].stride_k != 1;
   const bool row_fallback = dense >= 0 && g->operands[dense].stride_k != 1 && g->operands[dense].stride_i != 1 &&
                             llabs(g->operands[dense].stride_i) < llabs(g->operands[dense].stride_k);
-  if (row || row_fallback) {
+  // Short element spaces (e.g. a prior over a handful of coefficients) have too few row
+  // segments to fill the chip and would loop over all particles serially: lanes go along
+  // particles instead.
+  const bool short_rows = g->N < 256 && g->draw.operand == 0;
+  if ((row || row_fallback) && !short_rows) {
     p.shape = kRow;
     // fused draws: one Philox quad per lane and row keeps the register footprint at 4 waves/SIMD
     p.elems = g->draw.operand != 0 ? (env_int("MININF_AMD_DRAW_ELEMS", 4) == 8 ? 8 : 4)
@@ -861,29 +898,49 @@ size_t draw_partial_floats(const mi_group* g, const Plan& p) {
   return 2 * (size_t)p.grid.y * (size_t)g->N;
 }
 
+size_t finalize_offset(const mi_group* g, const Plan& p) {
+  const size_t middle = p.shape != kBcast ? draw_partial_floats(g, p) * sizeof(float)
+                                          : (size_t)mi::kPrep * (size_t)g->K * sizeof(float);
+  return (prep_offset(g, p) + middle + 255) / 256 * 256;
+}
+
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
-  if (p.shape != kBcast)
-    return prep_offset(g, p) + draw_partial_floats(g, p) * sizeof(float);
-  return prep_offset(g, p) + (size_t)mi::kPrep * (size_t)g->K * sizeof(float);
+  return finalize_offset(g, p) +
+         mi_finalize_scratch_bytes(p.nseg, g->K, g->num_sites + g->num_slots);
 }
 
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 }  // namespace
 
+size_t mi_finalize_scratch_bytes(int64_t nseg, int64_t K, int nv) {
+  if (nseg <= 2 * mi::kFinChunk) return 0;
+  return (size_t)nv * (size_t)ceil_div(nseg, mi::kFinChunk) * (size_t)K * sizeof(double);
+}
+
 int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
                        const double* scale, double slot_scale, float* total, double* site_lp,
-                       float* slot_grad, hipStream_t stream) {
+                       float* slot_grad, double* scratch, hipStream_t stream) {
   if (num_sites > MI_MAX_SITES) return MI_EINVAL;
   mi::FinalizeArgs A{};
   A.num_sites = num_sites;
   A.num_slots = num_slots;
   A.slot_scale = slot_scale;
   for (int i = 0; i < num_sites; ++i) A.scale[i] = scale[i];
-  const unsigned gy = num_sites == 1 ? (unsigned)(1 + num_slots) : 1u;
-  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(K, mi::kFinK), gy),
-                     dim3(mi::kFinK * mi::kFinG), 0, stream, part, nseg, K, A, total, site_lp,
-                     slot_grad);
+  const int nv = num_sites + num_slots;
+  const unsigned gx = (unsigned)ceil_div(K, mi::kFinK);
+  const unsigned gy = num_sites == 1 ? (unsigned)nv : 1u;
+  if (scratch != nullptr && mi_finalize_scratch_bytes(nseg, K, nv) != 0) {
+    // long segment lists: chunks of segments in parallel, then the chunk sums
+    const int64_t nchunk = ceil_div(nseg, mi::kFinChunk);
+    hipLaunchKernelGGL(mi::k_finalize_chunks, dim3(gx, (unsigned)nv, (unsigned)nchunk),
+                       dim3(mi::kFinK * mi::kFinG), 0, stream, part, nseg, K, scratch);
+    hipLaunchKernelGGL(mi::k_finalize<double>, dim3(gx, gy), dim3(mi::kFinK * mi::kFinG), 0,
+                       stream, scratch, nchunk, K, A, total, site_lp, slot_grad);
+  } else {
+    hipLaunchKernelGGL(mi::k_finalize<float>, dim3(gx, gy), dim3(mi::kFinK * mi::kFinG), 0,
+                       stream, part, nseg, K, A, total, site_lp, slot_grad);
+  }
   return to_code(hipGetLastError());
 }
 
@@ -1033,16 +1090,12 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
     e = hipGetLastError();
     if (e != hipSuccess) return to_code(e);
   }
-  mi::FinalizeArgs A{};
-  A.num_sites = reduced_lp;
-  A.num_slots = G.num_slots;
-  A.slot_scale = (double)G.grad_scale;
-  for (int i = 0; i < reduced_lp; ++i) A.scale[i] = prescaled ? 1.0 : G.sites[i].scale;
-  const unsigned gy = reduced_lp == 1 ? (unsigned)(1 + A.num_slots) : 1u;
-  hipLaunchKernelGGL(mi::k_finalize, dim3((unsigned)ceil_div(G.K, mi::kFinK), gy),
-                     dim3(mi::kFinK * mi::kFinG), 0, s, part, p.nseg, G.K, A, total, site_lp,
-                     slot_grad);
-  return to_code(hipGetLastError());
+  double scales[MI_MAX_SITES];
+  for (int i = 0; i < reduced_lp; ++i) scales[i] = prescaled ? 1.0 : G.sites[i].scale;
+  double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) +
+                                              finalize_offset(group, p));
+  return mi_launch_finalize(part, p.nseg, G.K, reduced_lp, G.num_slots, scales,
+                            (double)G.grad_scale, total, site_lp, slot_grad, scratch, s);
 }
 
 int mi_group_source(const mi_group* group, char* out, size_t out_bytes, size_t* needed) {
