@@ -1,0 +1,10 @@
+#!/bin/bash
+# Kernel traces of several configs (graph replay, as benched): usage gpurun_trace2.sh c2 c5 ...
+set -u
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for cfg in "$@"; do
+  rm -rf gpurun_out/trace_$cfg
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_$cfg -o run --output-format csv -- python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/trace_$cfg.log 2>&1
+  rc=$?; echo "trace $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done

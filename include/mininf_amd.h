@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 2
+#define MI_ABI_VERSION 3
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -61,6 +61,10 @@ enum mi_grad_mode {
 /* mi_group.options: the caller has zeroed `flags` (e.g. one buffer for every group of a step),
  * so mi_group_forward does not reset them. */
 #define MI_GROUP_FLAGS_ZEROED 1
+/* mi_group.options: leave the fused draw's per-particle-block partial sums of dloc / dscale in the
+ * workspace (mi_group_draw_partials) instead of reducing them into draw.dloc / draw.dscale -- the
+ * ELBO backward reduces them (MI_DRAW_PARTIALS). */
+#define MI_GROUP_DRAW_PARTIALS 2
 
 #define MI_FLAG_SUPPORT 1u  /* a (non-masked) value lies outside the family's support */
 #define MI_FLAG_PARAM 2u    /* a parameter violates its constraint (e.g. scale <= 0) */
@@ -160,6 +164,10 @@ int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_by
 int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
                            float* total, double* site_lp, float* slot_grad, uint32_t* flags,
                            void* start_event, void* stop_event, void* stream);
+
+/* Where a fused-draw group leaves its partial sums (MI_GROUP_DRAW_PARTIALS): dloc partials are
+ * rows [rows, N] at workspace + offset_bytes, dscale partials the next rows * N floats. */
+int mi_group_draw_partials(const mi_group* group, size_t* offset_bytes, int64_t* rows);
 
 /* The kernel source the engine specialises for `group` (site families, role kinds and gradient
  * targets compiled in; see mininf_amd/csrc/jit.cpp). Writes at most out_bytes (NUL-terminated) and
@@ -292,18 +300,58 @@ int mi_linear_struct_size(size_t* bytes);
 #define MI_MAX_BUFFERS 16
 
 /* One mean-field guide factor whose entropy enters the ELBO, viewed as n elements:
- *   MI_NORMAL: param[1] = scale (param[0], loc, is not read);   grad[1] = d loss / d scale
- *   MI_BETA:   param[0] = concentration1, param[1] = concentration0; grad[0], grad[1]
- * Parameters are fp32 with element stride `stride` (0 only when n == 1); grads (written by
- * mi_elbo_backward, may be NULL) use the same element strides, e.g. both Beta parameters and both
- * gradients interleaved in one [n, 2] concentration array. */
+ *   MI_NORMAL: param[0] = loc (read only with an absorbed draw), param[1] = scale
+ *   MI_BETA:   param[0] = concentration1, param[1] = concentration0
+ * Parameters are fp32 with element stride `stride` (0 only when n == 1). mi_elbo_backward writes
+ *   grad[j][i * grad_stride[j]] = d loss / d param_j(i)                  (transform[j] NONE)
+ *                               = d loss / d u_j(i) = (d loss / d param_j) * param_j
+ *                                                       (transform[j] EXP: param_j = exp(u_j))
+ * for every non-NULL grad[j]. The transforms restate ParameterizedDistribution's
+ * transform_to(constraint) (nn.py:86-96): EXP is transform_to(positive) = exp.
+ *
+ * Absorbed guide draw (draw_kind != MI_DRAW_NONE). The factor's K draws z (Normal: z = loc +
+ * eps * scale, normal.py:83-86; Beta: implicit reparameterisation, dirichlet.py:17-20) feed only
+ * site kernels of this ELBO, so d loss / d param also carries the draws' backward (what
+ * mi_normal_rsample_backward / mi_beta_rsample_backward and autograd's accumulation would add):
+ *   MI_DRAW_SOURCES:  dz[k, i] = sum_s source[s].ptr[k * stride_k + i * stride_i]  (pre-scaled by
+ *                     g0, like every speculative site gradient); Normal: eps from the generator
+ *                     (seed, step, step_device, stream_id, particle_offset) or `eps` [K, n];
+ *                     Beta: `draws` holds x [K, n] row-major.
+ *   MI_DRAW_PARTIALS: Normal draws fused into a site group (mi_draw): partial[0] / partial[1] hold
+ *                     partial_rows rows [rows, n] of sum_k g0 dT/dz and sum_k g0 dT/dz * eps. */
+#define MI_TRANSFORM_NONE 0
+#define MI_TRANSFORM_EXP 1
+#define MI_DRAW_NONE 0
+#define MI_DRAW_SOURCES 1
+#define MI_DRAW_PARTIALS 2
+#define MI_MAX_SOURCES 4
+
+typedef struct mi_source {
+  const float* ptr;
+  int64_t stride_k;
+  int64_t stride_i;
+} mi_source;
+
 typedef struct mi_factor {
   int32_t family;
-  int32_t pad0;
+  int32_t draw_kind;            /* MI_DRAW_* */
   int64_t n;
   const float* param[2];
   int64_t stride[2];
   float* grad[2];
+  int64_t grad_stride[2];
+  int32_t transform[2];         /* MI_TRANSFORM_* per parameter */
+  int32_t num_sources;
+  uint32_t stream_id;
+  mi_source source[MI_MAX_SOURCES];
+  const float* draws;           /* Beta draws x [K, n] */
+  const float* eps;             /* Normal: injected noise [K, n], or NULL to regenerate */
+  uint64_t seed;
+  uint64_t step;
+  const uint64_t* step_device;  /* may be NULL; added to step */
+  int64_t particle_offset;
+  const float* partial[2];      /* MI_DRAW_PARTIALS */
+  int64_t partial_rows;
 } mi_factor;
 
 /* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f sum_i H_f(i)
@@ -329,9 +377,11 @@ typedef struct mi_elbo {
 /* sizeof(mi_factor), sizeof(mi_elbo) as compiled. */
 int mi_elbo_struct_sizes(size_t* factor, size_t* elbo);
 
-/* Workspace of mi_elbo_forward. It holds a completion counter that must be zero before first use
- * (mi_elbo_workspace_init) and that every forward leaves at zero, so one workspace serves every
- * step (and captured HIP graphs) on one stream. */
+/* Workspace of mi_elbo_forward and mi_elbo_backward. Its first MI_ELBO_COUNTER_BYTES hold
+ * completion counters that must be zero before first use (mi_elbo_workspace_init) and that every
+ * launch leaves at zero, so one workspace serves every step (and captured HIP graphs) on one
+ * stream. */
+#define MI_ELBO_COUNTER_BYTES 16640
 int mi_elbo_workspace_bytes(const mi_elbo* elbo, size_t* bytes);
 int mi_elbo_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 
@@ -340,9 +390,11 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
                     void* stream);
 
 /* With u = *upstream (device scalar, d out / d loss): dterm[0] = u * g0 (the gradient of every
- * term element), factors[f].grad[j][i] = -u * entropy_scale * dH_f(i)/dparam_j, and every buffer
- * is multiplied by u unless u == 1. One launch. */
-int mi_elbo_backward(const mi_elbo* elbo, const float* upstream, float* dterm, void* stream);
+ * term element); factors[f].grad[j] = the gradient of -u * entropy_scale * H_f (plus u times the
+ * absorbed draw's backward, and the transform's chain rule; see mi_factor); every buffer is
+ * multiplied by u unless u == 1. One launch; `workspace` is the mi_elbo_forward workspace. */
+int mi_elbo_backward(const mi_elbo* elbo, const float* upstream, float* dterm, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

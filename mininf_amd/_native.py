@@ -29,6 +29,11 @@ LINEAR_MAX_P = 64
 NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
 GROUP_FLAGS_ZEROED = 1
+GROUP_DRAW_PARTIALS = 2
+TRANSFORM_NONE, TRANSFORM_EXP = 0, 1
+DRAW_NONE, DRAW_SOURCES, DRAW_PARTIALS = 0, 1, 2
+MAX_SOURCES = 4
+ELBO_COUNTER_BYTES = 16640
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -88,10 +93,19 @@ class Linear(ctypes.Structure):
     ]
 
 
+class Source(ctypes.Structure):
+    _fields_ = [("ptr", c_vp), ("stride_k", c_i64), ("stride_i", c_i64)]
+
+
 class Factor(ctypes.Structure):
     _fields_ = [
-        ("family", ctypes.c_int32), ("pad0", ctypes.c_int32), ("n", c_i64),
+        ("family", ctypes.c_int32), ("draw_kind", ctypes.c_int32), ("n", c_i64),
         ("param", c_vp * 2), ("stride", c_i64 * 2), ("grad", c_vp * 2),
+        ("grad_stride", c_i64 * 2), ("transform", ctypes.c_int32 * 2),
+        ("num_sources", ctypes.c_int32), ("stream_id", ctypes.c_uint32),
+        ("source", Source * MAX_SOURCES), ("draws", c_vp), ("eps", c_vp),
+        ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
+        ("particle_offset", c_i64), ("partial", c_vp * 2), ("partial_rows", c_i64),
     ]
 
 
@@ -115,6 +129,9 @@ _SIGNATURES = {
                                         c_vp, c_vp, c_vp]),
     "mi_group_forward_timed": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp,
                                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mi_group_draw_partials": (ctypes.c_int, [ctypes.POINTER(Group),
+                                              ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(c_i64)]),
     "mi_group_source": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.c_char_p, ctypes.c_size_t,
                                        ctypes.POINTER(ctypes.c_size_t)]),
     "mi_group_compile_check": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.c_char_p,
@@ -159,7 +176,8 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
     "mi_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp, c_vp]),
-    "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp]),
+    "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
+                                        c_vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = [os.path.join(CSRC, name)
            for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "jit.cpp")]
-HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "jit.hpp",
+HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "beta_grad.hpp", "jit.hpp",
                                                  "internal.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]
 EMBEDDED = {"embedded_header.inc": os.path.join(INCLUDE, "mininf_amd.h"),

@@ -750,7 +750,8 @@ bool validate_group(const mi_group* g) {
   const int draw = g->draw.operand - 1;
   if (draw >= g->num_operands || draw < -1) return false;
   if (draw >= 0 && (g->draw.loc == nullptr || g->draw.scale == nullptr ||
-                    (g->compute_grads && (g->draw.dloc == nullptr || g->draw.dscale == nullptr))))
+                    (g->compute_grads && !(g->options & MI_GROUP_DRAW_PARTIALS) &&
+                     (g->draw.dloc == nullptr || g->draw.dscale == nullptr))))
     return false;
   for (int o = 0; o < g->num_operands; ++o) {
     const mi_operand& op = g->operands[o];
@@ -892,9 +893,11 @@ size_t prep_offset(const mi_group* g, const Plan& p) {
   return (partial_bytes(g, p) + 255) / 256 * 256;
 }
 
-// Per-K-block partial dloc / dscale of a fused draw (when the grid splits the particles).
+// Per-K-block partial dloc / dscale of a fused draw (when the grid splits the particles, or when
+// the caller reduces them itself: MI_GROUP_DRAW_PARTIALS).
 size_t draw_partial_floats(const mi_group* g, const Plan& p) {
-  if (g->draw.operand == 0 || !g->compute_grads || p.grid.y <= 1) return 0;
+  if (g->draw.operand == 0 || !g->compute_grads) return 0;
+  if (p.grid.y <= 1 && !(g->options & MI_GROUP_DRAW_PARTIALS)) return 0;
   return 2 * (size_t)p.grid.y * (size_t)g->N;
 }
 
@@ -1084,7 +1087,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
     e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s);
     if (e != hipSuccess) return to_code(e);
   }
-  if (draw_partials != nullptr) {
+  if (draw_partials != nullptr && !(G.options & MI_GROUP_DRAW_PARTIALS)) {
     hipLaunchKernelGGL(mi::k_draw_reduce, dim3((unsigned)ceil_div(G.N, 256)), dim3(256), 0, s,
                        draw_partials, (int64_t)p.grid.y, G.N, G.draw.dloc, G.draw.dscale);
     e = hipGetLastError();
@@ -1096,6 +1099,16 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
                                               finalize_offset(group, p));
   return mi_launch_finalize(part, p.nseg, G.K, reduced_lp, G.num_slots, scales,
                             (double)G.grad_scale, total, site_lp, slot_grad, scratch, s);
+}
+
+int mi_group_draw_partials(const mi_group* group, size_t* offset_bytes, int64_t* rows) {
+  if (!validate_group(group) || offset_bytes == nullptr || rows == nullptr) return MI_EINVAL;
+  if (!(group->options & MI_GROUP_DRAW_PARTIALS)) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  if (draw_partial_floats(group, p) == 0) return MI_EINVAL;
+  *offset_bytes = prep_offset(group, p);
+  *rows = (int64_t)p.grid.y;
+  return 0;
 }
 
 int mi_group_source(const mi_group* group, char* out, size_t out_bytes, size_t* needed) {

@@ -159,6 +159,10 @@ class _GroupLauncher:
         self.keys: Dict[Tuple, int] = {}
         self.sites: List[Tuple[SiteRecord, List[int], Optional[torch.Tensor]]] = []
         self.num_slots = 0
+        # the fused draw's dloc / dscale partials stay in the workspace for the ELBO backward
+        # (MI_GROUP_DRAW_PARTIALS); set by the ELBO plan when it absorbs the draw
+        self.draw_partials = False
+        self.workspace: Optional[torch.Tensor] = None   # of the last run
 
     def try_add(self, site: SiteRecord, views: List[_View], mask: Optional[_View]) -> bool:
         constants = [v.constant for v in views]
@@ -198,14 +202,18 @@ class _GroupLauncher:
     def shares_dense_operand(self, views: List[_View]) -> bool:
         return any(v.key in self.keys and v.dense for v in views)
 
-    def inputs(self) -> List[torch.Tensor]:
-        """Autograd inputs: one per operand, two (loc, scale) for a fused draw."""
-        out: List[torch.Tensor] = []
-        for op in self.operands:
+    def inputs(self, skip: Sequence[int] = ()) -> List[Optional[torch.Tensor]]:
+        """
+        Autograd inputs: one per operand, two (loc, scale) for a fused draw; None for the operands
+        in ``skip`` (draws whose backward the ELBO absorbs).
+        """
+        out: List[Optional[torch.Tensor]] = []
+        for index, op in enumerate(self.operands):
             if op.view.draw is not None:
-                out.extend([op.view.draw.loc, op.view.draw.scale])
+                out.extend([None, None] if index in skip else [op.view.draw.loc,
+                                                               op.view.draw.scale])
             else:
-                out.append(op.view.tensor)
+                out.append(None if index in skip else op.view.tensor)
         return out
 
     @property
@@ -265,7 +273,9 @@ class _GroupLauncher:
                 dw.seed, dw.step = guide._philox_key(d.cfg)
                 dw.step_device = nat.ptr(d.cfg.step_device)
                 dw.particle_offset = d.cfg.particle_offset
-                if mode == nat.GRAD_DENSE:
+                if mode == nat.GRAD_DENSE and self.draw_partials:
+                    group.options |= nat.GROUP_DRAW_PARTIALS
+                elif mode == nat.GRAD_DENSE:
                     dloc = torch.empty(N, dtype=torch.float32, device=device)
                     dscale = torch.empty(N, dtype=torch.float32, device=device)
                     dw.dloc, dw.dscale = dloc.data_ptr(), dscale.data_ptr()
@@ -353,6 +363,13 @@ class _GroupLauncher:
             nat.ptr(site_lp), slot_grad.data_ptr(), flags.data_ptr(),
             None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
             nat.stream_handle(device)), "mi_group_forward_timed")
+        self.workspace = workspace
+        self.partials = None
+        if group.options & nat.GROUP_DRAW_PARTIALS:
+            offset, rows = ctypes.c_size_t(), ctypes.c_int64()
+            nat.check(lib.mi_group_draw_partials(ctypes.byref(group), ctypes.byref(offset),
+                                                 ctypes.byref(rows)), "mi_group_draw_partials")
+            self.partials = (workspace.data_ptr() + offset.value, rows.value)
         return total, site_lp, grads, slot_grad, flags
 
 
@@ -775,11 +792,179 @@ class EntropyFactor:
     """
     A guide factor whose entropy the ELBO kernels evaluate (``mi_factor``): ``tensor`` is the
     autograd input -- Normal: the scale as [n] (stride 1, or any stride when n == 1); Beta: the
-    interleaved [n, 2] concentration array.
+    interleaved [n, 2] concentration array. ``name`` / ``distribution`` identify the factor's
+    draw in the samples (for absorbing the draw's backward).
     """
     family: int
     n: int
     tensor: torch.Tensor
+    name: Optional[str] = None
+    distribution: Optional[object] = None
+
+
+@dataclasses.dataclass(eq=False)
+class _Absorbed:
+    """
+    A guide factor whose draw feeds only this ELBO's kernels: the ELBO backward computes the
+    draw's backward, the entropy gradient and the guide transform's chain rule in one kernel and
+    returns the gradients of the module's unconstrained parameters directly (``mi_factor`` with
+    ``draw_kind``). ``uses``: (kind, launcher / linear index, operand index) with kind in
+    "draw" (fused draw partials), "dense", "slot" (group gradients), "lin_theta", "lin_sigma".
+    ``params``: per factor parameter (Normal loc, scale; Beta concentration1, concentration0) the
+    unconstrained tensor and its MI_TRANSFORM, or None for a constant.
+    """
+    kind: int
+    uses: List[Tuple[str, int, int]]
+    params: List[Optional[Tuple[torch.Tensor, int]]]
+    drawn: Optional[guide.Drawn] = None
+    lazy: Optional[guide.LazyDraw] = None
+
+
+_FACTOR_PARAMS = {nat.NORMAL: ("loc", "scale"), nat.BETA: ("concentration1", "concentration0")}
+
+
+def _depends_on(tensors: Sequence[Optional[torch.Tensor]], target, limit: int = 20000) -> bool:
+    """
+    Whether autograd would route a gradient from any of ``tensors`` into the node ``target``.
+    """
+    if target is None:
+        return False
+    stack = [t.grad_fn for t in tensors if isinstance(t, torch.Tensor) and t.grad_fn is not None]
+    seen = set()
+    keep = []
+    while stack:
+        fn = stack.pop()
+        if fn is None or id(fn) in seen:
+            continue
+        if fn is target:
+            return True
+        seen.add(id(fn))
+        keep.append(fn)
+        if len(seen) > limit:
+            return True   # too large to prove independence
+        stack.extend(next_fn for next_fn, _ in fn.next_functions)
+    return False
+
+
+def _absorb_factor(factor: EntropyFactor, samples: Dict[str, torch.Tensor], launchers, linears,
+                   categorical, fallback) -> Optional[_Absorbed]:
+    """
+    The absorption plan of one guide factor, or None when its draw's backward has to stay with
+    autograd (the draw reaches the loss other than through the kernels' own operands, a parameter
+    does not come straight from a ParameterizedDistribution, ...).
+    """
+    dist = factor.distribution
+    if dist is None or factor.name is None or factor.name not in samples:
+        return None
+    sources = getattr(dist, "_mininf_amd_sources", None) or {}
+    params: List[Optional[Tuple[torch.Tensor, int]]] = []
+    for pname in _FACTOR_PARAMS[factor.family]:
+        source = sources.get(pname)
+        if source is None:
+            value = getattr(dist, pname, None)
+            if isinstance(value, torch.Tensor) and value.requires_grad:
+                return None   # derived some other way: autograd keeps it
+            params.append(None)
+            continue
+        u, kind = source
+        if tuple(u.shape) != tuple(dist.batch_shape) or u.dtype != torch.float32 or \
+                not u.is_cuda or (u.numel() > 1 and not u.is_contiguous()):
+            return None
+        transform = nat.TRANSFORM_EXP if kind == "exp" else nat.TRANSFORM_NONE
+        params.append((u, transform) if u.requires_grad else None)
+    if all(p is None for p in params):
+        return None
+    sample = samples[factor.name]
+    uses: List[Tuple[str, int, int]] = []
+    lazy = guide.lazy_of(sample)
+    if lazy is not None:
+        if lazy.real is not None or factor.family != nat.NORMAL:
+            return None
+        for li, launcher in enumerate(launchers):
+            for oi, op in enumerate(launcher.operands):
+                if op.view.draw is lazy:
+                    if op.mode != nat.GRAD_DENSE:
+                        return None
+                    uses.append(("draw", li, oi))
+        if len(uses) != 1:
+            return None
+        return _Absorbed(nat.DRAW_PARTIALS, uses, params, lazy=lazy)
+    drawn = guide.drawn_of(sample)
+    if drawn is None or drawn.base._version != 0:
+        return None
+    if (drawn.family == guide.BETA_FAMILY) != (factor.family == nat.BETA):
+        return None
+    z = drawn.base
+    N = drawn.N
+    storage = z.untyped_storage().data_ptr()
+
+    def shares(t) -> bool:
+        return isinstance(t, torch.Tensor) and t.untyped_storage().data_ptr() == storage
+
+    others: List[Optional[torch.Tensor]] = []
+    for li, launcher in enumerate(launchers):
+        for oi, op in enumerate(launcher.operands):
+            v = op.view
+            if v.draw is not None:
+                others.extend([v.draw.loc, v.draw.scale])
+                continue
+            if v.tensor is None:
+                continue
+            if not shares(v.tensor):
+                others.append(v.tensor)
+                continue
+            if v.tensor.data_ptr() != z.data_ptr():
+                return None
+            if op.mode == nat.GRAD_PARTICLE and N == 1 and v.sk == z.stride(0):
+                uses.append(("slot", li, oi))
+            elif op.mode == nat.GRAD_DENSE and launcher.N == N and v.sk == z.stride(0) and \
+                    (v.si == z.stride(1) or N == 1):
+                uses.append(("dense", li, oi))
+            else:
+                return None
+    for j, linear in enumerate(linears):
+        theta, sigma = linear.inputs()
+        for which, t in (("lin_theta", theta), ("lin_sigma", sigma)):
+            if t is None:
+                continue
+            if not shares(t):
+                others.append(t)
+                continue
+            if t.data_ptr() != z.data_ptr():
+                return None
+            if which == "lin_theta" and linear.theta_grad and N == linear.P and \
+                    tuple(t.stride()) == tuple(z.stride()):
+                uses.append((which, j, -1))
+            elif which == "lin_sigma" and linear.sigma_grad and N == 1 and \
+                    t.stride(0) == z.stride(0):
+                uses.append((which, j, -1))
+            else:
+                return None
+    for _, logits, _, _ in categorical:
+        if shares(logits):
+            return None
+        others.append(logits)
+    others.extend(fallback)
+    if len(uses) > nat.MAX_SOURCES or _depends_on(others, z.grad_fn):
+        return None
+    return _Absorbed(nat.DRAW_SOURCES, uses, params, drawn=drawn)
+
+
+def plan_absorption(factors: List[EntropyFactor], samples: Optional[Dict[str, torch.Tensor]],
+                    launchers, linears, categorical, fallback) -> Dict[int, _Absorbed]:
+    """
+    Factor index -> absorption plan, for the factors whose draws' backward the ELBO kernels take
+    over (``MININF_AMD_ABSORB=0`` disables it).
+    """
+    if not samples or not torch.is_grad_enabled() or \
+            os.environ.get("MININF_AMD_ABSORB", "1") == "0":
+        return {}
+    out: Dict[int, _Absorbed] = {}
+    for index, factor in enumerate(factors):
+        plan = _absorb_factor(factor, samples, launchers, linears, categorical, fallback)
+        if plan is not None:
+            out[index] = plan
+    return out
 
 
 _ELBO_WORKSPACE: Dict[Tuple[str, int], torch.Tensor] = {}
@@ -787,14 +972,14 @@ _ELBO_WORKSPACE: Dict[Tuple[str, int], torch.Tensor] = {}
 
 def _elbo_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     """
-    Per-device workspace of ``mi_elbo_forward`` (its completion counter must start at zero and is
-    left at zero by every launch, so the buffer is allocated and zeroed once and reused by every
-    step, including captured graphs).
+    Per-device workspace of ``mi_elbo_forward`` / ``mi_elbo_backward`` (its completion counters
+    must start at zero and are left at zero by every launch, so the buffer is allocated and zeroed
+    once and reused by every step, including captured graphs).
     """
     key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
     ws = _ELBO_WORKSPACE.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1 << 14), dtype=torch.uint8, device=device)
+        ws = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
         nat.check(nat.lib().mi_elbo_workspace_init(ws.data_ptr(), ws.numel(),
                                                    nat.stream_handle(device)),
                   "mi_elbo_workspace_init")
@@ -805,12 +990,14 @@ def _elbo_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
 class _ElboPlan:
     """
     Everything one ELBO evaluation launches, in the order of the autograd inputs:
-    site groups (their operand tensors), categorical sites (logits, value, mask), torch-evaluated
-    sites (their [K] log densities) and the entropy factors.
+    site groups (their operand tensors), categorical sites (logits, value, mask), linear sites
+    (theta, sigma), torch-evaluated sites (their [K] log densities) and the entropy factors (their
+    parameter tensor, or -- absorbed -- the unconstrained parameters of both parameters).
     """
     def __init__(self, K: int, g0: float, device: torch.device, launchers, categorical,
                  fallback: List[torch.Tensor], factors: List[EntropyFactor],
-                 entropy_scale: float, linears: Optional[List[_LinearLauncher]] = None) -> None:
+                 entropy_scale: float, linears: Optional[List[_LinearLauncher]] = None,
+                 absorbed: Optional[Dict[int, _Absorbed]] = None) -> None:
         self.K, self.g0, self.device = K, g0, device
         self.launchers = launchers
         self.categorical = categorical
@@ -823,17 +1010,36 @@ class _ElboPlan:
         self.cat_holders = [dict() for _ in categorical]
         self.flags: Optional[torch.Tensor] = None
         self.state = None
+        self.absorbed = absorbed or {}
+        # operands / linear inputs whose gradient an absorbed factor consumes
+        self.skip_ops: Dict[int, set] = collections.defaultdict(set)
+        self.skip_lin: set = set()
+        for plan in self.absorbed.values():
+            for kind, index, operand in plan.uses:
+                if kind in ("draw", "dense", "slot"):
+                    self.skip_ops[index].add(operand)
+                    if kind == "draw":
+                        launchers[index].draw_partials = True
+                else:
+                    self.skip_lin.add((kind, index))
 
     def inputs(self) -> List[Optional[torch.Tensor]]:
         out: List[Optional[torch.Tensor]] = []
-        for launcher in self.launchers:
-            out.extend(launcher.inputs())
+        for li, launcher in enumerate(self.launchers):
+            out.extend(launcher.inputs(self.skip_ops.get(li, ())))
         for _, lg, val, mask in self.categorical:
             out.extend([lg, val, mask])
-        for linear in self.linears:
-            out.extend(linear.inputs())
+        for j, linear in enumerate(self.linears):
+            theta, sigma = linear.inputs()
+            out.append(None if ("lin_theta", j) in self.skip_lin else theta)
+            out.append(None if ("lin_sigma", j) in self.skip_lin else sigma)
         out.extend(self.fallback)
-        out.extend(f.tensor for f in self.factors)
+        for index, f in enumerate(self.factors):
+            plan = self.absorbed.get(index)
+            if plan is None:
+                out.append(f.tensor)
+            else:
+                out.extend(p[0] if p is not None else None for p in plan.params)
         return out
 
     def _describe(self, terms: List[torch.Tensor], buffers: List[torch.Tensor]) -> nat.Elbo:
@@ -861,6 +1067,55 @@ class _ElboPlan:
             E.buffer_len[j] = b.numel()
         return E
 
+    def _describe_absorbed(self, E: nat.Elbo, results, lin_results) -> None:
+        """Fill the absorbed draws' fields of the factor descriptors (after the site launches)."""
+        for index, plan in self.absorbed.items():
+            d = E.factors[index]
+            f = self.factors[index]
+            d.draw_kind = plan.kind
+            for j, p in enumerate(plan.params):
+                if p is not None:
+                    d.transform[j] = p[1]
+            if f.family == nat.NORMAL:
+                loc = f.distribution.loc.reshape(f.n)
+                if f.n > 1 and loc.stride(0) != 1:
+                    loc = loc.contiguous()
+                plan.loc = loc   # kept alive with the plan
+                d.param[0] = loc.data_ptr()
+                d.stride[0] = loc.stride(0) if f.n > 1 else 0
+            if plan.kind == nat.DRAW_PARTIALS:
+                _, li, _ = plan.uses[0]
+                ptr, rows = self.launchers[li].partials
+                d.partial[0], d.partial[1] = ptr, ptr + 4 * rows * f.n
+                d.partial_rows = rows
+                continue
+            cfg = plan.drawn.cfg
+            if f.family == nat.BETA:
+                d.draws = plan.drawn.base.data_ptr()
+            else:
+                d.eps = nat.ptr(cfg.noise)
+                d.seed, d.step = guide._philox_key(cfg)
+                d.step_device = nat.ptr(cfg.step_device)
+                d.stream_id = cfg.stream_id
+                d.particle_offset = cfg.particle_offset
+            d.num_sources = len(plan.uses)
+            for s, (kind, li, oi) in enumerate(plan.uses):
+                src = d.source[s]
+                if kind == "dense":
+                    grad = results[li][0][oi]
+                    src.ptr = grad.data_ptr()
+                    src.stride_k, src.stride_i = grad.stride()
+                elif kind == "slot":
+                    slot_grad = results[li][1]
+                    src.ptr = slot_grad[self.launchers[li].operands[oi].slot].data_ptr()
+                    src.stride_k, src.stride_i = 1, 0
+                elif kind == "lin_theta":
+                    src.ptr = lin_results[li].data_ptr()
+                    src.stride_k, src.stride_i = 1, self.K
+                else:   # lin_sigma
+                    src.ptr = lin_results[li][self.linears[li].P].data_ptr()
+                    src.stride_k, src.stride_i = 1, 0
+
     def forward(self) -> torch.Tensor:
         terms: List[torch.Tensor] = []
         buffers: List[torch.Tensor] = []
@@ -870,22 +1125,33 @@ class _ElboPlan:
             [len(l.sites) for l in self.launchers]
         self.flags = torch.zeros(max(1, sum(sizes)), dtype=torch.int32, device=self.device)
         cursor = len(self.categorical) + len(self.linears)
-        for launcher, holder in zip(self.launchers, self.holders):
+        for li, (launcher, holder) in enumerate(zip(self.launchers, self.holders)):
             need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
             part = self.flags[cursor:cursor + len(launcher.sites)]
             cursor += len(launcher.sites)
             total, site_lp, grads, slot_grad, flags = launcher.run(need, part)
             holder["flags"], holder["site_lp"] = flags, site_lp
             terms.append(total)
+            skip = self.skip_ops.get(li, set())
             if need:
-                for g in grads:
+                # speculative buffers the backward rescales when the upstream is not 1 (those an
+                # absorbed factor consumes are scaled inside its own reduction instead)
+                for oi, g in enumerate(grads):
+                    if oi in skip:
+                        continue
                     if isinstance(g, tuple):
                         buffers.extend(g)
                     elif g is not None:
                         buffers.append(g)
                 if launcher.num_slots:
-                    buffers.append(slot_grad[:launcher.num_slots])
-            results.append((grads, slot_grad))
+                    absorbed_slots = {launcher.operands[oi].slot for oi in skip
+                                      if launcher.operands[oi].mode == nat.GRAD_PARTICLE}
+                    if absorbed_slots:
+                        buffers.extend(slot_grad[j:j + 1] for j in range(launcher.num_slots)
+                                       if j not in absorbed_slots)
+                    else:
+                        buffers.append(slot_grad[:launcher.num_slots])
+            results.append((grads, slot_grad, launcher.workspace))
         cat_results = []
         for j, ((site, lg, val, mask), holder) in enumerate(zip(self.categorical,
                                                                  self.cat_holders)):
@@ -904,7 +1170,15 @@ class _ElboPlan:
             holder["flags"] = flags
             terms.append(total)
             if dslots is not None:
-                buffers.append(dslots)
+                theta_out = ("lin_theta", j) in self.skip_lin
+                sigma_out = ("lin_sigma", j) in self.skip_lin
+                if not theta_out and not sigma_out:
+                    buffers.append(dslots)
+                else:
+                    if not theta_out:
+                        buffers.append(dslots[:linear.P])
+                    if not sigma_out and dslots.shape[0] > linear.P:
+                        buffers.append(dslots[linear.P:])
             lin_results.append(dslots)
         terms.extend(t.contiguous() for t in self.fallback)
         if len(terms) > nat.MAX_TERMS:
@@ -913,6 +1187,7 @@ class _ElboPlan:
         extra = buffers[nat.MAX_BUFFERS:]
         buffers = buffers[:nat.MAX_BUFFERS]
         E = self._describe(terms, buffers)
+        self._describe_absorbed(E, results, lin_results)
         size = ctypes.c_size_t()
         lib = nat.lib()
         nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
@@ -932,25 +1207,50 @@ class _ElboPlan:
         device = self.device
         u = u.to(torch.float32).contiguous()
         dterm = torch.empty(1, dtype=torch.float32, device=device)
-        fgrads = []
+        fgrads: List[List[Optional[torch.Tensor]]] = []
         for j, f in enumerate(self.factors):
+            d = E.factors[j]
+            plan = self.absorbed.get(j)
+            if plan is not None:
+                out_j: List[Optional[torch.Tensor]] = []
+                for q, p in enumerate(plan.params):
+                    if p is None:
+                        d.grad[q] = None
+                        out_j.append(None)
+                        continue
+                    grad = torch.empty(p[0].shape, dtype=torch.float32, device=device)
+                    d.grad[q] = grad.data_ptr()
+                    d.grad_stride[q] = 1
+                    out_j.append(grad)
+                fgrads.append(out_j)
+                continue
             grad = torch.empty_like(f.tensor)
             base = grad.data_ptr()
-            d = E.factors[j]
             if f.family == nat.BETA:
                 d.grad[0], d.grad[1] = base, base + 4
+                d.grad_stride[0] = d.grad_stride[1] = 2
             else:
                 d.grad[1] = base
-            fgrads.append(grad)
-        nat.check(nat.lib().mi_elbo_backward(ctypes.byref(E), u.data_ptr(), dterm.data_ptr(),
-                                             nat.stream_handle(device)), "mi_elbo_backward")
+                d.grad_stride[1] = grad.stride(0) if f.n > 1 else 1
+            fgrads.append([grad])
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
+                  "mi_elbo_workspace_bytes")
+        ws = _elbo_workspace(device, size.value)
+        nat.check(lib.mi_elbo_backward(ctypes.byref(E), u.data_ptr(), dterm.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), nat.stream_handle(device)),
+                  "mi_elbo_backward")
         for buffer in extra:
             buffer.mul_(u)
         out: List[Optional[torch.Tensor]] = []
-        for launcher, (grads, slot_grad) in zip(self.launchers, results):
-            for op, grad in zip(launcher.operands, grads):
+        for li, (launcher, (grads, slot_grad, _)) in enumerate(zip(self.launchers, results)):
+            skip = self.skip_ops.get(li, ())
+            for oi, (op, grad) in enumerate(zip(launcher.operands, grads)):
                 if op.view.draw is not None:
-                    out.extend(grad if grad is not None else (None, None))
+                    out.extend((None, None) if oi in skip or grad is None else grad)
+                elif oi in skip:
+                    out.append(None)
                 elif op.mode == nat.GRAD_DENSE:
                     out.append(grad)
                 elif op.mode == nat.GRAD_PARTICLE:
@@ -959,10 +1259,13 @@ class _ElboPlan:
                     out.append(None)
         for dlogits in cat_results:
             out.extend([dlogits, None, None])
-        for linear, dslots in zip(self.linears, lin_results):
-            out.extend(linear.grads(dslots))
+        for j, (linear, dslots) in enumerate(zip(self.linears, lin_results)):
+            dtheta, dsigma = linear.grads(dslots)
+            out.append(None if ("lin_theta", j) in self.skip_lin else dtheta)
+            out.append(None if ("lin_sigma", j) in self.skip_lin else dsigma)
         out.extend(dterm.expand(self.K) for _ in self.fallback)
-        out.extend(fgrads)
+        for grads_j in fgrads:
+            out.extend(grads_j)
         return out
 
 
@@ -1016,7 +1319,7 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
     from . import guide
     fused: List[EntropyFactor] = []
     rest = []
-    for factor in approximation.values():
+    for name, factor in approximation.items():
         cls = type(factor)
         n = max(1, int(factor.batch_shape.numel()))
         if len(fused) < nat.MAX_FACTORS and cls is Normal and factor.scale.dtype == torch.float32 \
@@ -1024,11 +1327,11 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
             scale = factor.scale.reshape(n)
             if n > 1 and scale.stride(0) != 1:
                 scale = scale.contiguous()
-            fused.append(EntropyFactor(nat.NORMAL, n, scale))
+            fused.append(EntropyFactor(nat.NORMAL, n, scale, name, factor))
         elif len(fused) < nat.MAX_FACTORS and cls is Beta:
             conc = guide.beta_concentration(factor, n)
             if conc.is_cuda:
-                fused.append(EntropyFactor(nat.BETA, n, conc))
+                fused.append(EntropyFactor(nat.BETA, n, conc, name, factor))
             else:
                 rest.append(factor)
         else:
@@ -1037,7 +1340,8 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
 
 
 def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[EntropyFactor],
-         entropy_scale: float) -> Tuple[torch.Tensor, LogJoint]:
+         entropy_scale: float, samples: Optional[Dict[str, torch.Tensor]] = None
+         ) -> Tuple[torch.Tensor, LogJoint]:
     """
     ``g0 * sum_k log p(x, z_k) - entropy_scale * H[factors]`` as one autograd node: the site
     kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
@@ -1053,8 +1357,10 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         if not bad:
             break
         _materialize_draws(trace, bad)
-    plan = _ElboPlan(trace.K, g0, device, launchers, categorical,
-                     [value for _, value in trace.fallback], factors, entropy_scale, linears)
+    fallback = [value for _, value in trace.fallback]
+    absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
+    plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
+                     entropy_scale, linears, absorbed)
     loss = _ElboFn.apply(plan, *plan.inputs())
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):

@@ -172,16 +172,50 @@ class LazyDraw:
         if self.real is None:
             z = _NormalRsampleFn.apply(self.cfg, self.loc, self.loc_s, self.scale, self.scale_s)
             self.real = z.reshape((self.cfg.K,) + tuple(self.shape))
+            _DRAWN[self.real.data_ptr()] = Drawn(NORMAL_FAMILY, self.cfg, z, self.N)
         return self.real
 
 
 # data pointer of a live placeholder -> its draw (reset by every lazy draw_all)
 _LAZY: Dict[int, LazyDraw] = {}
 
+NORMAL_FAMILY, BETA_FAMILY = "normal", "beta"
+
+
+@dataclasses.dataclass(eq=False)
+class Drawn:
+    """
+    A materialised guide draw of the last draw_all: ``base`` is the [K, N] output of the sampler's
+    autograd node (Normal: :class:`_NormalRsampleFn`, Beta: :class:`_BetaRsampleFn`), from which
+    the ELBO can take over the draw's backward (``mi_factor`` absorbed draws).
+    """
+    family: str
+    cfg: DrawConfig
+    base: torch.Tensor
+    N: int
+
+
+# data pointer of a materialised draw -> its record (reset by every draw_all)
+_DRAWN: Dict[int, Drawn] = {}
+
 
 def release_lazy() -> None:
-    """Forget the placeholders of the last lazy draw_all (the loss has planned its kernels)."""
+    """
+    Forget the placeholders and draw records of the last draw_all (the loss has planned its
+    kernels; holding them would keep the step's autograd graph alive).
+    """
     _LAZY.clear()
+    _DRAWN.clear()
+
+
+def drawn_of(tensor) -> Optional[Drawn]:
+    """The materialised draw a sample tensor (or a view sharing its storage start) is, or None."""
+    if not _DRAWN or not isinstance(tensor, torch.Tensor):
+        return None
+    try:
+        return _DRAWN.get(tensor.data_ptr())
+    except RuntimeError:
+        return None
 
 
 def lazy_of(tensor) -> Optional[LazyDraw]:
@@ -228,6 +262,7 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
                                                 torch.Size(shape), placeholder)
             return placeholder
         z = _NormalRsampleFn.apply(cfg, loc, loc_s, scale, scale_s)
+        _DRAWN[z.data_ptr()] = Drawn(NORMAL_FAMILY, cfg, z, N)
         return z.reshape((cfg.K,) + tuple(shape))
     if cls is Beta:
         shape = distribution.batch_shape
@@ -238,6 +273,7 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
             cfg.noise = cfg.noise.to(device=conc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
         x = _BetaRsampleFn.apply(cfg, conc)
+        _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N)
         return x.reshape((cfg.K,) + tuple(shape))
     if cfg.noise is not None:
         return cfg.noise
@@ -253,6 +289,7 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
     Normal factors become :class:`LazyDraw` placeholders evaluated inside the site kernels.
     """
     _LAZY.clear()
+    _DRAWN.clear()
     samples = {}
     for stream_id, (name, factor) in enumerate(approximation.items()):
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,

@@ -95,14 +95,24 @@ class ParameterizedDistribution(nn.Module):
         """"""
         constraints = cast(Dict, self.distribution_cls.arg_constraints)
         arguments = {}
+        sources = {}
         for name, unconstrained in self.distribution_parameters.items():
             transform = distributions.transform_to(constraints[name])
             # The reference exposes `1 * value` so the distribution never holds the nn.Parameter
             # itself (nn.py:92-94); a view is likewise a distinct tensor and costs no kernel.
-            arguments[name] = unconstrained.view_as(unconstrained) \
-                if _is_identity_transform(transform) \
-                else _forward_transform(transform)(unconstrained)
-        return self.distribution_cls(**arguments, **self.distribution_constants)  # type: ignore
+            if _is_identity_transform(transform):
+                arguments[name] = unconstrained.view_as(unconstrained)
+                sources[name] = (unconstrained, "identity")
+            else:
+                forward = _forward_transform(transform)
+                arguments[name] = forward(unconstrained)
+                if isinstance(forward, distributions.ExpTransform):
+                    sources[name] = (unconstrained, "exp")
+        distribution = self.distribution_cls(**arguments, **self.distribution_constants)
+        # How each parameter derives from this module's nn.Parameters: the fused ELBO can then
+        # write the guide's gradients directly (mi_factor transforms, engine.elbo).
+        distribution._mininf_amd_sources = sources  # type: ignore[attr-defined]
+        return distribution  # type: ignore
 
 
 class FactorizedDistribution(DistributionDict):
@@ -238,7 +248,7 @@ class EvidenceLowerBoundLoss(nn.Module):
             # Fused path: site kernels, guide entropy and the reduction in one autograd node.
             factors, rest = engine.entropy_factors(approximation)
             try:
-                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world)
+                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples)
             finally:
                 # The placeholder registry is only needed while tracing and planning; holding it
                 # would keep this step's autograd graph (and its AccumulateGrad streams) alive.

@@ -480,3 +480,92 @@ def test_fused_guide_draw_matches_materialised(device, n, use_exp, monkeypatch):
     assert abs(fused[0] - plain[0]) <= 1e-5 * abs(plain[0])
     for name in plain[1]:
         torch.testing.assert_close(fused[1][name], plain[1][name], rtol=1e-4, atol=1e-5)
+
+
+def _absorb_cases(device, case):
+    """Models whose guide draws the ELBO backward can absorb (or must not)."""
+    rng = np.random.default_rng(12)
+    if case == "beta_scalar":   # C2-shaped: one Beta factor, many particles (cross-slice sums)
+        x = torch.as_tensor((rng.random(5000) < 0.7).astype(np.float32), device=device)
+
+        def model():
+            theta = mi.sample("theta", Beta(2.0, 2.0))
+            mi.sample("x", Bernoulli(theta), sample_shape=[5000])
+        approx = mi.nn.ParameterizedFactorizedDistribution(
+            theta=mi.nn.ParameterizedDistribution(Beta, concentration1=1.7, concentration0=2.6))
+        return mi.condition(model, x=x), approx.to(device), 2048
+    if case == "two_factor":
+        cond, approx, _, K = _two_factor_case(device, n=700, K=16)
+        return cond, approx, K
+    if case in ("linear", "linear_sigma"):
+        n, p = 4000, 6
+        X = torch.as_tensor(rng.normal(size=(n, p)).astype(np.float32), device=device)
+        y = torch.as_tensor(rng.normal(size=n).astype(np.float32), device=device)
+
+        def model():
+            theta = mi.sample("theta", Normal(0.0, 1.0), sample_shape=p)
+            sigma = mi.sample("sigma", Normal(1.0, 0.1)) if case == "linear_sigma" else 0.8
+            mi.sample("y", Normal(X @ theta, sigma))
+        guide = {"theta": mi.nn.ParameterizedDistribution(Normal, loc=torch.full((p,), 0.1),
+                                                          scale=torch.full((p,), 0.5))}
+        if case == "linear_sigma":
+            guide["sigma"] = mi.nn.ParameterizedDistribution(Normal, loc=1.0, scale=0.05)
+        return mi.condition(model, y=y), mi.nn.ParameterizedFactorizedDistribution(guide) \
+            .to(device), 64
+    if case == "hierarchical":    # fused draw (partials) + a scalar factor used as a loc (slot)
+        cond, approx = _hierarchical(device, 4096)
+        return cond, approx, 48
+    cond, approx = _hierarchical(device, 2048, use_exp=True)   # z.exp(): must not be absorbed
+    return cond, approx, 16
+
+
+@pytest.mark.parametrize("case", ["beta_scalar", "two_factor", "linear", "linear_sigma",
+                                  "hierarchical", "exp_use"])
+def test_absorbed_draws_match_autograd(device, case, monkeypatch):
+    """
+    Guide draws whose backward the ELBO kernel absorbs (mi_factor draw_kind: Beta implicit
+    gradient, Normal eps regeneration, fused-draw partials; entropy and exp transform folded in)
+    against the same step with the draws' backward left to autograd (MININF_AMD_ABSORB=0).
+    """
+    cond, approx, K = _absorb_cases(device, case)
+
+    def run(scale=1.0):
+        for q in approx.parameters():
+            q.grad = None
+        loss = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=3)(cond, approx())
+        (scale * loss).backward()
+        return float(loss), {k: q.grad.detach().clone() for k, q in approx.named_parameters()}
+
+    absorbed = run()
+    scaled = run(-1.5)
+    monkeypatch.setenv("MININF_AMD_ABSORB", "0")
+    plain = run()
+    assert abs(absorbed[0] - plain[0]) <= 1e-5 * abs(plain[0])
+    for name in plain[1]:
+        torch.testing.assert_close(absorbed[1][name], plain[1][name], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(scaled[1][name], -1.5 * plain[1][name], rtol=1e-4, atol=1e-5)
+
+
+def test_absorption_plan(device):
+    """Which factors the ELBO absorbs: all of the hierarchical model's, none when z is used
+    outside the site kernels."""
+    from mininf_amd import engine
+    seen = []
+    original = engine.plan_absorption
+
+    def spy(*args, **kwargs):
+        out = original(*args, **kwargs)
+        seen.append(sorted((args[0][i].name, p.kind) for i, p in out.items()))
+        return out
+    engine.plan_absorption = spy
+    try:
+        for case in ("hierarchical", "exp_use", "beta_scalar", "linear"):
+            cond, approx, K = _absorb_cases(device, case)
+            mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=3)(cond, approx()).backward()
+    finally:
+        engine.plan_absorption = original
+    import mininf_amd._native as nat
+    assert seen[0] == [("mu", nat.DRAW_SOURCES), ("z", nat.DRAW_PARTIALS)]
+    assert ("z", nat.DRAW_SOURCES) not in seen[1] and ("z", nat.DRAW_PARTIALS) not in seen[1]
+    assert seen[2] == [("theta", nat.DRAW_SOURCES)]
+    assert seen[3] == [("theta", nat.DRAW_SOURCES)]
