@@ -257,13 +257,16 @@ int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t ke
  * family: MI_NORMAL (sigma = scale[k * scale_stride_k], or scale_constant when scale == NULL) or
  * MI_BERNOULLI_LOGITS (scale unused). P <= MI_LINEAR_MAX_P. */
 #define MI_LINEAR_MAX_P 64
+/* options bit: run the VALU kernel even where the matrix-core (v_mfma_f32_32x32x2_f32) kernel
+ * applies (contiguous 16-byte aligned rows of X, P % 4 == 0); for cross-checks. */
+#define MI_LINEAR_VALU 2
 
 typedef struct mi_linear {
   int64_t K;
   int64_t N;
   int64_t P;
   int32_t family;
-  int32_t options;        /* MI_GROUP_FLAGS_ZEROED */
+  int32_t options;        /* MI_GROUP_FLAGS_ZEROED | MI_LINEAR_VALU */
   const float* x;         /* X[i, j] at x[i * x_stride_i + j * x_stride_j] */
   int64_t x_stride_i;
   int64_t x_stride_j;

@@ -25,6 +25,7 @@ MAX_TERMS = 8
 MAX_FACTORS = 8
 MAX_BUFFERS = 16
 LINEAR_MAX_P = 64
+LINEAR_VALU = 2
 
 NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2

@@ -17,6 +17,7 @@
 #include "internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mi {
 
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(kLinThreads) void k_linear(const mi_linear L, int k
         const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
         fl |= (m != 0.0f && bad) ? MI_FLAG_SUPPORT : 0u;
       }
-      ys[r] = y;
+      ys[r] = m != 0.0f ? y : 0.0f;   // masked-out values (NaN in missing data) are never used
       ms[r] = m;
     }
     __syncthreads();
@@ -164,6 +165,268 @@ __global__ __launch_bounds__(kLinThreads) void k_linear(const mi_linear L, int k
   publish_flags(flags, fl);
 }
 
+// ---- matrix-core formulation -------------------------------------------------------------------
+// The site is two contractions around an elementwise step, per 32-row tile of X and 32 particles:
+//   MU[i, k]     = sum_p X[i, p] theta[k, p]                 (v_mfma_f32_32x32x2_f32, A = X, B = theta^T)
+//   R[i, k]      = mask_i * dlogp/dloc(y_i, MU[i, k])        (VALU, in the accumulator registers)
+//   DTH[k, p]   += sum_i R[i, k] X[i, p]                     (v_mfma_f32_32x32x2_f32, A = R^T, B = X)
+// The 32x32 accumulator of the first product holds particle k = lane & 31 and row
+// (r & 3) + 8 (r >> 2) + 4 (lane >> 5) in register r, which is exactly the A operand of the second
+// product's k-step r (A[m = lane & 31][kd = lane >> 5]), so R never leaves the registers; its B
+// operand is the matching X row, read from LDS. f32-in MFMA is an exact fmaf chain, so the numerics
+// are those of the VALU kernel's dot products, at the matrix-core rate (MI355X_MICROARCH.md: 157 TF).
+//
+// Block: 8 waves = WT particle tiles of 32 x RS row subsets (WT * RS = 8). X is staged through one
+// LDS buffer in stages of CH rows (prefetched into registers during the previous stage's MFMAs) as
+// [row][feature parity][feature / 2], so the first product's A fragment (lane: row lane & 31,
+// features 2s + (lane >> 5)) is a contiguous 16-byte-read run. Partials: one tile per (block, row
+// subset), reduced in fp64 by k_finalize as for the VALU kernel.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int PT, int NT>
+struct MfShape {
+  static constexpr int NW = NT / kWave;    // waves per block
+  static constexpr int PM = 32 * PT;       // padded features
+  static constexpr int HS = 16 * PT;       // floats per feature-parity half of an LDS row
+  static constexpr int RSTR = PM + 4;      // LDS row stride (floats): 16-byte aligned, skewed banks
+  static constexpr int CH = (NT >= 512 ? 256 : 128) / PT;   // rows per stage
+  static constexpr int TILES = CH / 32;    // 32-row tiles per stage
+  static constexpr int QPT = CH * PM / 4 / NT;   // float4 loads per thread per stage
+};
+
+// Grid: one dimension of gx * gy blocks, gx (row blocks) a multiple of 8. Blocks are dealt to the
+// 8 XCDs round-robin, so block b's row block is chosen such that the gy particle groups of one row
+// block run on one XCD (b, b + 8, ...) and share its L2 copy of the X rows.
+template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW, bool GRADS>
+__global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int wt, int gy,
+                                                          int64_t stages_per_block,
+                                                          int64_t ntile,
+                                                          float* __restrict__ part,
+                                                          uint32_t* __restrict__ flags) {
+  using S = MfShape<PT, NT>;
+  constexpr int kMfThreads = NT;
+  constexpr int kMfWaves = S::NW;
+  const int64_t bid = blockIdx.x;
+  const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
+  const int64_t group = (bid / 8) % gy;
+  __shared__ __attribute__((aligned(16))) float xs[S::CH * S::RSTR];
+  __shared__ float2 yms[S::CH];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
+  const int h = lane >> 5, c = lane & 31;
+  const int rs_count = kMfWaves / wt;
+  const int pt = wave % wt, rs = wave / wt;
+  const int64_t K = L.K, N = L.N;
+  const int P = (int)L.P;
+  const int64_t k0 = (group * wt + pt) * 32;
+  constexpr bool grads = GRADS;
+  const bool per_particle_sigma = FAMILY == MI_NORMAL && L.scale != nullptr;
+  uint32_t fl = 0u;
+
+  // B fragment of the first product: theta[k0 + c][2 s + h]
+  float thf[S::HS];
+  {
+    const int64_t kk = k0 + c;
+#pragma unroll
+    for (int s = 0; s < S::HS; ++s) {
+      const int p = 2 * s + h;
+      thf[s] = (kk < K && p < P) ? L.theta[kk * L.theta_stride_k + p * L.theta_stride_j] : 0.0f;
+    }
+  }
+
+  // dtheta: fp32 MFMA accumulators per stage, carried in fp64 across stages (PT = 1); with two
+  // feature tiles the fp64 copy would not fit the 256 registers of a 2-wave/SIMD launch, so the
+  // accumulators run in fp32 over the block's rows, as in the VALU kernel.
+  constexpr bool kFlush64 = FLUSH64;
+  double dth[kFlush64 ? PT : 1][kFlush64 ? 16 : 1];
+#pragma unroll
+  for (int t = 0; t < (kFlush64 ? PT : 1); ++t)
+#pragma unroll
+    for (int r = 0; r < (kFlush64 ? 16 : 1); ++r) dth[t][r] = 0.0;
+  f32x16 acc2[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) acc2[t] = f32x16{};
+  double lpd = 0.0;      // Normal: sum of mask * (y - loc)^2; Bernoulli: sum of mask * log p
+  float cnt = 0.0f;      // observed rows seen by this lane (Normal)
+
+  const int64_t nstage = (N + S::CH - 1) / S::CH;
+  const int64_t st0 = row_block * stages_per_block;
+  const int64_t st1 = min(nstage, st0 + stages_per_block);
+
+  // ---- staging: X quads and (y, mask) of one stage into registers, then into LDS ---------------
+  float4 xq[S::QPT];
+  float2 ymr = make_float2(0.0f, 0.0f);
+  auto load_stage = [&](int64_t st) {
+    const int64_t row0 = st * S::CH;
+#pragma unroll
+    for (int q = 0; q < S::QPT; ++q) {
+      const int e = tid + q * kMfThreads;
+      const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
+      const int64_t i = row0 + row;
+      xq[q] = (i < N && 4 * c4 < P)
+                  ? *reinterpret_cast<const float4*>(L.x + i * L.x_stride_i + 4 * c4)
+                  : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    if (tid < S::CH) {
+      const int64_t i = row0 + tid;
+      float y = 0.0f, m = 0.0f;
+      if (i < N) {
+        y = L.value[i * L.value_stride_i];
+        m = (L.mask == nullptr || L.mask[i * L.mask_stride_i] != 0) ? 1.0f : 0.0f;
+        const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
+        fl |= (m != 0.0f && bad) ? MI_FLAG_SUPPORT : 0u;
+      }
+      ymr = make_float2(m != 0.0f ? y : 0.0f, m);
+    }
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < S::QPT; ++q) {
+      const int e = tid + q * kMfThreads;
+      const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
+      float* dst = xs + row * S::RSTR + 2 * c4;
+      *reinterpret_cast<float2*>(dst) = make_float2(xq[q].x, xq[q].z);           // even features
+      *reinterpret_cast<float2*>(dst + S::HS) = make_float2(xq[q].y, xq[q].w);   // odd features
+    }
+    if (tid < S::CH) yms[tid] = ymr;
+  };
+
+  // MU = X theta^T for the tile's 32 rows and this wave's 32 particles
+  auto gemm1 = [&](int tile) -> f32x16 {
+    f32x16 mu = f32x16{};
+    const float* xa = xs + (tile * 32 + c) * S::RSTR + h * S::HS;
+#pragma unroll
+    for (int s = 0; s < S::HS; s += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(xa + s);
+      mu = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, thf[s + 0], mu, 0, 0, 0);
+      mu = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, thf[s + 1], mu, 0, 0, 0);
+      mu = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, thf[s + 2], mu, 0, 0, 0);
+      mu = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, thf[s + 3], mu, 0, 0, 0);
+    }
+    return mu;
+  };
+  // log density and mask * d/dloc in place (Normal: d = y - loc, the 1/sigma^2 factor is applied
+  // per particle at the end)
+  auto elementwise = [&](f32x16& mu, int tile) {
+    float lpt = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float2 ym = yms[row];
+      const float loc = mu[r];
+      fl |= (loc != loc) ? MI_FLAG_PARAM : 0u;
+      if (FAMILY == MI_NORMAL) {
+        const float d = ym.y * (ym.x - loc);
+        lpt = fmaf(d, d, lpt);
+        cnt += ym.y;
+        mu[r] = d;
+      } else {
+        Elem el;
+        eval_bernoulli_logits(loc, ym.x, el);
+        lpt = fmaf(ym.y, el.lp, lpt);
+        mu[r] = ym.y * el.d[0];
+      }
+    }
+    lpd += (double)lpt;
+  };
+  // DTH[k, p] += sum_rows R[row, k] X[row, p]: k-step r pairs register r with its row
+  auto gemm2 = [&](const f32x16& R, int tile) {
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int p = 32 * t + c;
+      const float* xb = xs + (p & 1) * S::HS + (p >> 1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(R[r], xb[row * S::RSTR], acc2[t], 0, 0, 0);
+      }
+    }
+  };
+
+  if (st0 < st1) {
+    load_stage(st0);
+    store_stage();
+  }
+  __syncthreads();
+  for (int64_t st = st0; st < st1; ++st) {
+    if (st + 1 < st1) load_stage(st + 1);   // in flight during this stage's MFMAs
+    // Software pipeline over this wave's tiles: the first product of tile j + 1 is issued before
+    // the elementwise step of tile j, so its MFMAs run while the VALU evaluates the densities.
+    const int ntl = (S::TILES - rs + rs_count - 1) / rs_count;
+    if (ntl > 0) {
+      f32x16 cur = gemm1(rs);
+      for (int j = 0; j + 1 < ntl; ++j) {
+        const int tile = rs + j * rs_count;
+        const f32x16 nxt = gemm1(tile + rs_count);
+        elementwise(cur, tile);
+        if (GRADS) gemm2(cur, tile);
+        cur = nxt;
+      }
+      const int last = rs + (ntl - 1) * rs_count;
+      elementwise(cur, last);
+      if (GRADS) gemm2(cur, last);
+    }
+    if (kFlush64) {
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dth[kFlush64 ? t : 0][kFlush64 ? r : 0] += (double)acc2[t][r];
+        acc2[t] = f32x16{};
+      }
+    }
+    __syncthreads();
+    if (st + 1 < st1) {
+      store_stage();
+      __syncthreads();
+    }
+  }
+
+  // ---- partials of tile (block, row subset) ---------------------------------------------------
+  const int64_t tile_id = row_block * rs_count + rs;
+  const float wscale = (float)L.site_scale;
+  lpd += __shfl_xor(lpd, 32, kWave);
+  cnt += __shfl_xor(cnt, 32, kWave);
+  if (h == 0) {
+    const int64_t kk = k0 + c;
+    if (kk < K) {
+      if (FAMILY == MI_NORMAL) {
+        // -(y - loc)^2 / (2 sigma^2) - log(sigma) - log(sqrt(2 pi))   (normal.py:88-103)
+        const float sigma = per_particle_sigma ? L.scale[kk * L.scale_stride_k] : L.scale_constant;
+        fl |= !(sigma > 0.0f) ? MI_FLAG_PARAM : 0u;
+        const double inv2 = 1.0 / ((double)sigma * (double)sigma);
+        const double cst = -(double)logf(sigma) - (double)kHalfLog2Pi;
+        part[tile_id * K + kk] = (float)(-0.5 * lpd * inv2 + (double)cnt * cst);
+        if (per_particle_sigma && grads)
+          part[((int64_t)(1 + P) * ntile + tile_id) * K + kk] =
+              (float)((double)wscale * (lpd * inv2 - (double)cnt) / (double)sigma);
+      } else {
+        part[tile_id * K + kk] = (float)lpd;
+      }
+    }
+  }
+  if (grads) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t kk = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (kk >= K) continue;
+      double w = (double)wscale;
+      if (FAMILY == MI_NORMAL) {
+        const double sigma =
+            per_particle_sigma ? (double)L.scale[kk * L.scale_stride_k] : (double)L.scale_constant;
+        w /= sigma * sigma;
+      }
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int p = 32 * t + c;
+        const double v = kFlush64 ? dth[kFlush64 ? t : 0][kFlush64 ? r : 0] : (double)acc2[t][r];
+        if (p < P) part[((int64_t)(1 + p) * ntile + tile_id) * K + kk] = (float)(v * w);
+      }
+    }
+  }
+  publish_flags(flags, fl);
+}
+
 }  // namespace mi
 
 namespace {
@@ -177,13 +440,66 @@ bool valid(const mi_linear* L) {
 }
 
 struct Geometry {
-  int kb;
-  int64_t gy, rows_per_tile, ntile;
+  bool mfma;
+  int kb;              // VALU kernel: particles per block
+  int wt;              // MFMA kernel: 32-particle tiles per block
+  int pt;              // MFMA kernel: 32-feature tiles (1 or 2)
+  int variant;         // MFMA kernel: launch variant (kMfVariants)
+  int64_t gx, gy, rows_per_tile, stages_per_block, ntile;
   int nv;
 };
 
+// The matrix-core kernel takes contiguous, 16-byte aligned rows of X (row stride a multiple of 4
+// floats) with P % 4 == 0; anything else, or MI_LINEAR_VALU, runs the VALU kernel.
+bool use_mfma(const mi_linear* L) {
+  return !(L->options & MI_LINEAR_VALU) && L->P % 4 == 0 && L->x_stride_j == 1 &&
+         L->x_stride_i >= L->P && L->x_stride_i % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(L->x) & 15) == 0;
+}
+
+// Matrix-core launch variants: block size, fp64 carry of the dtheta accumulators across stages,
+// minimum waves per SIMD (register budget). MININF_AMD_LINEAR_TUNE selects one (tuning only).
+struct MfVariant {
+  int threads;
+  bool flush64;
+  int minw;
+};
+constexpr MfVariant kMfVariants[] = {{512, true, 1}, {512, false, 1}, {256, false, 1},
+                                     {256, false, 4}};
+
+int mf_variant() {
+  static const int v = [] {
+    const char* e = getenv("MININF_AMD_LINEAR_TUNE");
+    const int n = e != nullptr ? atoi(e) : 0;
+    return (n >= 0 && n < (int)(sizeof(kMfVariants) / sizeof(kMfVariants[0]))) ? n : 0;
+  }();
+  return v;
+}
+
 Geometry geometry(const mi_linear* L) {
   Geometry g{};
+  g.nv = 1 + (int)L->P + ((L->family == MI_NORMAL && L->scale != nullptr) ? 1 : 0);
+  g.mfma = use_mfma(L);
+  if (g.mfma) {
+    const MfVariant v = kMfVariants[mf_variant()];
+    const int waves = v.threads / 64;
+    g.variant = mf_variant();
+    g.pt = L->P <= 32 ? 1 : 2;
+    const int64_t ptiles = ceil_div(L->K, 32);
+    int wt = 1;
+    while (wt < waves && wt < ptiles) wt <<= 1;
+    g.wt = wt;
+    g.gy = ceil_div(ptiles, wt);
+    const int64_t ch = (v.threads >= 512 ? 256 : 128) / g.pt;
+    const int64_t nstage = ceil_div(L->N, ch);
+    // about 512 (512-thread) or 1024 (256-thread) blocks over the grid, whole stages per block;
+    // row blocks padded to a multiple of 8 (see k_linear_mfma)
+    const int64_t target = std::max<int64_t>(1, (v.threads >= 512 ? 512 : 1024) / g.gy);
+    g.stages_per_block = ceil_div(nstage, target);
+    g.gx = ceil_div(ceil_div(nstage, g.stages_per_block), 8) * 8;
+    g.ntile = g.gx * (waves / wt);
+    return g;
+  }
   int kb = 1;
   while (kb < 256 && kb < L->K) kb <<= 1;
   g.kb = kb;
@@ -192,7 +508,7 @@ Geometry geometry(const mi_linear* L) {
   const int64_t tiles = std::max<int64_t>(1, 768 / g.gy);
   g.rows_per_tile = std::max<int64_t>(mi::kLinChunk, ceil_div(ceil_div(L->N, tiles), mi::kLinChunk) * mi::kLinChunk);
   g.ntile = ceil_div(L->N, g.rows_per_tile);
-  g.nv = 1 + (int)L->P + ((L->family == MI_NORMAL && L->scale != nullptr) ? 1 : 0);
+  g.gx = g.ntile;
   return g;
 }
 
@@ -203,9 +519,39 @@ size_t partial_bytes(const mi_linear* site, const Geometry& g) {
   return ((size_t)g.nv * (size_t)g.ntile * (size_t)site->K * sizeof(float) + 255) / 256 * 256;
 }
 
+template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW>
+void launch_mfma(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
+                 hipStream_t s) {
+  const dim3 grid((unsigned)(g.gx * g.gy));
+  if (L.compute_grads)
+    hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, true>), grid, dim3(NT),
+                       0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags);
+  else
+    hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, false>), grid, dim3(NT),
+                       0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags);
+}
+
+template <int FAMILY, int PT>
+void launch_mfma_variant(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
+                         hipStream_t s) {
+  switch (g.variant) {
+    case 1: launch_mfma<FAMILY, PT, 512, false, 1>(L, g, part, flags, s); break;
+    case 2: launch_mfma<FAMILY, PT, 256, false, 1>(L, g, part, flags, s); break;
+    case 3: launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s); break;
+    default: launch_mfma<FAMILY, PT, 512, PT == 1, 1>(L, g, part, flags, s); break;
+  }
+}
+
 template <int FAMILY>
 void launch(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags, hipStream_t s) {
-  const dim3 grid((unsigned)g.ntile, (unsigned)g.gy);
+  const dim3 grid((unsigned)g.gx, (unsigned)g.gy);
+  if (g.mfma) {
+    if (g.pt == 1)
+      launch_mfma_variant<FAMILY, 1>(L, g, part, flags, s);
+    else
+      launch_mfma_variant<FAMILY, 2>(L, g, part, flags, s);
+    return;
+  }
   if (L.P <= 8)
     hipLaunchKernelGGL((mi::k_linear<FAMILY, 8>), grid, dim3(mi::kLinThreads), 0, s, L, g.kb,
                        g.rows_per_tile, g.ntile, part, flags);

@@ -151,7 +151,7 @@ class _BetaRsampleFn(torch.autograd.Function):
 
 @dataclasses.dataclass(eq=False)   # identity semantics: used in sets
 class LazyDraw:
-    """
+    r"""
     A Normal factor's K draws left to the site kernels (``mi_draw``): the model is traced with
     ``placeholder`` -- a [K, *shape] zero-stride view of a private one-element buffer, recognised
     by its data pointer -- and site groups that read it compute ``loc + eps * scale`` in registers
