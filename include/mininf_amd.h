@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 3
+#define MI_ABI_VERSION 4
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -237,6 +237,15 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
                              size_t workspace_bytes, float* dc1, int64_t dc1_stride, float* dc0,
                              int64_t dc0_stride, void* stream);
 
+/* The upstream-independent factors of mi_beta_rsample_backward, per draw:
+ *   out[(k * N + i) * 2 + 0] =  dgrad(x, c1, c1+c0) * (1 - x)
+ *   out[(k * N + i) * 2 + 1] = -dgrad(1 - x, c0, c1+c0) * x          (fp64, [K, N, 2])
+ * so dc1[i] = sum_k dx[k,i] * out[k,i,0] and dc0[i] = sum_k dx[k,i] * out[k,i,1]. They depend only
+ * on the draws, so this can run beside the site kernels; mi_elbo_forward reads them through
+ * mi_factor.dgrad. */
+int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const float* c0,
+                  int64_t c0_stride, int64_t K, int64_t N, double* out, void* stream);
+
 /* Raw generator output for tests: out[k, i] = standard normal eps of mi_normal_rsample. */
 int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
                      int64_t particle_offset, float* out, void* stream);
@@ -355,6 +364,8 @@ typedef struct mi_factor {
   int64_t particle_offset;
   const float* partial[2];      /* MI_DRAW_PARTIALS */
   int64_t partial_rows;
+  const double* dgrad;          /* Beta, MI_DRAW_SOURCES: mi_beta_dgrad output [K, n, 2], or NULL
+                                   to evaluate the implicit gradients in mi_elbo_forward */
 } mi_factor;
 
 /* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f sum_i H_f(i)

@@ -107,6 +107,7 @@ class Factor(ctypes.Structure):
         ("source", Source * MAX_SOURCES), ("draws", c_vp), ("eps", c_vp),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
         ("particle_offset", c_i64), ("partial", c_vp * 2), ("partial_rows", c_i64),
+        ("dgrad", c_vp),
     ]
 
 
@@ -157,6 +158,7 @@ _SIGNATURES = {
     "mi_beta_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
                                        ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                        c_vp]),
+    "mi_beta_dgrad": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,

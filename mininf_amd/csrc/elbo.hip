@@ -161,7 +161,14 @@ template <bool BETA>
 MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int tk,
                       double& s0, double& s1) {
   const int64_t n = F.n;
-  if (BETA) {
+  if (BETA && F.dgrad != nullptr) {   // factors precomputed by mi_beta_dgrad
+    for (int64_t k = r0; k < r1; k += tk) {
+      const double g = (double)source_sum(F, k, i);
+      if (g == 0.0) continue;   // as the evaluating branch: a zero upstream never meets the factor
+      s0 += g * F.dgrad[2 * (k * n + i)];
+      s1 += g * F.dgrad[2 * (k * n + i) + 1];
+    }
+  } else if (BETA) {
     const float a = F.param[0][i * F.stride[0]], b = F.param[1][i * F.stride[1]];
     const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
     const double psi_a = digamma((double)a), psi_b = digamma((double)b);
@@ -480,8 +487,9 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, mi::AbsorbPlan& P, int6
   while (ti < 64 && ti < F.n) ti <<= 1;
   const int tk = mi::kElboThreads / ti;
   const int64_t gx = ceil_div(F.n, ti);
-  // rows per particle lane: one Beta gradient per thread (long fp64 chains), a few otherwise
-  const int64_t per_lane = forward_absorbed(F) ? 1 : 4;
+  // rows per particle lane: one Beta gradient per thread (long fp64 chains) unless mi_beta_dgrad
+  // precomputed them, a few otherwise
+  const int64_t per_lane = (forward_absorbed(F) && F.dgrad == nullptr) ? 1 : 4;
   int64_t slices = ceil_div(rows, (int64_t)tk * per_lane);
   slices = std::max<int64_t>(1, std::min<int64_t>(slices, ceil_div(2048, gx)));
   if (slices > 1 && counters + gx > kMaxCounters) slices = 1;

@@ -266,6 +266,29 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
   }
 }
 
+// Per-draw implicit-gradient factors of Beta draws, independent of the upstream gradient:
+//   out[(k N + i) 2 + 0] =  dgrad(x, a, a+b) (1 - x),  out[... + 1] = -dgrad(1 - x, b, a+b) x
+// so that sum_k dx[k,i] out[k,i,j] is mi_beta_rsample_backward's dc1 / dc0. One thread per
+// (draw, component): the fp64 chains (digammas, dirichlet_grad) are the whole cost, and they depend
+// only on the draw, so this launch can run beside the site kernels that produce dx.
+__global__ __launch_bounds__(kGuideThreads) void k_beta_dgrad(
+    const float* __restrict__ x, const float* __restrict__ c1, int64_t c1_s,
+    const float* __restrict__ c0, int64_t c0_s, int64_t K, int64_t N, double* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (t >= 2 * K * N) return;
+  const int j = (int)(t & 1);
+  const int64_t e = t >> 1, i = e % N;
+  const float a = c1[i * c1_s], b = c0[i * c0_s];
+  const float tot = a + b;  // concentration.sum(-1) in fp32, dirichlet.py:18
+  const double psi_t = digamma((double)tot);
+  const float xv = x[e];
+  if (j == 0) {
+    out[t] = dirichlet_grad(xv, a, tot, digamma((double)a), psi_t) * (double)(1.0f - xv);
+  } else {
+    out[t] = -dirichlet_grad(1.0f - xv, b, tot, digamma((double)b), psi_t) * (double)xv;
+  }
+}
+
 // Raw generator access for tests.
 __global__ void k_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step,
                                 uint32_t stream_id, int64_t poff, float* __restrict__ out) {
@@ -427,6 +450,16 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
   hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o1, o0, gy, N, dc1,
                      dc1_stride, dc0, dc0_stride);
+  return to_code(hipGetLastError());
+}
+
+int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const float* c0,
+                  int64_t c0_stride, int64_t K, int64_t N, double* out, void* stream) {
+  if (x == nullptr || c1 == nullptr || c0 == nullptr || out == nullptr || K < 1 || N < 1)
+    return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_beta_dgrad, dim3((unsigned)ceil_div(2 * K * N, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), x, c1,
+                     c1_stride, c0, c0_stride, K, N, out);
   return to_code(hipGetLastError());
 }
 

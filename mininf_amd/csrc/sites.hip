@@ -542,6 +542,148 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
   publish_flags(flags, fl);
 }
 
+// Bernoulli BCAST over unmasked contiguous data, the shared values read by the scalar unit.
+// Every lane of a wave needs the same x_i, so the chunk is read with s_load (constant address
+// space, wave-uniform addresses) into SGPRs, and a v_pk_fma_f32 takes the SGPR pair (x_i, x_i+1)
+// against the VGPR pair (l_k, l_k) of one particle: two evals per lane per instruction with no LDS
+// traffic (the LDS kernel above moves 1 KB of broadcast data per 8 packed FMAs).
+//
+// log p(x | l) = x l - softplus(l) and d/dl = x - sigmoid(l), so a chunk's partials are
+//   lp:   sum_i x_i l_k            slot: w dl_k sum_i x_i
+// and the particle-constant parts, -N softplus(l_k) and -N w dl_k sigmoid(l_k), are written once,
+// by the chunk-0 blocks, into one extra segment (index gridDim.x): no chunk repeats the
+// transcendentals, and k_finalize adds the extra segment like any other (nseg = chunks + 1).
+// Partial sums: fp32 over at most 64 terms (as k_site_bcast), carried in fp64.
+typedef const __attribute__((address_space(4))) float smem_float;
+
+template <int FAMILY, int kSmemP, int kSmemChunk>
+__global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
+                                                                   float* __restrict__ part,
+                                                                   int64_t nseg,
+                                                                   uint32_t* __restrict__ flags) {
+  __shared__ float scratch[kBcastThreads / 64];
+  const mi_site& st = G.sites[0];
+  const float* xg = G.operands[st.operand[2]].data;
+  const int64_t c = blockIdx.x;
+  const int64_t i0 = c * kSmemChunk;
+  const int len = (int)min((int64_t)kSmemChunk, G.N - i0);
+  uint32_t fl = 0u;
+
+  // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
+  const int64_t K = G.K;
+  const int64_t kbase = (int64_t)blockIdx.y * (kBcastThreads * kSmemP) + threadIdx.x;
+  float lg[kSmemP], dl[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) {
+    const int64_t k = kbase + p * kBcastThreads;
+    const float a = role_scalar(G, st, 0, min(k, K - 1));
+    bool bad;
+    dl[p] = 1.0f;
+    if (FAMILY == MI_BERNOULLI_PROBS) {
+      bad = !(a >= 0.0f && a <= 1.0f);
+      bernoulli_probs_to_logits(a, lg[p], dl[p]);
+    } else {
+      lg[p] = a;
+      bad = a != a;
+    }
+    fl |= (c == 0 && k < K && bad) ? MI_FLAG_PARAM : 0u;
+  }
+
+  // ---- sum_i x_i l_k: element pairs from SGPRs against duplicated particle logits --------------
+  f32x2 ld[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) ld[p] = f32x2{lg[p], lg[p]};
+  double acc[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) acc[p] = 0.0;
+  smem_float* xs = (smem_float*)(xg + i0);
+  auto flush = [&](const f32x2 (&in)[2][kSmemP]) {
+#pragma unroll
+    for (int p = 0; p < kSmemP; ++p)
+      acc[p] += (double)((in[0][p].x + in[0][p].y) + (in[1][p].x + in[1][p].y));
+  };
+  // Whole 256-element blocks in groups of 32 (two s_load_dwordx16): the next group's loads are in
+  // flight during this group's packed FMAs (scalar loads return out of order, so every use waits
+  // for all of them: one group of lookahead). Even and odd element pairs go to separate
+  // accumulators, 2 kSmemP independent chains of 64 terms per block.
+  constexpr int kGroup = 32, kBlock = 256;
+  const int nfull = len & ~(kBlock - 1);
+  int j = 0;
+  if (nfull > 0) {
+    float xc[kGroup];
+#pragma unroll
+    for (int e = 0; e < kGroup; ++e) xc[e] = xs[e];
+    for (; j < nfull; j += kBlock) {
+      f32x2 in[2][kSmemP];
+#pragma unroll
+      for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
+#pragma unroll
+      for (int g = 0; g < kBlock; g += kGroup) {
+        const int nxt = min(j + g + kGroup, nfull - kGroup);   // in bounds; the last is unused
+        float xn[kGroup];
+#pragma unroll
+        for (int e = 0; e < kGroup; ++e) xn[e] = xs[nxt + e];
+#pragma unroll
+        for (int e = 0; e < kGroup; e += 2) {
+          const f32x2 xv = f32x2{xc[e], xc[e + 1]};
+#pragma unroll
+          for (int p = 0; p < kSmemP; ++p)
+            in[(e >> 1) & 1][p] = __builtin_elementwise_fma(xv, ld[p], in[(e >> 1) & 1][p]);
+        }
+#pragma unroll
+        for (int e = 0; e < kGroup; ++e) xc[e] = xn[e];
+      }
+      flush(in);
+    }
+  }
+  if (j < len) {   // the chunk's tail: element pairs, a zero for an odd last element
+    f32x2 in[2][kSmemP];
+#pragma unroll
+    for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
+    for (int e = 0; j < len; j += 2, ++e) {
+      const f32x2 xv = f32x2{xs[j], j + 1 < len ? xs[j + 1] : 0.0f};
+#pragma unroll
+      for (int p = 0; p < kSmemP; ++p)
+        in[e & 1][p] = __builtin_elementwise_fma(xv, ld[p], in[e & 1][p]);
+    }
+    flush(in);
+  }
+
+  // ---- chunk sum and support flags (vector loads, L2-resident by now) --------------------------
+  float s_a = 0.0f;
+  for (int i = threadIdx.x; i < len; i += kBcastThreads) {
+    const float v = xg[i0 + i];
+    fl |= !(v == 0.0f || v == 1.0f) ? MI_FLAG_SUPPORT : 0u;
+    s_a += v;
+  }
+  s_a = block_sum(s_a, scratch);
+
+  // ---- partials of this chunk, and the particle-constant segment from the chunk-0 blocks -------
+  const int o_a = st.operand[0];
+  const int slot_a = (G.compute_grads != 0 && o_a >= 0 && G.operands[o_a].grad_mode == MI_GRAD_PARTICLE)
+                         ? G.operands[o_a].slot : -1;
+  const float w = (float)st.scale;
+  const int64_t extra = nseg - 1;
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) {
+    const int64_t k = kbase + p * kBcastThreads;
+    if (k >= K) continue;
+    part[c * K + k] = (float)acc[p];
+    if (slot_a >= 0) part[((int64_t)(1 + slot_a) * nseg + c) * K + k] = w * (s_a * dl[p]);
+    if (c == 0) {
+      const float l = lg[p];
+      const float t = expf(-fabsf(l));
+      const double softplus = (double)(fmaxf(l, 0.0f) + log1pf(t));
+      const double sig = (double)(l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t));
+      const double n = (double)G.N;
+      part[extra * K + k] = (float)(-n * softplus);
+      if (slot_a >= 0)
+        part[((int64_t)(1 + slot_a) * nseg + extra) * K + k] = w * (float)(-n * sig * (double)dl[p]);
+    }
+  }
+  publish_flags(flags, fl);
+}
+
 // -------------------------------------------------------------------------------------------------
 // Finalize: fixed-order fp64 reduction of partials over segments.
 // -------------------------------------------------------------------------------------------------
@@ -810,6 +952,36 @@ bool bcast_eligible(const mi_group* g) {
   return true;
 }
 
+// Bernoulli BCAST sites over unmasked contiguous data run k_site_bcast_smem (MININF_AMD_BCAST_SMEM=0
+// selects the LDS kernel, for cross-checks).
+bool bcast_smem(const mi_group* g) {
+  static const bool enabled = env_int("MININF_AMD_BCAST_SMEM", 1) != 0;
+  const mi_site& st = g->sites[0];
+  return enabled && (st.family == MI_BERNOULLI_LOGITS || st.family == MI_BERNOULLI_PROBS) &&
+         st.mask == nullptr && g->operands[st.operand[2]].stride_i == 1;
+}
+
+// k_site_bcast_smem launch variants: particles per lane, chunk length (MININF_AMD_BCAST_TUNE).
+struct SmemVariant {
+  int p;
+  int chunk;
+};
+constexpr SmemVariant kSmemVariants[] = {{4, 4096}, {8, 4096}, {4, 8192}, {8, 8192}, {8, 2048}};
+
+int smem_variant() {
+  static const int v = [] {
+    const int n = env_int("MININF_AMD_BCAST_TUNE", 0);
+    return (n >= 0 && n < (int)(sizeof(kSmemVariants) / sizeof(kSmemVariants[0]))) ? n : 0;
+  }();
+  return v;
+}
+
+// Dynamic LDS reserved by the BCAST launches (tuning: caps the workgroups per CU).
+unsigned bcast_lds() {
+  static const unsigned bytes = (unsigned)env_int("MININF_AMD_BCAST_LDS", 0);
+  return bytes;
+}
+
 struct Plan {
   Shape shape;
   int elems;               // ROW: elements per lane per row
@@ -826,8 +998,12 @@ Plan make_plan(const mi_group* g) {
   (void)nv;
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
-    p.nseg = ceil_div(g->N, mi::kBcastChunk);
-    p.grid = dim3((unsigned)p.nseg, (unsigned)ceil_div(g->K, mi::kBcastThreads * mi::kBcastP));
+    const bool smem = bcast_smem(g);
+    const SmemVariant v = kSmemVariants[smem_variant()];
+    const int64_t chunks = ceil_div(g->N, smem ? v.chunk : mi::kBcastChunk);
+    p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
+    p.grid = dim3((unsigned)chunks,
+                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? v.p : mi::kBcastP)));
     return p;
   }
   int dense = -1;
@@ -905,6 +1081,18 @@ size_t finalize_offset(const mi_group* g, const Plan& p) {
   const size_t middle = p.shape != kBcast ? draw_partial_floats(g, p) * sizeof(float)
                                           : (size_t)mi::kPrep * (size_t)g->K * sizeof(float);
   return (prep_offset(g, p) + middle + 255) / 256 * 256;
+}
+
+template <int FAM>
+void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
+  const dim3 block(mi::kBcastThreads);
+  switch (smem_variant()) {
+    case 1: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 4096>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+    case 2: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 8192>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+    case 3: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 8192>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+    case 4: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 2048>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+    default: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+  }
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
@@ -1003,7 +1191,8 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
   if (group->draw.operand != 0 && (p.shape != kRow || !draw_supported(group))) return MI_EUNSUPPORTED;
   float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
-  if (p.shape == kBcast) {
+  const bool smem = p.shape == kBcast && bcast_smem(group);
+  if (p.shape == kBcast && !smem) {
     const dim3 pg((unsigned)ceil_div(G.K, 256));
     switch (G.sites[0].family) {
       case MI_BERNOULLI_LOGITS:
@@ -1028,14 +1217,21 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   switch (p.shape) {
     case kBcast: {
       const bool masked = G.sites[0].mask != nullptr;
+      if (smem) {
+        if (G.sites[0].family == MI_BERNOULLI_PROBS)
+          launch_smem<MI_BERNOULLI_PROBS>(G, p, part, flags, s);
+        else
+          launch_smem<MI_BERNOULLI_LOGITS>(G, p, part, flags, s);
+        break;
+      }
       switch (G.sites[0].family) {
 #define MI_LAUNCH_BCAST(FAM)                                                                   \
   case FAM:                                                                                    \
     if (masked)                                                                                \
-      hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), 0, s, \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), bcast_lds(), s, \
                          G, prep, part, p.nseg, flags);                                        \
     else                                                                                       \
-      hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), 0,   \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), bcast_lds(),   \
                          s, G, prep, part, p.nseg, flags);                                     \
     break;
         MI_LAUNCH_BCAST(MI_BERNOULLI_LOGITS)

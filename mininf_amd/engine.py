@@ -1092,6 +1092,7 @@ class _ElboPlan:
             cfg = plan.drawn.cfg
             if f.family == nat.BETA:
                 d.draws = plan.drawn.base.data_ptr()
+                d.dgrad = nat.ptr(plan.drawn.dgrad)
             else:
                 d.eps = nat.ptr(cfg.noise)
                 d.seed, d.step = guide._philox_key(cfg)
@@ -1194,6 +1195,7 @@ class _ElboPlan:
                   "mi_elbo_workspace_bytes")
         ws = _elbo_workspace(self.device, size.value)
         loss = torch.empty((), dtype=torch.float32, device=self.device)
+        guide.join_side()   # Beta implicit-gradient factors (mi_beta_dgrad) from the side stream
         nat.check(lib.mi_elbo_forward(ctypes.byref(E), ws.data_ptr(), ws.numel(), loss.data_ptr(),
                                       nat.stream_handle(self.device)), "mi_elbo_forward")
         self.state = (E, results, cat_results, lin_results, extra, terms)

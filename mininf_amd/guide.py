@@ -193,10 +193,62 @@ class Drawn:
     cfg: DrawConfig
     base: torch.Tensor
     N: int
+    dgrad: Optional[torch.Tensor] = None   # Beta: mi_beta_dgrad factors [K, N, 2] (side stream)
 
 
 # data pointer of a materialised draw -> its record (reset by every draw_all)
 _DRAWN: Dict[int, Drawn] = {}
+
+# Work launched on a side stream by the draws (Beta implicit-gradient factors) that the main
+# stream has not joined yet: joined by join_side() before the ELBO reads it, and always before a
+# captured step ends.
+_SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
+_PENDING: list = []
+# fp64 [K, N, 2] factors up to this many draws (64 MiB); larger Beta factors are evaluated inside
+# mi_elbo_forward as before
+BETA_DGRAD_MAX = 1 << 22
+
+
+def _side_stream(device: torch.device) -> torch.cuda.Stream:
+    index = device.index if device.index is not None else torch.cuda.current_device()
+    stream = _SIDE_STREAMS.get(index)
+    if stream is None:
+        stream = _SIDE_STREAMS[index] = torch.cuda.Stream(device=device)
+    return stream
+
+
+def join_side() -> None:
+    """Make the current stream wait for the side-stream work of the last draws."""
+    current = torch.cuda.current_stream()
+    for event in _PENDING:
+        current.wait_event(event)
+    _PENDING.clear()
+
+
+def _beta_dgrad(x: torch.Tensor, conc: torch.Tensor, K: int, N: int) -> Optional[torch.Tensor]:
+    """
+    Launch mi_beta_dgrad for the draws x on the side stream (MININF_AMD_BETA_DGRAD=1): its fp64
+    chains depend only on the draws, so they can run beside the site kernels instead of inside
+    mi_elbo_forward. Off by default: measured on MI355X (C2, hipGraph replay) the two-queue graph
+    cost more per node than the overlap saved (0.17 -> 0.24 ms per step).
+    """
+    if not (torch.is_grad_enabled() and conc.requires_grad) or K * N > BETA_DGRAD_MAX or \
+            os.environ.get("MININF_AMD_BETA_DGRAD", "0") != "1":
+        return None
+    main = torch.cuda.current_stream()
+    side = _side_stream(x.device)
+    out = torch.empty((K, N, 2), dtype=torch.float64, device=x.device)
+    side.wait_stream(main)
+    base = conc.data_ptr()
+    nat.check(nat.lib().mi_beta_dgrad(x.data_ptr(), base, 2, base + 4, 2, K, N, out.data_ptr(),
+                                      side.cuda_stream), "mi_beta_dgrad")
+    event = torch.cuda.Event()
+    event.record(side)
+    # main-stream tensors used on the side stream: not reused before the side work is done
+    for t in (x, conc, out):
+        t.record_stream(side)
+    _PENDING.append(event)
+    return out
 
 
 def release_lazy() -> None:
@@ -273,7 +325,7 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
             cfg.noise = cfg.noise.to(device=conc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
         x = _BetaRsampleFn.apply(cfg, conc)
-        _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N)
+        _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N, _beta_dgrad(x, conc, cfg.K, N))
         return x.reshape((cfg.K,) + tuple(shape))
     if cfg.noise is not None:
         return cfg.noise

@@ -129,6 +129,34 @@ def test_bcast_site_matches_oracle(device):
         assert np.abs(got - want).max() <= 1e-5 * np.abs(want).max()
 
 
+@pytest.mark.parametrize("family", ["bernoulli_probs", "bernoulli_logits"])
+@pytest.mark.parametrize("N,K", [(5000, 300), (2048 + 257, 2100), (1024 + 1, 64), (4096 * 3, 513)])
+@pytest.mark.parametrize("kernel", ["smem", "lds"])
+def test_bcast_bernoulli_kernels(device, family, N, K, kernel):
+    """
+    Bernoulli BCAST sites (per-particle parameter against shared data) on both kernels: unmasked
+    contiguous data runs k_site_bcast_smem (scalar-unit loads, whole 256-element blocks plus an
+    odd or even tail), a mask -- all true here, so the answers are the same -- the LDS kernel.
+    Particle counts cover a partial particle block and more than one block.
+    """
+    rng = np.random.default_rng(N + K)
+    x = (rng.random(N) < 0.6).astype(np.float32)
+    if family == "bernoulli_probs":
+        a = rng.random(K).astype(np.float32) * 0.98 + 0.01
+        want_lp, want_d = lpf.bernoulli_probs(a[:, None], x[None, :])
+    else:
+        a = (3 * rng.normal(size=K)).astype(np.float32)
+        want_lp, want_d = lpf.bernoulli_logits(a[:, None], x[None, :])
+    param = torch.as_tensor(a, device=device).reshape(K, 1).requires_grad_()
+    mask = torch.ones(N, dtype=torch.bool, device=device) if kernel == "lds" else None
+    total, _, slot, flags, _ = launch(family, [param], torch.as_tensor(x, device=device), device,
+                                      mask=mask, K=K, N=N)
+    np.testing.assert_allclose(total.numpy(), want_lp.sum(1), rtol=1e-6, atol=1e-6 * N)
+    g = want_d.sum(1)
+    assert np.abs(-slot[0].numpy() - g).max() <= 1e-5 * np.abs(g).max()
+    assert (flags == 0).all()
+
+
 def c5_case(device, n=3000, K=24):
     rng = np.random.default_rng(1)
     mask = torch.as_tensor(rng.random(n) > 0.2, device=device)
@@ -523,14 +551,19 @@ def _absorb_cases(device, case):
     return cond, approx, 16
 
 
-@pytest.mark.parametrize("case", ["beta_scalar", "two_factor", "linear", "linear_sigma",
-                                  "hierarchical", "exp_use"])
+@pytest.mark.parametrize("case", ["beta_scalar", "beta_scalar_dgrad", "two_factor", "linear",
+                                  "linear_sigma", "hierarchical", "exp_use"])
 def test_absorbed_draws_match_autograd(device, case, monkeypatch):
     """
     Guide draws whose backward the ELBO kernel absorbs (mi_factor draw_kind: Beta implicit
     gradient, Normal eps regeneration, fused-draw partials; entropy and exp transform folded in)
     against the same step with the draws' backward left to autograd (MININF_AMD_ABSORB=0).
+    Beta: the implicit-gradient factors evaluated inside mi_elbo_forward, or precomputed by
+    mi_beta_dgrad on the side stream (beta_scalar_dgrad, MININF_AMD_BETA_DGRAD=1).
     """
+    if case == "beta_scalar_dgrad":
+        monkeypatch.setenv("MININF_AMD_BETA_DGRAD", "1")
+        case = "beta_scalar"
     cond, approx, K = _absorb_cases(device, case)
 
     def run(scale=1.0):

@@ -1,0 +1,69 @@
+// Microbenchmark: sustained FP32 VALU rate of v_pk_fma_f32 vs v_fma_f32 on this device (the
+// ceiling the BCAST / linear site kernels are compared with). Build: hipcc -O3 --offload-arch=gfx950
+#include <hip/hip_runtime.h>
+#include <cstdio>
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_pk(float* out, float a, int iters) {
+  f32x2 acc[CH];
+  const f32x2 m = f32x2{a, a * 0.5f};
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = f32x2{(float)threadIdx.x + c, (float)c};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) acc[c] = __builtin_elementwise_fma(acc[c], m, m);
+  }
+  float s = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) s += acc[c].x + acc[c].y;
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_fma(float* out, float a, int iters) {
+  float acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = (float)threadIdx.x + c;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) acc[c] = fmaf(acc[c], a, a);
+  }
+  float s = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) s += acc[c];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <typename F>
+void run(const char* name, F launch, double flop) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int w = 0; w < 3; ++w) launch();
+  hipEventRecord(a);
+  const int reps = 10;
+  for (int r = 0; r < reps; ++r) launch();
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  printf("%-28s %8.1f us  %7.1f TFLOP/s\n", name, 1e3 * ms / reps, flop * reps / (ms * 1e-3) / 1e12);
+}
+
+int main() {
+  float* out;
+  const int blocks = 2048, iters = 2000;
+  hipMalloc(&out, blocks * 256 * sizeof(float));
+  const double lanes = (double)blocks * 256 * iters * 16;
+  run("pk_fma 8 chains", [&] { hipLaunchKernelGGL(k_pk<8>, dim3(blocks), dim3(256), 0, 0, out, 0.999f, iters); }, lanes * 8 * 4);
+  run("pk_fma 4 chains", [&] { hipLaunchKernelGGL(k_pk<4>, dim3(blocks), dim3(256), 0, 0, out, 0.999f, iters); }, lanes * 4 * 4);
+  run("fma 8 chains", [&] { hipLaunchKernelGGL(k_fma<8>, dim3(blocks), dim3(256), 0, 0, out, 0.999f, iters); }, lanes * 8 * 2);
+  run("fma 16 chains", [&] { hipLaunchKernelGGL(k_fma<16>, dim3(blocks), dim3(256), 0, 0, out, 0.999f, iters); }, lanes * 16 * 2);
+  run("pk_fma 8 chains (1024 blk)", [&] { hipLaunchKernelGGL(k_pk<8>, dim3(1024), dim3(256), 0, 0, out, 0.999f, iters); }, lanes / 2 * 8 * 4);
+  return 0;
+}
