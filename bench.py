@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 import mininf_amd  # noqa: E402
 from mininf_amd import engine  # noqa: E402
-from mininf_amd.distributed import all_reduce_gradients  # noqa: E402
+from mininf_amd.distributed import GradientBucket  # noqa: E402
 from mininf_amd.graph import StepGraph  # noqa: E402
 from torch.distributions import Bernoulli, Beta, Normal  # noqa: E402
 
@@ -272,18 +272,29 @@ def main():
     timer = EventTimer()
     engine.KERNEL_TIMER = timer
 
+    # N > 1: the step is split around the one all-reduce of the gradients -- zero_grad, forward,
+    # backward and packing the gradients into a flat bucket (captured), the RCCL all-reduce of the
+    # bucket, then Adam on gradients bound to the reduced bucket (captured separately).
+    bucket = GradientBucket(module.parameters(), group) if world > 1 else None
+
     def forward_backward():
         optimizer.zero_grad(set_to_none=True)
         loss = loss_fn(w["conditioned"](), w["guide"]())
         loss.backward()
         if world == 1:
             optimizer.step()
+        else:
+            bucket.pack()
         return loss
+
+    def apply_update():
+        bucket.bind()
+        optimizer.step()
 
     def finish_step():
         if world > 1:
-            all_reduce_gradients(module.parameters(), group)
-            optimizer.step()
+            bucket.all_reduce()
+            apply_update()
 
     def barrier():
         if world > 1:
@@ -323,10 +334,13 @@ def main():
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
         captured = StepGraph(forward_backward, warmup=2)
+        update = StepGraph(apply_update, warmup=1) if world > 1 else None
 
         def graph_step():
             out = captured()
-            finish_step()
+            if world > 1:
+                bucket.all_reduce()
+                update()
             return out
 
         for _ in range(args.warmup):

@@ -44,3 +44,52 @@ def all_reduce_gradients(parameters: Iterable[torch.nn.Parameter], group=None,
         g.copy_(bucket[offset:offset + n].view_as(g))
         offset += n
     return bucket[offset] if loss is not None else None
+
+
+class GradientBucket:
+    """
+    The guide gradients of one rank as ONE flat fp32 buffer, for a step split around the
+    all-reduce: ``pack()`` (one concatenation kernel, capturable) after the backward,
+    ``all_reduce()`` (one RCCL call), then ``bind()`` points every ``param.grad`` at its slice of the
+    reduced buffer -- no copy back -- so the optimizer step (also capturable) reads the sums.
+    The result equals :func:`all_reduce_gradients` (the gloo tests check this). Clear the
+    gradients with ``zero_grad(set_to_none=True)`` before each backward, so that the backward
+    does not accumulate into the bound views.
+
+    Args:
+        parameters: The parameters whose gradients to reduce (all of them must receive one).
+        group: Process group (default: the world).
+    """
+    def __init__(self, parameters: Iterable[torch.nn.Parameter], group=None) -> None:
+        self.params = [p for p in parameters if p.requires_grad]
+        if not self.params:
+            raise ValueError("no parameters to reduce")
+        dtypes = {p.dtype for p in self.params}
+        if len(dtypes) != 1:
+            raise ValueError(f"parameters of one dtype expected, got {dtypes}")
+        self.group = group
+        self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=dtypes.pop(),
+                                device=self.params[0].device)
+        self.views = []
+        offset = 0
+        for p in self.params:
+            self.views.append(self.flat[offset:offset + p.numel()].view_as(p))
+            offset += p.numel()
+
+    def pack(self) -> None:
+        """Copy this rank's gradients into the flat buffer."""
+        grads = []
+        for p in self.params:
+            if p.grad is None:
+                raise RuntimeError("a parameter of the bucket has no gradient")
+            grads.append(p.grad.reshape(-1))
+        torch.cat(grads, out=self.flat)
+
+    def all_reduce(self) -> None:
+        """Sum the flat buffer over the ranks (in place)."""
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+
+    def bind(self) -> None:
+        """Make every ``param.grad`` the view of its slice of the flat buffer."""
+        for p, v in zip(self.params, self.views):
+            p.grad = v

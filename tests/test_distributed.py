@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mininf_amd.distributed import all_reduce_gradients
+from mininf_amd.distributed import GradientBucket, all_reduce_gradients
 from mininf_amd.nn import EvidenceLowerBoundLoss
 
 
@@ -73,3 +73,50 @@ def test_indivisible_particles_rejected():
             um.patch.object(dist, "get_rank", return_value=0):
         with pytest.raises(ValueError, match="not divisible"):
             loss._shard()
+
+
+def bucket_worker(rank, world, port, queue):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        a = torch.nn.Parameter(torch.randn(3, 2))
+        b = torch.nn.Parameter(torch.randn(()))
+        bucket = GradientBucket([a, b], dist.group.WORLD)
+        out = []
+        for step in range(2):   # twice: the second backward runs with grads bound to the bucket
+            for p in (a, b):
+                p.grad = None
+            ((rank + 1) * (a.square().sum() + step * b * a.sum())).backward()
+            bucket.pack()
+            bucket.all_reduce()
+            bucket.bind()
+            got = [a.grad.clone(), b.grad.clone()]
+            for p in (a, b):
+                p.grad = None
+            ((rank + 1) * (a.square().sum() + step * b * a.sum())).backward()
+            all_reduce_gradients([a, b], dist.group.WORLD)
+            out.append([torch.equal(x, y) for x, y in zip(got, [a.grad, b.grad])])
+        queue.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_bucket_matches_all_reduce_gradients():
+    """
+    The split step bench.py captures for N > 1 (pack in the backward graph, one all-reduce,
+    gradients bound to the reduced buffer) gives the same sums as all_reduce_gradients.
+    """
+    world = 2
+    ctx = mp.get_context("spawn")
+    queue = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=bucket_worker, args=(r, world, port, queue)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [queue.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in results:
+        assert all(all(step) for step in out), (rank, out)
