@@ -246,6 +246,29 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
 int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const float* c0,
                   int64_t c0_stride, int64_t K, int64_t N, double* out, void* stream);
 
+/* Start of one ELBO step (EvidenceLowerBoundLoss.forward) in one launch: *snapshot = *counter (the
+ * generator step this call's draws and their backward use), *counter += 1, and
+ * flags[0 .. nflags) = 0 (the call's validation words, MI_GROUP_FLAGS_ZEROED). */
+int mi_step_begin(uint64_t* counter, uint64_t* snapshot, uint32_t* flags, int64_t nflags,
+                  void* stream);
+
+/* Constrained parameters of one guide factor in one launch, interleaved [n, m]:
+ *   out[i * m + j] = exp(u[j][i * stride[j]])   (transform[j] MI_TRANSFORM_EXP: transform_to(positive),
+ *                                                 torch constraint_registry.py:184-189)
+ *                  = u[j][i * stride[j]]        (MI_TRANSFORM_NONE)
+ * ParameterizedDistribution.forward (reference nn.py:86-96) for a Beta guide, whose Dirichlet keeps
+ * exactly this [..., 2] (concentration1, concentration0) layout (beta.py:36-40). */
+#define MI_MAX_PARAMS 4
+typedef struct mi_params {
+  int32_t m;
+  int32_t pad0;
+  int64_t n;
+  const float* u[MI_MAX_PARAMS];
+  int64_t stride[MI_MAX_PARAMS];
+  int32_t transform[MI_MAX_PARAMS];
+} mi_params;
+int mi_transform_params(const mi_params* params, float* out, void* stream);
+
 /* Raw generator output for tests: out[k, i] = standard normal eps of mi_normal_rsample. */
 int mi_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step, uint32_t stream_id,
                      int64_t particle_offset, float* out, void* stream);

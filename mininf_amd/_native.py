@@ -111,6 +111,15 @@ class Factor(ctypes.Structure):
     ]
 
 
+MAX_PARAMS = 4
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int32), ("pad0", ctypes.c_int32), ("n", c_i64),
+                ("u", c_vp * MAX_PARAMS), ("stride", c_i64 * MAX_PARAMS),
+                ("transform", ctypes.c_int32 * MAX_PARAMS)]
+
+
 class Elbo(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("num_terms", ctypes.c_int32), ("num_factors", ctypes.c_int32),
@@ -159,6 +168,8 @@ _SIGNATURES = {
                                        ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                        c_vp]),
     "mi_beta_dgrad": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mi_step_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mi_transform_params": (ctypes.c_int, [ctypes.POINTER(Params), c_vp, c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,

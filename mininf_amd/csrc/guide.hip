@@ -289,6 +289,41 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_dgrad(
   }
 }
 
+// Start of an ELBO step in one launch: snapshot[0] = counter[0] (the step the draws of this call use,
+// read again by the backward's eps regeneration), counter[0] += 1 (the next call draws anew, also
+// when replayed from a captured graph), flags[0 .. nflags) = 0 (the step's validation words).
+__global__ __launch_bounds__(kGuideThreads) void k_step_begin(uint64_t* __restrict__ counter,
+                                                              uint64_t* __restrict__ snapshot,
+                                                              uint32_t* __restrict__ flags,
+                                                              int64_t nflags) {
+  const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (t == 0) {
+    const uint64_t c = *counter;
+    *snapshot = c;
+    *counter = c + 1u;
+  }
+  if (t < nflags) flags[t] = 0u;
+}
+
+// Constrained guide parameters of one factor, interleaved: out[i * m + j] = T_j(u_j[i * stride_j])
+// with T_j = exp (transform_to(positive), constraint_registry.py:184-189) or the identity.
+__global__ __launch_bounds__(kGuideThreads) void k_transform_params(const mi_params P,
+                                                                    float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (t >= P.n * P.m) return;
+  const int64_t i = t / P.m;
+  const int j = (int)(t - i * P.m);
+  float u = 0.0f;
+  int tr = MI_TRANSFORM_NONE;
+#pragma unroll
+  for (int q = 0; q < MI_MAX_PARAMS; ++q)
+    if (q == j) {
+      u = P.u[q][i * P.stride[q]];
+      tr = P.transform[q];
+    }
+  out[t] = tr == MI_TRANSFORM_EXP ? expf(u) : u;
+}
+
 // Raw generator access for tests.
 __global__ void k_philox_normal(int64_t K, int64_t N, uint64_t seed, uint64_t step,
                                 uint32_t stream_id, int64_t poff, float* __restrict__ out) {
@@ -460,6 +495,31 @@ int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const floa
   hipLaunchKernelGGL(mi::k_beta_dgrad, dim3((unsigned)ceil_div(2 * K * N, mi::kGuideThreads)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), x, c1,
                      c1_stride, c0, c0_stride, K, N, out);
+  return to_code(hipGetLastError());
+}
+
+int mi_step_begin(uint64_t* counter, uint64_t* snapshot, uint32_t* flags, int64_t nflags,
+                  void* stream) {
+  if (counter == nullptr || snapshot == nullptr || nflags < 0 || (nflags > 0 && flags == nullptr))
+    return MI_EINVAL;
+  const int64_t threads = std::max<int64_t>(1, nflags);
+  hipLaunchKernelGGL(mi::k_step_begin, dim3((unsigned)ceil_div(threads, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), counter,
+                     snapshot, flags, nflags);
+  return to_code(hipGetLastError());
+}
+
+int mi_transform_params(const mi_params* params, float* out, void* stream) {
+  if (params == nullptr || out == nullptr || params->m < 1 || params->m > MI_MAX_PARAMS ||
+      params->n < 1)
+    return MI_EINVAL;
+  for (int j = 0; j < params->m; ++j)
+    if (params->u[j] == nullptr ||
+        (params->transform[j] != MI_TRANSFORM_NONE && params->transform[j] != MI_TRANSFORM_EXP))
+      return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_transform_params,
+                     dim3((unsigned)ceil_div(params->n * params->m, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), *params, out);
   return to_code(hipGetLastError());
 }
 

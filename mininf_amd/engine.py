@@ -997,8 +997,10 @@ class _ElboPlan:
     def __init__(self, K: int, g0: float, device: torch.device, launchers, categorical,
                  fallback: List[torch.Tensor], factors: List[EntropyFactor],
                  entropy_scale: float, linears: Optional[List[_LinearLauncher]] = None,
-                 absorbed: Optional[Dict[int, _Absorbed]] = None) -> None:
+                 absorbed: Optional[Dict[int, _Absorbed]] = None,
+                 zeroed_flags: Optional[torch.Tensor] = None) -> None:
         self.K, self.g0, self.device = K, g0, device
+        self.zeroed_flags = zeroed_flags
         self.launchers = launchers
         self.categorical = categorical
         self.linears = linears or []
@@ -1124,7 +1126,12 @@ class _ElboPlan:
         # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
         sizes = [1] * (len(self.categorical) + len(self.linears)) + \
             [len(l.sites) for l in self.launchers]
-        self.flags = torch.zeros(max(1, sum(sizes)), dtype=torch.int32, device=self.device)
+        words = max(1, sum(sizes))
+        zeroed, self.zeroed_flags = self.zeroed_flags, None   # zero only for the first forward
+        if zeroed is not None and zeroed.numel() >= words:
+            self.flags = zeroed[:words]
+        else:
+            self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
         cursor = len(self.categorical) + len(self.linears)
         for li, (launcher, holder) in enumerate(zip(self.launchers, self.holders)):
             need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
@@ -1342,12 +1349,14 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
 
 
 def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[EntropyFactor],
-         entropy_scale: float, samples: Optional[Dict[str, torch.Tensor]] = None
-         ) -> Tuple[torch.Tensor, LogJoint]:
+         entropy_scale: float, samples: Optional[Dict[str, torch.Tensor]] = None,
+         flags: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, LogJoint]:
     """
     ``g0 * sum_k log p(x, z_k) - entropy_scale * H[factors]`` as one autograd node: the site
     kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
     backward is one ``mi_elbo_backward`` launch (plus the guide samplers' own backward).
+    ``flags``: already-zeroed int32 validation words for the step (``mi_step_begin``), used when
+    the plan's sites fit.
     """
     _, bad = _lazy_uses(trace)
     if bad:
@@ -1362,7 +1371,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
-                     entropy_scale, linears, absorbed)
+                     entropy_scale, linears, absorbed, flags)
     loss = _ElboFn.apply(plan, *plan.inputs())
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):

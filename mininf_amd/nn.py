@@ -14,12 +14,13 @@ estimates. The returned loss is a 0-d float32 tensor with ``grad_fn``.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, cast, Dict, Optional, Set, Type
 
 import torch
 from torch import distributions, nn
 
-from . import engine, graph, guide, linear, particles
+from . import _native, engine, graph, guide, linear, particles
 from .core import condition, LogProbTracer
 from .util import _normalize_shape, maybe_as_tensor, OptionalSize, TensorDict
 
@@ -93,6 +94,9 @@ class ParameterizedDistribution(nn.Module):
 
     def forward(self) -> distributions.Distribution:
         """"""
+        fused = self._fused_beta()
+        if fused is not None:
+            return fused
         constraints = cast(Dict, self.distribution_cls.arg_constraints)
         arguments = {}
         sources = {}
@@ -113,6 +117,60 @@ class ParameterizedDistribution(nn.Module):
         # write the guide's gradients directly (mi_factor transforms, engine.elbo).
         distribution._mininf_amd_sources = sources  # type: ignore[attr-defined]
         return distribution  # type: ignore
+
+
+    def _fused_beta(self) -> Optional[distributions.Distribution]:
+        """
+        A Beta guide with both concentrations learnable on the device: the two ``exp`` transforms
+        and the ``torch.stack`` of ``Beta.__init__`` (beta.py:36-40) as one launch
+        (``mi_transform_params``) writing the interleaved ``[..., 2]`` array its Dirichlet keeps;
+        the distribution is then assembled exactly as ``Beta.__init__`` does, argument
+        validation included.
+        """
+        if self.distribution_cls is not distributions.Beta:
+            return None
+        params = self.distribution_parameters
+        if set(params) != {"concentration1", "concentration0"} or \
+                set(self.distribution_constants) - {"validate_args"}:
+            return None
+        u1, u0 = params["concentration1"], params["concentration0"]
+        if not (u1.is_cuda and u1.dtype == torch.float32 and u0.dtype == torch.float32 and
+                u1.device == u0.device and u1.shape == u0.shape):
+            return None
+        conc = _ExpStackFn.apply(u1, u0)
+        validate = self.distribution_constants.get("validate_args")
+        beta = distributions.Beta.__new__(distributions.Beta)
+        beta._dirichlet = distributions.Dirichlet(conc, validate_args=validate)
+        distributions.Distribution.__init__(beta, beta._dirichlet._batch_shape,
+                                            validate_args=validate)
+        beta._mininf_amd_sources = {  # type: ignore[attr-defined]
+            "concentration1": (u1, "exp"), "concentration0": (u0, "exp")}
+        return beta
+
+
+class _ExpStackFn(torch.autograd.Function):
+    """``torch.stack([exp(u1), exp(u0)], -1)`` in one launch (``mi_transform_params``)."""
+    @staticmethod
+    def forward(ctx, u1: torch.Tensor, u0: torch.Tensor):  # type: ignore[override]
+        out = torch.empty(tuple(u1.shape) + (2,), dtype=torch.float32, device=u1.device)
+        P = _native.Params()
+        P.m, P.n = 2, max(1, u1.numel())
+        for j, u in enumerate((u1, u0)):
+            flat = u.reshape(-1)
+            P.u[j] = flat.data_ptr()
+            P.stride[j] = flat.stride(0) if u.numel() > 1 else 0
+            P.transform[j] = _native.TRANSFORM_EXP
+        _native.check(_native.lib().mi_transform_params(ctypes.byref(P), out.data_ptr(),
+                                                        _native.stream_handle(u1.device)),
+                      "mi_transform_params")
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad: torch.Tensor):  # type: ignore[override]
+        (out,) = ctx.saved_tensors
+        d = grad * out   # d exp(u) / du = exp(u)
+        return d[..., 0], d[..., 1]
 
 
 class FactorizedDistribution(DistributionDict):
@@ -192,6 +250,9 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.process_group = process_group
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
 
+    # validation words zeroed with the step counter's advance; plans with more sites zero their own
+    FLAG_WORDS = 64
+
     def _shard(self):
         """
         (world size, rank, local K, particle offset) of this rank.
@@ -219,9 +280,17 @@ class EvidenceLowerBoundLoss(nn.Module):
             if self._counter is None or self._counter.device != device:
                 self._counter = torch.zeros(1, dtype=torch.int64, device=device)
             # The draws (and their regeneration in backward) use a snapshot of the device counter,
-            # which is then advanced on the device -- replays of a captured step draw anew.
-            step = self._counter.clone()
-            self._counter.add_(1)
+            # which is advanced on the device -- replays of a captured step draw anew -- by the
+            # same launch that zeroes the call's validation words (mi_step_begin).
+            if device.type == "cuda":
+                step = torch.empty(1, dtype=torch.int64, device=device)
+                flags = torch.empty(self.FLAG_WORDS, dtype=torch.int32, device=device)
+                _native.check(_native.lib().mi_step_begin(
+                    self._counter.data_ptr(), step.data_ptr(), flags.data_ptr(),
+                    self.FLAG_WORDS, _native.stream_handle(device)), "mi_step_begin")
+            else:   # the samplers reject host guides with the engine's device error
+                step, flags = self._counter.clone(), None
+                self._counter.add_(1)
             # Large Normal factors are drawn lazily: the site kernels compute them in registers
             # (mi_draw). If the model uses a draw in any other operation, the trace is repeated
             # with real draws (same counter, same values).
@@ -248,7 +317,8 @@ class EvidenceLowerBoundLoss(nn.Module):
             # Fused path: site kernels, guide entropy and the reduction in one autograd node.
             factors, rest = engine.entropy_factors(approximation)
             try:
-                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples)
+                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples,
+                                          flags=flags)
             finally:
                 # The placeholder registry is only needed while tracing and planning; holding it
                 # would keep this step's autograd graph (and its AccumulateGrad streams) alive.

@@ -606,3 +606,30 @@ def test_absorption_plan(device):
     assert ("z", nat.DRAW_SOURCES) not in seen[1] and ("z", nat.DRAW_PARTIALS) not in seen[1]
     assert seen[2] == [("theta", nat.DRAW_SOURCES)]
     assert seen[3] == [("theta", nat.DRAW_SOURCES)]
+
+
+def test_fused_beta_guide_matches_torch_construction(device):
+    """
+    ParameterizedDistribution(Beta) on the device builds its interleaved concentration array in one
+    launch (mi_transform_params) and assembles the Beta as Beta.__init__ does: same parameters,
+    shapes, log densities, entropy and gradients as the host module's torch construction.
+    """
+    c1 = torch.tensor([0.7, 2.5, 9.0])
+    c0 = torch.tensor([1.3, 0.4, 6.0])
+    host = mi.nn.ParameterizedDistribution(Beta, concentration1=c1, concentration0=c0)
+    dev = mi.nn.ParameterizedDistribution(Beta, concentration1=c1, concentration0=c0).to(device)
+    qh, qd = host(), dev()
+    assert type(qd) is Beta and qd.batch_shape == qh.batch_shape and qd.event_shape == ()
+    torch.testing.assert_close(qd.concentration1.cpu(), qh.concentration1, rtol=1e-6, atol=0)
+    torch.testing.assert_close(qd.concentration0.cpu(), qh.concentration0, rtol=1e-6, atol=0)
+    x = torch.tensor([0.2, 0.5, 0.9])
+    (qh.log_prob(x).sum() + qh.entropy().sum()).backward()
+    (qd.log_prob(x.to(device)).sum() + qd.entropy().sum()).backward()
+    for name, p in host.distribution_parameters.items():
+        torch.testing.assert_close(dev.distribution_parameters[name].grad.cpu(), p.grad,
+                                   rtol=1e-5, atol=1e-6)
+    bad = mi.nn.ParameterizedDistribution(Beta, concentration1=c1, concentration0=c0,
+                                          validate_args=True).to(device)
+    bad.distribution_parameters["concentration1"].data.fill_(float("nan"))
+    with pytest.raises(ValueError, match="concentration"):   # Dirichlet's check, as in torch
+        bad()
