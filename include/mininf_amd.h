@@ -118,6 +118,23 @@ typedef struct mi_draw {
   float* dscale;
 } mi_draw;
 
+/* Independent work carried by extra workgroups of a group's launch (see mi_group_side_supported):
+ * the per-draw Beta implicit-gradient factors of mi_beta_dgrad for draws x [K, N] (row-major) of
+ * Beta(c1, c0), written to out [K, N, 2] (fp64). Their fp64 chains are latency-bound and
+ * independent of the group's sites, so they run beside the site kernel's VALU-bound workgroups
+ * instead of inside mi_elbo_forward (which then reads them through mi_factor.dgrad).
+ * out == NULL: no side job (a zero-initialised descriptor has none). */
+typedef struct mi_side {
+  const float* x;
+  const float* c1;
+  int64_t c1_stride;
+  const float* c0;
+  int64_t c0_stride;
+  int64_t K;
+  int64_t N;
+  double* out;
+} mi_side;
+
 /* A group of sites evaluated over one shared [K, N] element space in a single pass, so that an
  * operand read by several sites (e.g. a latent z that is the value of one site and the loc of
  * another) is loaded once and its gradient accumulated in registers. */
@@ -133,6 +150,7 @@ typedef struct mi_group {
   mi_site sites[MI_MAX_SITES];
   mi_operand operands[MI_MAX_OPERANDS];
   mi_draw draw;          /* draw.operand == 0: no operand is a fused guide draw */
+  mi_side side;          /* side.out == NULL: no side job */
 } mi_group;
 
 /* Library identification: returns MI_ABI_VERSION and writes the offload target ("gfx950"). */
@@ -142,6 +160,10 @@ int mi_abi_version(char* target, size_t target_bytes);
 int mi_struct_sizes(size_t* operand, size_t* site, size_t* group);
 
 /* ---- site log-probability accumulation (replaces core.py:211-273 + torch log_prob) ------------ */
+
+/* *supported = 1 when mi_group_forward runs `group`'s side job (the Bernoulli BCAST kernel over
+ * unmasked contiguous data carries it), else 0: the caller then computes the factors elsewhere. */
+int mi_group_side_supported(const mi_group* group, int* supported);
 
 /* Workspace needed by mi_group_forward for this descriptor. */
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);

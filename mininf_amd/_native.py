@@ -68,6 +68,11 @@ class Draw(ctypes.Structure):
     ]
 
 
+class Side(ctypes.Structure):
+    _fields_ = [("x", c_vp), ("c1", c_vp), ("c1_stride", c_i64), ("c0", c_vp),
+                ("c0_stride", c_i64), ("K", c_i64), ("N", c_i64), ("out", c_vp)]
+
+
 class Group(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("N", c_i64),
@@ -75,7 +80,7 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
-        ("draw", Draw),
+        ("draw", Draw), ("side", Side),
     ]
 
 
@@ -169,6 +174,8 @@ _SIGNATURES = {
                                        c_vp]),
     "mi_beta_dgrad": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "mi_step_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "mi_group_side_supported": (ctypes.c_int, [ctypes.POINTER(Group),
+                                               ctypes.POINTER(ctypes.c_int)]),
     "mi_transform_params": (ctypes.c_int, [ctypes.POINTER(Params), c_vp, c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),

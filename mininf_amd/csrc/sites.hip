@@ -19,6 +19,7 @@
 //            log p is hoisted out of the element loop, leaving one FMA per (particle, element).
 // All three write per-(segment, particle) partial sums (fp32) that k_finalize reduces in fp64 in a
 // fixed order, so results are deterministic run to run.
+#include "beta_grad.hpp"
 #include "common.hpp"
 
 #include <algorithm>
@@ -556,15 +557,36 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
 // Partial sums: fp32 over at most 64 terms (as k_site_bcast), carried in fp64.
 typedef const __attribute__((address_space(4))) float smem_float;
 
+// One workgroup of a group's side job (mi_side): the mi_beta_dgrad factors of 256 (draw, component)
+// pairs, one per thread -- latency-bound fp64 chains that run beside the site workgroups.
+MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
+  const int64_t t = b * kBcastThreads + threadIdx.x;
+  if (t >= 2 * S.K * S.N) return;
+  const int j = (int)(t & 1);
+  const int64_t e = t >> 1, i = e % S.N;
+  const float a = S.c1[i * S.c1_stride], bb = S.c0[i * S.c0_stride];
+  const float tot = a + bb;  // concentration.sum(-1) in fp32, dirichlet.py:18
+  const double psi_t = digamma((double)tot);
+  const float xv = S.x[e];
+  S.out[t] = j == 0
+                 ? dirichlet_grad(xv, a, tot, digamma((double)a), psi_t) * (double)(1.0f - xv)
+                 : -dirichlet_grad(1.0f - xv, bb, tot, digamma((double)bb), psi_t) * (double)xv;
+}
+
+
 template <int FAMILY, int kSmemP, int kSmemChunk>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
+  const int64_t c = blockIdx.x;
+  if (c >= nseg - 1) {   // workgroups past the chunks: the side job (mi_side), row 0 only
+    if (blockIdx.y == 0) beta_side_block(G.side, c - (nseg - 1));
+    return;
+  }
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
-  const int64_t c = blockIdx.x;
   const int64_t i0 = c * kSmemChunk;
   const int len = (int)min((int64_t)kSmemChunk, G.N - i0);
   uint32_t fl = 0u;
@@ -895,6 +917,10 @@ bool validate_group(const mi_group* g) {
                     (g->compute_grads && !(g->options & MI_GROUP_DRAW_PARTIALS) &&
                      (g->draw.dloc == nullptr || g->draw.dscale == nullptr))))
     return false;
+  if (g->side.out != nullptr &&
+      (g->side.x == nullptr || g->side.c1 == nullptr || g->side.c0 == nullptr || g->side.K < 1 ||
+       g->side.N < 1))
+    return false;
   for (int o = 0; o < g->num_operands; ++o) {
     const mi_operand& op = g->operands[o];
     if (o == draw) continue;  // computed in the kernel
@@ -1002,7 +1028,9 @@ Plan make_plan(const mi_group* g) {
     const SmemVariant v = kSmemVariants[smem_variant()];
     const int64_t chunks = ceil_div(g->N, smem ? v.chunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
-    p.grid = dim3((unsigned)chunks,
+    const int64_t side = (smem && g->side.out != nullptr)
+                             ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
+    p.grid = dim3((unsigned)(chunks + side),
                   (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? v.p : mi::kBcastP)));
     return p;
   }
@@ -1155,6 +1183,13 @@ int mi_struct_sizes(size_t* operand, size_t* site, size_t* group) {
   return 0;
 }
 
+int mi_group_side_supported(const mi_group* group, int* supported) {
+  if (!validate_group(group) || supported == nullptr) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  *supported = (p.shape == kBcast && bcast_smem(group)) ? 1 : 0;
+  return 0;
+}
+
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
   if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -1190,6 +1225,7 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   bool prescaled = false;  // partials already carry the site scales
   float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
   if (group->draw.operand != 0 && (p.shape != kRow || !draw_supported(group))) return MI_EUNSUPPORTED;
+  if (group->side.out != nullptr && !(p.shape == kBcast && bcast_smem(group))) return MI_EUNSUPPORTED;
   float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
   const bool smem = p.shape == kBcast && bcast_smem(group);
   if (p.shape == kBcast && !smem) {

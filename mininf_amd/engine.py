@@ -163,6 +163,11 @@ class _GroupLauncher:
         # (MI_GROUP_DRAW_PARTIALS); set by the ELBO plan when it absorbs the draw
         self.draw_partials = False
         self.workspace: Optional[torch.Tensor] = None   # of the last run
+        # Beta implicit-gradient factors carried as extra workgroups of this launch (mi_side):
+        # (draws x [K, N], concentration [N, 2]) set by the ELBO plan; side_out is the [K, N, 2]
+        # result of the last run, or None when the group's kernel cannot carry the job
+        self.side: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+        self.side_out: Optional[torch.Tensor] = None
 
     def try_add(self, site: SiteRecord, views: List[_View], mask: Optional[_View]) -> bool:
         constants = [v.constant for v in views]
@@ -347,6 +352,24 @@ class _GroupLauncher:
         nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
                   "mi_group_workspace_bytes")
         workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        self.side_out = None
+        if self.side is not None:
+            x, conc = self.side
+            supported = ctypes.c_int(0)
+            nat.check(lib.mi_group_side_supported(ctypes.byref(group), ctypes.byref(supported)),
+                      "mi_group_side_supported")
+            if supported.value:
+                Ks, Ns = x.shape
+                out = torch.empty((Ks, Ns, 2), dtype=torch.float64, device=device)
+                sd = group.side
+                sd.x, sd.c1, sd.c1_stride = x.data_ptr(), conc.data_ptr(), 2
+                sd.c0, sd.c0_stride = conc.data_ptr() + 4, 2
+                sd.K, sd.N, sd.out = Ks, Ns, out.data_ptr()
+                nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
+                          "mi_group_workspace_bytes")
+                if workspace.numel() < size.value:
+                    workspace = torch.empty(size.value, dtype=torch.uint8, device=device)
+                self.side_out = out
         total = torch.empty(K, dtype=torch.float32, device=device)
         site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device) \
             if self.per_site else None
@@ -818,6 +841,7 @@ class _Absorbed:
     params: List[Optional[Tuple[torch.Tensor, int]]]
     drawn: Optional[guide.Drawn] = None
     lazy: Optional[guide.LazyDraw] = None
+    side_dgrad: Optional[torch.Tensor] = None   # Beta factors computed by a site launch (mi_side)
 
 
 _FACTOR_PARAMS = {nat.NORMAL: ("loc", "scale"), nat.BETA: ("concentration1", "concentration0")}
@@ -1094,7 +1118,8 @@ class _ElboPlan:
             cfg = plan.drawn.cfg
             if f.family == nat.BETA:
                 d.draws = plan.drawn.base.data_ptr()
-                d.dgrad = nat.ptr(plan.drawn.dgrad)
+                d.dgrad = nat.ptr(plan.side_dgrad if plan.side_dgrad is not None
+                                  else plan.drawn.dgrad)
             else:
                 d.eps = nat.ptr(cfg.noise)
                 d.seed, d.step = guide._philox_key(cfg)
@@ -1133,11 +1158,26 @@ class _ElboPlan:
         else:
             self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
         cursor = len(self.categorical) + len(self.linears)
+        # absorbed Beta draws whose implicit-gradient factors a site launch can carry (mi_side)
+        side_jobs = [plan for plan in self.absorbed.values()
+                     if plan.drawn is not None and plan.drawn.family == guide.BETA_FAMILY and
+                     plan.drawn.dgrad is None and plan.drawn.conc is not None and
+                     plan.drawn.base.numel() <= guide.BETA_DGRAD_MAX and
+                     os.environ.get("MININF_AMD_BETA_SIDE", "1") != "0"]
+        for plan in side_jobs:
+            plan.side_dgrad = None
         for li, (launcher, holder) in enumerate(zip(self.launchers, self.holders)):
             need = any(op.mode != nat.GRAD_NONE for op in launcher.operands)
+            job = side_jobs[0] if side_jobs else None
+            launcher.side = None if job is None else (
+                job.drawn.base.reshape(self.K, job.drawn.N), job.drawn.conc)
             part = self.flags[cursor:cursor + len(launcher.sites)]
             cursor += len(launcher.sites)
             total, site_lp, grads, slot_grad, flags = launcher.run(need, part)
+            if job is not None and launcher.side_out is not None:
+                job.side_dgrad = launcher.side_out
+                side_jobs.pop(0)
+            launcher.side = None
             holder["flags"], holder["site_lp"] = flags, site_lp
             terms.append(total)
             skip = self.skip_ops.get(li, set())

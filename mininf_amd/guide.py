@@ -194,6 +194,7 @@ class Drawn:
     base: torch.Tensor
     N: int
     dgrad: Optional[torch.Tensor] = None   # Beta: mi_beta_dgrad factors [K, N, 2] (side stream)
+    conc: Optional[torch.Tensor] = None    # Beta: the interleaved [N, 2] concentration drawn from
 
 
 # data pointer of a materialised draw -> its record (reset by every draw_all)
@@ -325,7 +326,8 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
             cfg.noise = cfg.noise.to(device=conc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
         x = _BetaRsampleFn.apply(cfg, conc)
-        _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N, _beta_dgrad(x, conc, cfg.K, N))
+        _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N, _beta_dgrad(x, conc, cfg.K, N),
+                                     conc)
         return x.reshape((cfg.K,) + tuple(shape))
     if cfg.noise is not None:
         return cfg.noise

@@ -551,18 +551,23 @@ def _absorb_cases(device, case):
     return cond, approx, 16
 
 
-@pytest.mark.parametrize("case", ["beta_scalar", "beta_scalar_dgrad", "two_factor", "linear",
+@pytest.mark.parametrize("case", ["beta_scalar", "beta_scalar_inline", "beta_scalar_dgrad",
+                                  "two_factor", "linear",
                                   "linear_sigma", "hierarchical", "exp_use"])
 def test_absorbed_draws_match_autograd(device, case, monkeypatch):
     """
     Guide draws whose backward the ELBO kernel absorbs (mi_factor draw_kind: Beta implicit
     gradient, Normal eps regeneration, fused-draw partials; entropy and exp transform folded in)
     against the same step with the draws' backward left to autograd (MININF_AMD_ABSORB=0).
-    Beta: the implicit-gradient factors evaluated inside mi_elbo_forward, or precomputed by
-    mi_beta_dgrad on the side stream (beta_scalar_dgrad, MININF_AMD_BETA_DGRAD=1).
+    Beta: the implicit-gradient factors computed by extra workgroups of the site launch (mi_side,
+    the default), inside mi_elbo_forward (beta_scalar_inline, MININF_AMD_BETA_SIDE=0), or by
+    mi_beta_dgrad on a side stream (beta_scalar_dgrad, MININF_AMD_BETA_DGRAD=1).
     """
     if case == "beta_scalar_dgrad":
         monkeypatch.setenv("MININF_AMD_BETA_DGRAD", "1")
+        case = "beta_scalar"
+    if case == "beta_scalar_inline":
+        monkeypatch.setenv("MININF_AMD_BETA_SIDE", "0")
         case = "beta_scalar"
     cond, approx, K = _absorb_cases(device, case)
 
@@ -633,3 +638,36 @@ def test_fused_beta_guide_matches_torch_construction(device):
     bad.distribution_parameters["concentration1"].data.fill_(float("nan"))
     with pytest.raises(ValueError, match="concentration"):   # Dirichlet's check, as in torch
         bad()
+
+
+@pytest.mark.parametrize("N,K", [(5000, 2048), (3000, 96)])
+def test_bcast_side_job_matches_beta_dgrad(device, N, K):
+    """
+    The Beta implicit-gradient factors carried as extra workgroups of the BCAST site launch
+    (mi_side) are bit-identical to mi_beta_dgrad's, and the site results are unchanged by them.
+    """
+    rng = np.random.default_rng(N)
+    x = (rng.random(N) < 0.6).astype(np.float32)
+    conc = torch.as_tensor([[1.7, 2.6]], dtype=torch.float32, device=device)
+    draws = torch.distributions.Beta(torch.tensor(1.7), torch.tensor(2.6)).sample((K, 1))
+    draws = draws.to(device).contiguous()
+    probs = draws.reshape(K, 1).clone().requires_grad_()
+    base = launch("bernoulli_probs", [probs], torch.as_tensor(x, device=device), device, K=K, N=N)
+
+    views = [engine._View(probs, probs.stride(0), 0),
+             engine._View(torch.as_tensor(x, device=device).reshape(1, -1).expand(K, N), 0, 1)]
+    site = SiteRecord("s", "bernoulli_probs", [], torch.Size([N]), 1.0, None, "bernoulli_probs")
+    launcher = engine._GroupLauncher(K, N, -1.0, device, per_site=True)
+    assert launcher.try_add(site, views, None)
+    launcher.side = (draws, conc)
+    total, _, _, slot, flags = launcher.run(True)
+    torch.cuda.synchronize()
+    assert launcher.side_out is not None, "the BCAST kernel should carry the side job"
+    want = torch.empty((K, 1, 2), dtype=torch.float64, device=device)
+    c = conc.data_ptr()
+    nat.check(nat.lib().mi_beta_dgrad(draws.data_ptr(), c, 2, c + 4, 2, K, 1, want.data_ptr(),
+                                      None), "mi_beta_dgrad")
+    torch.cuda.synchronize()
+    assert torch.equal(launcher.side_out, want)
+    assert torch.equal(total.cpu(), base[0]) and torch.equal(slot.cpu(), base[2])
+    assert int(flags.cpu().max()) == 0
