@@ -188,12 +188,12 @@ def measured_traffic(name):
     correction). None when that config has not been profiled.
     """
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
     if not files:
         return None, None
     with open(files[-1]) as fh:
         entry = json.load(fh).get(name)
-    if entry is None:
+    if entry is None or "traffic_bytes_per_launch" not in entry:
         return None, None
     return entry["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 

@@ -458,22 +458,25 @@ bool use_mfma(const mi_linear* L) {
 }
 
 // Matrix-core launch variants: block size, fp64 carry of the dtheta accumulators across stages,
-// minimum waves per SIMD (register budget). MININF_AMD_LINEAR_TUNE selects one (tuning only).
+// minimum waves per SIMD (register budget). MININF_AMD_LINEAR_TUNE forces one (tuning and tests).
 struct MfVariant {
   int threads;
   bool flush64;
   int minw;
 };
 constexpr MfVariant kMfVariants[] = {{512, true, 1}, {512, false, 1}, {256, false, 1},
-                                     {256, false, 4}};
+                                     {256, false, 4}, {256, true, 2}};
 
-int mf_variant() {
-  static const int v = [] {
+// Default per feature tiles (measured on MI355X, tools/linear_bench.py): one tile (P <= 32) runs
+// variant 3 (256 threads, 4 waves/SIMD, fp32 dtheta accumulators over the block's rows: C3 329 us
+// vs 346 us for variant 0), two tiles variant 4 (256 threads, 2 waves/SIMD: 350 us vs 370 us).
+int mf_variant(int pt) {
+  static const int forced = [] {
     const char* e = getenv("MININF_AMD_LINEAR_TUNE");
-    const int n = e != nullptr ? atoi(e) : 0;
-    return (n >= 0 && n < (int)(sizeof(kMfVariants) / sizeof(kMfVariants[0]))) ? n : 0;
+    const int n = e != nullptr ? atoi(e) : -1;
+    return (n >= 0 && n < (int)(sizeof(kMfVariants) / sizeof(kMfVariants[0]))) ? n : -1;
   }();
-  return v;
+  return forced >= 0 ? forced : (pt == 1 ? 3 : 4);
 }
 
 Geometry geometry(const mi_linear* L) {
@@ -481,10 +484,10 @@ Geometry geometry(const mi_linear* L) {
   g.nv = 1 + (int)L->P + ((L->family == MI_NORMAL && L->scale != nullptr) ? 1 : 0);
   g.mfma = use_mfma(L);
   if (g.mfma) {
-    const MfVariant v = kMfVariants[mf_variant()];
-    const int waves = v.threads / 64;
-    g.variant = mf_variant();
     g.pt = L->P <= 32 ? 1 : 2;
+    g.variant = mf_variant(g.pt);
+    const MfVariant v = kMfVariants[g.variant];
+    const int waves = v.threads / 64;
     const int64_t ptiles = ceil_div(L->K, 32);
     int wt = 1;
     while (wt < waves && wt < ptiles) wt <<= 1;
@@ -538,6 +541,7 @@ void launch_mfma_variant(const mi_linear& L, const Geometry& g, float* part, uin
     case 1: launch_mfma<FAMILY, PT, 512, false, 1>(L, g, part, flags, s); break;
     case 2: launch_mfma<FAMILY, PT, 256, false, 1>(L, g, part, flags, s); break;
     case 3: launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s); break;
+    case 4: launch_mfma<FAMILY, PT, 256, PT == 1, 2>(L, g, part, flags, s); break;
     default: launch_mfma<FAMILY, PT, 512, PT == 1, 1>(L, g, part, flags, s); break;
   }
 }
