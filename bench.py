@@ -234,6 +234,37 @@ def cpu_baseline(name, budget_s=12.0):
             "ms_per_step_extrapolated": 1e3 * elapsed / steps * w["k_local"] / k_cpu}
 
 
+def launch_ranks(n):
+    """
+    Run this command as ``torch.distributed.run --nproc-per-node n`` in a child process (the
+    driver's own launch form) and return its exit status. The parent never touches the GPU.
+    """
+    import socket
+    import subprocess
+    with socket.socket() as sock:
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def check_launch(args, world, rank):
+    """--check-launch: the ranks meet, sum their ranks with one all-reduce, rank 0 prints."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "check_launch": True,
+                          "rank_sum": float(t)}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -249,11 +280,22 @@ def main():
                          "several ranks share one GPU to exercise the sharded path)")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile 20 extra steps and print the hottest host functions to stderr")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="rendezvous and one all-reduce only, no GPU work: prints the line's "
+                         "n_gpus (tests the --gpus launch path on a CPU host)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` on its own: start the N ranks as child processes (one per
+        # GPU) before this process touches the GPU, and exit with their status.
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
+    if args.check_launch:
+        raise SystemExit(check_launch(args, world, rank))
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     group = None
@@ -277,7 +319,8 @@ def main():
     # N > 1: the step is split around the one all-reduce of the gradients -- zero_grad, forward,
     # backward and packing the gradients into a flat bucket (captured), the RCCL all-reduce of the
     # bucket, then Adam on gradients bound to the reduced bucket (captured separately).
-    bucket = GradientBucket(module.parameters(), group) if world > 1 else None
+    # The bucket also carries the rank's loss share, so the one all-reduce yields the global ELBO.
+    bucket = GradientBucket(module.parameters(), group, with_loss=True) if world > 1 else None
 
     def forward_backward():
         optimizer.zero_grad(set_to_none=True)
@@ -286,7 +329,7 @@ def main():
         if world == 1:
             optimizer.step()
         else:
-            bucket.pack()
+            bucket.pack(loss)
         return loss
 
     def apply_update():
@@ -321,6 +364,8 @@ def main():
     def eager_step():
         loss = forward_backward()
         finish_step()
+        if world > 1:
+            return bucket.loss()   # the global loss (sum of the ranks' shares)
         return loss.detach()   # keep no autograd graph alive across steps (graph capture needs it)
 
     # Eager steps: every kernel launched from Python (the kernel timing comes from these).
@@ -343,6 +388,7 @@ def main():
             if world > 1:
                 bucket.all_reduce()
                 update()
+                return bucket.loss()
             return out
 
         for _ in range(args.warmup):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 4
+#define MI_ABI_VERSION 5
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -205,9 +205,12 @@ int mi_group_compile_check(const mi_group* group, char* log, size_t log_bytes);
 int mi_scale_rows(float* x, int64_t stride_k, int64_t stride_i, int64_t K, int64_t N,
                   const float* g, float g0, void* stream);
 
-/* Categorical site: logits[k, i, c] (already normalised, categorical.py:74-78), value int64[i]:
- *   total[k] += scale * sum_i mask_i * logits[k, i, value_i]       (categorical.py:150-156)
- * and, when dlogits != NULL, dlogits[k,i,c] = g0 * scale * mask_i * [c == value_i] (dense). */
+/* Categorical site (replaces Categorical.__init__'s normalisation, categorical.py:74-78, and
+ * log_prob, categorical.py:150-156): logits[k, i, c] raw (or already normalised), value int64:
+ *   total[k] = scale * sum_i mask_i * (logits[k, i, value_i] - logsumexp_c logits[k, i, c])
+ * and, when dlogits != NULL (same strides as logits), every entry is written:
+ *   dlogits[k, i, c] = g0 * scale * mask_i * ([c == value_i] - softmax_c(logits[k, i, :])).
+ * A value outside [0, C) of an observed element sets MI_FLAG_SUPPORT in flags[0]. */
 int mi_categorical_forward(const float* logits, int64_t stride_k, int64_t stride_i,
                            int64_t stride_c, int64_t K, int64_t N, int64_t C,
                            const int64_t* value, int64_t value_stride_k, int64_t value_stride_i,
@@ -411,6 +414,10 @@ typedef struct mi_factor {
   int64_t partial_rows;
   const double* dgrad;          /* Beta, MI_DRAW_SOURCES: mi_beta_dgrad output [K, n, 2], or NULL
                                    to evaluate the implicit gradients in mi_elbo_forward */
+  double* saved;                /* Beta, MI_DRAW_SOURCES: [n, 4] fp64 sums mi_elbo_forward writes
+                                   and mi_elbo_backward of the same evaluation reads (required).
+                                   Owned by the caller per evaluation, so evaluations sharing a
+                                   workspace may interleave (loss1 + loss2, then backward). */
 } mi_factor;
 
 /* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f sum_i H_f(i)

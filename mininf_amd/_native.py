@@ -35,6 +35,7 @@ TRANSFORM_NONE, TRANSFORM_EXP = 0, 1
 DRAW_NONE, DRAW_SOURCES, DRAW_PARTIALS = 0, 1, 2
 MAX_SOURCES = 4
 ELBO_COUNTER_BYTES = 16640
+ABI_VERSION = 5   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -112,7 +113,7 @@ class Factor(ctypes.Structure):
         ("source", Source * MAX_SOURCES), ("draws", c_vp), ("eps", c_vp),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
         ("particle_offset", c_i64), ("partial", c_vp * 2), ("partial_rows", c_i64),
-        ("dgrad", c_vp),
+        ("dgrad", c_vp), ("saved", c_vp),
     ]
 
 
@@ -224,6 +225,11 @@ def lib() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.restype = restype
             fn.argtypes = argtypes
+        target = ctypes.create_string_buffer(16)
+        version = handle.mi_abi_version(target, 16)
+        if version != ABI_VERSION:   # the struct mirrors below would be misread
+            raise NativeError(f"{LIB_PATH} has ABI version {version}, this binding expects "
+                              f"{ABI_VERSION}; rebuild it (mininf_amd/build.py --force).")
         _LIB = handle
     return _LIB
 

@@ -107,7 +107,7 @@ struct AbsorbPlan {
   int64_t rows_per_slice[MI_MAX_FACTORS];
   int64_t counter[MI_MAX_FACTORS];   // first completion counter of the factor's columns
   int64_t partial[MI_MAX_FACTORS];   // offset (doubles) of its [slices, n, 2] partial sums
-  int64_t pre[MI_MAX_FACTORS];       // offset (doubles) of its [n, 4] forward sums, or -1
+  int32_t pre[MI_MAX_FACTORS];       // 1: a Beta factor whose [n, 4] forward sums are in F.saved
 };
 
 // Block-dependent selections from the by-value kernel descriptors, written as unrolled
@@ -221,13 +221,13 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   const int local = bid - pick(P.first, a);
   const int gx = pick(P.gx, a), ti = pick(P.ti, a), slices = pick(P.slices, a);
   const int64_t rows_per_slice = pick(P.rows_per_slice, a);
-  const int64_t pre_offset = pick(P.pre, a);
+  const bool has_pre = pick(P.pre, a) != 0;
   const int col = local % gx, slice = local / gx;
   const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kElboThreads / ti;
   const int64_t i = (int64_t)col * ti + tx;
-  if (!FORWARD && pre_offset >= 0) {   // Beta: sums and entropy derivatives from the forward
+  if (!FORWARD && has_pre) {   // Beta: sums and entropy derivatives from the forward
     if (i < F.n) {
-      const double* pre = work + pre_offset + 4 * i;
+      const double* pre = F.saved + 4 * i;
       write_grad(F, 0, i, (double)u * pre[0] + w * pre[2]);
       write_grad(F, 1, i, (double)u * pre[1] + w * pre[3]);
     }
@@ -274,7 +274,7 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
     double d0, d1;
     entropy_grad(F, i, d0, d1);
     if (FORWARD) {
-      double* pre = work + pre_offset + 4 * i;
+      double* pre = F.saved + 4 * i;
       pre[0] = s0;
       pre[1] = s1;
       pre[2] = d0;
@@ -425,6 +425,10 @@ bool valid_factor(const mi_factor& F) {
   }
 }
 
+bool forward_absorbed(const mi_factor& F) {
+  return F.family == MI_BETA && F.draw_kind == MI_DRAW_SOURCES;
+}
+
 bool valid(const mi_elbo* e) {
   if (e == nullptr || e->K < 1 || e->num_terms < 0 || e->num_terms > MI_MAX_TERMS ||
       e->num_factors < 0 || e->num_factors > MI_MAX_FACTORS || e->num_buffers < 0 ||
@@ -436,6 +440,8 @@ bool valid(const mi_elbo* e) {
     if (!valid_factor(e->factors[f])) return false;
   for (int b = 0; b < e->num_buffers; ++b)
     if (e->buffers[b] == nullptr || e->buffer_len[b] < 0) return false;
+  for (int f = 0; f < e->num_factors; ++f)
+    if (forward_absorbed(e->factors[f]) && e->factors[f].saved == nullptr) return false;
   return true;
 }
 
@@ -451,9 +457,6 @@ int64_t longest_factor(const mi_elbo* e) {
   return n;
 }
 
-bool forward_absorbed(const mi_factor& F) {
-  return F.family == MI_BETA && F.draw_kind == MI_DRAW_SOURCES;
-}
 
 // Counter words (uint32) of the workspace: [0] the forward loss counter, absorbed-draw columns
 // from kCounterFirst on.
@@ -461,7 +464,8 @@ constexpr int64_t kCounterFirst = 64;
 constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned);
 
 // Launch plans of both kernels and the layout of the fp64 work area that follows the counters:
-// [loss partials | forward absorbed partials | Beta pre sums | backward absorbed partials].
+// [loss partials | forward absorbed partials | backward absorbed partials]. All of it is scratch
+// of one launch; what the backward needs from the forward lives in the caller's mi_factor.saved.
 struct Layout {
   mi::AbsorbPlan fwd, bwd;
   int64_t doubles;
@@ -473,7 +477,7 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, mi::AbsorbPlan& P, int6
   const int a = P.num++;
   P.index[a] = f;
   P.first[a] = blocks;
-  P.pre[a] = -1;
+  P.pre[a] = 0;
   if (!forward && forward_absorbed(F)) {   // finish only: one element per thread
     P.ti[a] = mi::kElboThreads;
     P.gx[a] = (int)ceil_div(F.n, mi::kElboThreads);
@@ -523,10 +527,7 @@ Layout make_layout(const mi_elbo* e) {
     if (forward_absorbed(e->factors[f]))
       add_absorbed(e, f, true, L.fwd, counters, doubles, blocks);
   L.fwd.first[L.fwd.num] = blocks;
-  for (int a = 0; a < L.fwd.num; ++a) {   // the forward's results, read by the backward
-    L.fwd.pre[a] = doubles;
-    doubles += 4 * e->factors[L.fwd.index[a]].n;
-  }
+  for (int a = 0; a < L.fwd.num; ++a) L.fwd.pre[a] = 1;   // writes F.saved
   blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind != MI_DRAW_NONE) {

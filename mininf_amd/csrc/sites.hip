@@ -842,7 +842,12 @@ __global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ x, int64
 }
 
 // -------------------------------------------------------------------------------------------------
-// Categorical (gather of normalised logits), lanes along elements.
+// Categorical: normalisation (categorical.py:74-78, logits - logsumexp) and gather
+// (categorical.py:150-156) of one (particle, element) row per lane, lanes along elements. The row's
+// C logits are read twice (max, then the exponentials; the second pass hits L1/L2). Gradient with
+// respect to the given logits, dense: g * (onehot(v) - softmax) -- exact for raw logits, and for
+// already normalised ones (whose logsumexp is 0) the same vector autograd's normalisation backward
+// passes through unchanged.
 // -------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_categorical(
     const float* __restrict__ logits, int64_t sk, int64_t si, int64_t sc, int64_t K, int64_t N,
@@ -857,15 +862,30 @@ __global__ __launch_bounds__(256) void k_categorical(
     float acc = 0.0f;
     for (int e = 0; e < 16; ++e) {
       const int64_t i = seg * 1024 + e * 64 + lane;
-      if (i < N) {
-        const bool obs = mask == nullptr || mask[i * msi] != 0;
-        const int64_t v = value[k * vsk + i * vsi];
-        const bool ok = v >= 0 && v < C;
-        fl |= (obs && !ok) ? MI_FLAG_SUPPORT : 0u;
-        if (obs && ok) {
-          const int64_t off = k * sk + i * si + v * sc;
-          acc += logits[off];
-          if (dlogits != nullptr) dlogits[off] = gscale;
+      if (i >= N) break;
+      const bool obs = mask == nullptr || mask[i * msi] != 0;
+      const int64_t v = value[k * vsk + i * vsi];
+      const bool ok = v >= 0 && v < C;
+      fl |= (obs && !ok) ? MI_FLAG_SUPPORT : 0u;
+      const float* row = logits + k * sk + i * si;
+      float* drow = dlogits == nullptr ? nullptr : dlogits + k * sk + i * si;
+      if (!(obs && ok)) {   // masked lanes: value and gradient 0 (util.py:85-90)
+        if (drow != nullptr)
+          for (int64_t c = 0; c < C; ++c) drow[c * sc] = 0.0f;
+        continue;
+      }
+      float mx = -INFINITY;
+      for (int64_t c = 0; c < C; ++c) mx = fmaxf(mx, row[c * sc]);
+      const float shift = isinf(mx) ? 0.0f : mx;   // torch.logsumexp's all--inf guard
+      float se = 0.0f;
+      for (int64_t c = 0; c < C; ++c) se += expf(row[c * sc] - shift);
+      const float lse = logf(se) + shift;
+      acc += row[v * sc] - lse;
+      if (drow != nullptr) {
+        const float inv = 1.0f / se;
+        for (int64_t c = 0; c < C; ++c) {
+          const float soft = expf(row[c * sc] - shift) * inv;
+          drow[c * sc] = gscale * ((c == v ? 1.0f : 0.0f) - soft);
         }
       }
     }

@@ -56,11 +56,16 @@ class GradientBucket:
     gradients with ``zero_grad(set_to_none=True)`` before each backward, so that the backward
     does not accumulate into the bound views.
 
+    With ``with_loss`` the buffer carries one more element, the rank's loss share (``pack(loss)``),
+    so the same single all-reduce also yields the global loss (:meth:`loss`).
+
     Args:
         parameters: The parameters whose gradients to reduce (all of them must receive one).
         group: Process group (default: the world).
+        with_loss: Reserve the loss element.
     """
-    def __init__(self, parameters: Iterable[torch.nn.Parameter], group=None) -> None:
+    def __init__(self, parameters: Iterable[torch.nn.Parameter], group=None,
+                 with_loss: bool = False) -> None:
         self.params = [p for p in parameters if p.requires_grad]
         if not self.params:
             raise ValueError("no parameters to reduce")
@@ -68,22 +73,33 @@ class GradientBucket:
         if len(dtypes) != 1:
             raise ValueError(f"parameters of one dtype expected, got {dtypes}")
         self.group = group
-        self.flat = torch.zeros(sum(p.numel() for p in self.params), dtype=dtypes.pop(),
-                                device=self.params[0].device)
+        self.with_loss = with_loss
+        self.flat = torch.zeros(sum(p.numel() for p in self.params) + int(with_loss),
+                                dtype=dtypes.pop(), device=self.params[0].device)
         self.views = []
         offset = 0
         for p in self.params:
             self.views.append(self.flat[offset:offset + p.numel()].view_as(p))
             offset += p.numel()
 
-    def pack(self) -> None:
-        """Copy this rank's gradients into the flat buffer."""
+    def pack(self, loss: Optional[torch.Tensor] = None) -> None:
+        """Copy this rank's gradients (and loss share, with ``with_loss``) into the flat buffer."""
         grads = []
         for p in self.params:
             if p.grad is None:
                 raise RuntimeError("a parameter of the bucket has no gradient")
             grads.append(p.grad.reshape(-1))
+        if self.with_loss:
+            if loss is None:
+                raise ValueError("this bucket carries the loss: pack(loss)")
+            grads.append(loss.detach().reshape(1).to(self.flat.dtype))
         torch.cat(grads, out=self.flat)
+
+    def loss(self) -> torch.Tensor:
+        """The loss element (after :meth:`all_reduce`: the global loss)."""
+        if not self.with_loss:
+            raise ValueError("this bucket does not carry the loss")
+        return self.flat[-1]
 
     def all_reduce(self) -> None:
         """Sum the flat buffer over the ranks (in place)."""

@@ -449,7 +449,7 @@ def _run_categorical(site: SiteRecord, g0: float, logits: torch.Tensor, value: t
     """
     K, N, C = logits.shape
     device = logits.device
-    dlogits = torch.zeros_like(logits) if need else None
+    dlogits = torch.empty_like(logits) if need else None   # every entry written
     size = ctypes.c_size_t()
     lib = nat.lib()
     nat.check(lib.mi_categorical_workspace_bytes(K, N, ctypes.byref(size)),
@@ -658,6 +658,7 @@ class LogJoint:
     pending: List[Tuple[str, dict, List[SiteRecord]]]
     checks: list
     flags: Optional[torch.Tensor] = None      # int32, one word per pending site, in order
+    sticky: bool = False                      # flags are never zeroed by a replay (graph mode)
 
     def flag_vector(self) -> Optional[torch.Tensor]:
         """
@@ -842,6 +843,7 @@ class _Absorbed:
     drawn: Optional[guide.Drawn] = None
     lazy: Optional[guide.LazyDraw] = None
     side_dgrad: Optional[torch.Tensor] = None   # Beta factors computed by a site launch (mi_side)
+    saved: Optional[torch.Tensor] = None        # Beta: [n, 4] fp64 forward sums (mi_factor.saved)
 
 
 _FACTOR_PARAMS = {nat.NORMAL: ("loc", "scale"), nat.BETA: ("concentration1", "concentration0")}
@@ -992,6 +994,9 @@ def plan_absorption(factors: List[EntropyFactor], samples: Optional[Dict[str, to
 
 
 _ELBO_WORKSPACE: Dict[Tuple[str, int], torch.Tensor] = {}
+# workspaces replaced by a larger one: a captured hipGraph may still hold their addresses, so they
+# are never freed
+_ELBO_RETIRED: List[torch.Tensor] = []
 
 
 def _elbo_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -1003,6 +1008,8 @@ def _elbo_workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
     ws = _ELBO_WORKSPACE.get(key)
     if ws is None or ws.numel() < nbytes:
+        if ws is not None:
+            _ELBO_RETIRED.append(ws)
         ws = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
         nat.check(nat.lib().mi_elbo_workspace_init(ws.data_ptr(), ws.numel(),
                                                    nat.stream_handle(device)),
@@ -1117,6 +1124,10 @@ class _ElboPlan:
                 continue
             cfg = plan.drawn.cfg
             if f.family == nat.BETA:
+                # the forward's per-element sums for this evaluation's backward, owned by the
+                # plan so that interleaved evaluations never share them
+                plan.saved = torch.empty(4 * f.n, dtype=torch.float64, device=self.device)
+                d.saved = plan.saved.data_ptr()
                 d.draws = plan.drawn.base.data_ptr()
                 d.dgrad = nat.ptr(plan.side_dgrad if plan.side_dgrad is not None
                                   else plan.drawn.dgrad)

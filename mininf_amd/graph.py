@@ -13,9 +13,10 @@ What makes the ELBO capturable:
 * the guide generator reads its step counter from device memory (``mi_*_rsample`` ``step_device``),
   and the loss increments that word on the device, so every replay draws fresh particles;
 * inside :func:`graph_safe` the engine does not synchronise to raise validation errors: the
-  per-site flag words are gathered on the device by the graph, copied to pinned host memory after
-  each replay, and checked once that replay has finished (:meth:`StepGraph.check`, or non-blockingly before the next
-  replay) -- errors are raised with the reference's messages, at most one step late;
+  per-site flag words are accumulated on the device (never cleared by a replay, so a violation in
+  any replay persists), copied to pinned host memory after each replay, and checked once that
+  replay has finished (:meth:`StepGraph.check`, or non-blockingly before the next replay) --
+  errors are raised with the reference's messages, a few steps late at most, and never lost;
 * ``torch.distributions`` argument validation (a host sync per check) is off inside the captured
   region; the site kernels' MI_FLAG_PARAM checks cover the model's parameters;
 * while capturing, ``torch.distributions``' ``broadcast_all`` turns Python numbers into device
@@ -113,6 +114,7 @@ class StepGraph:
         self.step = step
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        count = 0
         with torch.cuda.stream(side):
             for _ in range(max(1, warmup)):
                 collector: List = []
@@ -120,7 +122,14 @@ class StepGraph:
                     step()
                 for joint in collector:
                     joint.raise_on_violation()
+                count = sum(joint.flag_count() for joint in collector)
         torch.cuda.current_stream().wait_stream(side)
+        # Validation results must survive replays the host does not inspect: the step's words are
+        # OR-ed into this accumulator by the graph itself (allocated and zeroed outside the capture)
+        # unless the step's only flags already are never-zeroed words (EvidenceLowerBoundLoss in
+        # graph mode), which then serve as the accumulator without an extra node.
+        self._accumulator = torch.zeros(max(1, count), dtype=torch.int64,
+                                        device=torch.cuda.current_device())
         torch.cuda.synchronize()
 
         self.graph = torch.cuda.CUDAGraph()
@@ -130,9 +139,21 @@ class StepGraph:
             self.output = step()
             flags = [joint.flag_vector() for joint in self._joints]
             flags = [f for f in flags if f is not None]
-            if len(flags) > 1:
-                flags = [torch.cat([f.to(torch.int64) for f in flags])]
-            self._flags_device = flags[0] if flags else None
+            if len(self._joints) == 1 and flags and self._joints[0].sticky and \
+                    flags[0] is self._joints[0].flags:
+                self._flags_device = flags[0]
+                self._accumulator = None
+            elif flags:
+                vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
+                    else flags[0]
+                if vector.numel() != count:
+                    raise RuntimeError(f"the captured step has {vector.numel()} validation words, "
+                                       f"its warm-up steps {count}")
+                self._accumulator.bitwise_or_(vector)
+                self._flags_device = self._accumulator
+            else:
+                self._flags_device = None
+                self._accumulator = None
         # Pinned host memory cannot be allocated while capturing: the copy of the flags is enqueued
         # after each replay instead (one small asynchronous D2H copy).
         self._flags_host = None
@@ -166,6 +187,9 @@ class StepGraph:
             return
         self._pending = False
         values = self._flags_host.tolist()
+        if any(values):   # raising: clear the accumulated words for a caller that carries on
+            self._done.synchronize()
+            self._flags_device.zero_()
         cursor = 0
         for joint in self._joints:
             count = joint.flag_count()

@@ -249,6 +249,7 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.validate = validate
         self.process_group = process_group
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
+        self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
 
     # validation words zeroed with the step counter's advance; plans with more sites zero their own
     FLAG_WORDS = 64
@@ -282,12 +283,23 @@ class EvidenceLowerBoundLoss(nn.Module):
             # The draws (and their regeneration in backward) use a snapshot of the device counter,
             # which is advanced on the device -- replays of a captured step draw anew -- by the
             # same launch that zeroes the call's validation words (mi_step_begin).
+            sticky = False
             if device.type == "cuda":
                 step = torch.empty(1, dtype=torch.int64, device=device)
-                flags = torch.empty(self.FLAG_WORDS, dtype=torch.int32, device=device)
+                if graph.deferred() is not None:
+                    # Graph mode: validation words that no replay zeroes. Violations accumulate
+                    # until the host reads them (StepGraph), so a replay that the host never
+                    # inspects cannot lose one; StepGraph clears them when it raises.
+                    if self._sticky_flags is None or self._sticky_flags.device != device:
+                        self._sticky_flags = torch.zeros(self.FLAG_WORDS, dtype=torch.int32,
+                                                         device=device)
+                    flags, zero, sticky = self._sticky_flags, 0, True
+                else:
+                    flags = torch.empty(self.FLAG_WORDS, dtype=torch.int32, device=device)
+                    zero = self.FLAG_WORDS
                 _native.check(_native.lib().mi_step_begin(
                     self._counter.data_ptr(), step.data_ptr(), flags.data_ptr(),
-                    self.FLAG_WORDS, _native.stream_handle(device)), "mi_step_begin")
+                    zero, _native.stream_handle(device)), "mi_step_begin")
             else:   # the samplers reject host guides with the engine's device error
                 step, flags = self._counter.clone(), None
                 self._counter.add_(1)
@@ -319,6 +331,8 @@ class EvidenceLowerBoundLoss(nn.Module):
             try:
                 loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples,
                                           flags=flags)
+                joint.sticky = sticky and joint.flags is not None and not joint.checks and \
+                    joint.flags.data_ptr() == flags.data_ptr()
             finally:
                 # The placeholder registry is only needed while tracing and planning; holding it
                 # would keep this step's autograd graph (and its AccumulateGrad streams) alive.

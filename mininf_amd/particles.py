@@ -274,6 +274,11 @@ class ParticleTracer(TracerMixin):
 
         declared = batch.get_shape()
         family, params = classify(distribution)
+        if family == "categorical" and self._validate_parameters and \
+                torch.is_floating_point(data):
+            # The kernel reads int64 values and checks only the range; fractional or NaN values
+            # (integer_interval's `value % 1 == 0`, constraints.py) are checked here (memoised).
+            self._check_support(name, value, distribution, cast(Constraint, distribution.support))
         if family == "categorical":
             shape = torch.broadcast_shapes(tuple(data.shape), distribution.batch_shape)
         elif family != "torch":

@@ -99,3 +99,75 @@ def hierarchical_masked_elbo(y, b, mask, mu_loc, mu_scale, z_loc, z_scale, eps_m
     out["grad_z_loc"] = -dT_z.mean(0)
     out["grad_z_scale"] = (-(dT_z * eps_z).mean(0) - 1.0 / z_scale) * z_scale
     return out
+
+
+def categorical_masked_elbo(y, mask, loc, scale, eps):
+    """
+    Categorical model (no reference test or example; SURVEY.md A11): theta ~ N(0, 1)[C];
+    y ~ Categorical(logits=theta)[n] masked (torch categorical.py:74-78 normalisation,
+    150-156 gather; masked sum core.py:262-265). Guide MF Normal(loc, scale)[C], eps [K, C].
+    """
+    y, m = np.asarray(y, np.int64), _f64(mask)
+    loc, scale, eps = (_f64(a) for a in (loc, scale, eps))
+    K, C = eps.shape
+    theta = _f64(np.float32(loc) + np.float32(eps) * np.float32(scale))       # [K, C]
+    lse = special.logsumexp(theta, axis=1, keepdims=True)
+    norm = theta - lse
+    counts = np.bincount(y, weights=m, minlength=C)[:C]                         # [C]
+    T = (-0.5 * theta ** 2 - lpf.HALF_LOG_2PI).sum(1) + norm @ counts
+    H = (0.5 + lpf.HALF_LOG_2PI + np.log(scale)).sum()
+    loss = -(T.mean() + H)
+    dT = -theta + counts[None, :] - m.sum() * np.exp(norm)
+    grad_loc = -dT.mean(0)
+    grad_scale = -(dT * eps).mean(0) - 1.0 / scale
+    return {"loss": float(loss), "T": T, "grad_loc": grad_loc, "grad_u_scale": grad_scale * scale}
+
+
+def regression_elbo_gram(G, Xty, yty, n, loc, scale, eps, batch_scale=1.0):
+    """
+    ``regression_elbo`` through the data's sufficient statistics G = X^T X, X^T y, y^T y (fp64),
+    for full-size checks: sum_i (y_i - x_i theta)^2 = y^T y - 2 theta^T X^T y + theta^T G theta.
+    """
+    G, Xty, loc, scale, eps = (_f64(a) for a in (G, Xty, loc, scale, eps))
+    K = eps.shape[0]
+    theta = _f64(np.float32(loc) + np.float32(eps) * np.float32(scale))
+    rss = float(yty) - 2.0 * theta @ Xty + np.einsum("kp,pq,kq->k", theta, G, theta)
+    lp_prior = (-0.5 * theta ** 2 - lpf.HALF_LOG_2PI).sum(1)
+    lp_y = batch_scale * (-0.5 * rss - n * lpf.HALF_LOG_2PI)
+    T = lp_prior + lp_y
+    H = (0.5 + lpf.HALF_LOG_2PI + np.log(scale)).sum()
+    loss = -(T.mean() + H)
+    dT = -theta + batch_scale * (Xty[None, :] - theta @ G)
+    grad_loc = -dT.mean(0)
+    grad_scale = -(dT * eps).mean(0) - 1.0 / scale
+    return {"loss": float(loss), "T": T, "grad_loc": grad_loc, "grad_u_scale": grad_scale * scale}
+
+
+def hierarchical_masked_elbo_chunked(y, b, mask, mu_loc, mu_scale, z_loc, z_scale, eps_mu,
+                                     eps_z_rows, K, chunk=16, y_scale=0.5):
+    """
+    ``hierarchical_masked_elbo`` over K particles taken ``chunk`` at a time (full-size checks):
+    ``eps_z_rows(k0, k1)`` returns the z noise of particles [k0, k1). Loss and gradients are
+    particle means, so the chunks combine with weights k1 - k0.
+    """
+    eps_mu = _f64(eps_mu)
+    T = []
+    acc = {"grad_mu_loc": 0.0, "grad_mu_scale": 0.0, "grad_z_loc": 0.0, "grad_z_scale": 0.0}
+    z_scale64 = _f64(z_scale)
+    for k0 in range(0, K, chunk):
+        k1 = min(K, k0 + chunk)
+        part = hierarchical_masked_elbo(y, b, mask, mu_loc, mu_scale, z_loc, z_scale,
+                                        eps_mu[k0:k1], eps_z_rows(k0, k1), y_scale)
+        w = (k1 - k0) / K
+        T.append(part["T"])
+        # undo the entropy terms (added once below) before weighting the particle means
+        acc["grad_mu_loc"] += w * part["grad_mu_loc"]
+        acc["grad_mu_scale"] += w * (part["grad_mu_scale"] + 1.0)
+        acc["grad_z_loc"] = acc["grad_z_loc"] + w * part["grad_z_loc"]
+        acc["grad_z_scale"] = acc["grad_z_scale"] + w * (part["grad_z_scale"] + 1.0)
+    T = np.concatenate(T)
+    H = (0.5 + lpf.HALF_LOG_2PI + np.log(float(mu_scale))) + \
+        (0.5 + lpf.HALF_LOG_2PI + np.log(z_scale64)).sum()
+    acc["grad_mu_scale"] -= 1.0
+    acc["grad_z_scale"] = acc["grad_z_scale"] - 1.0
+    return {"loss": float(-(T.mean() + H)), "T": T, **acc}

@@ -22,3 +22,28 @@ def test_measured_traffic_reads_the_pmc_summary():
         assert traffic is not None and traffic > 0, cfg
         assert source.startswith("profiles/r") and source.endswith("_pmc.json")
     assert bench.measured_traffic("c1") == (None, None)
+
+
+def _bench(*argv, env_extra=None):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_bench_gpus_flag_starts_that_many_ranks():
+    """`bench.py --gpus 2` on its own starts two ranks (torch.distributed.run child process) and
+    the line reports n_gpus 2 (--gpus was ignored)."""
+    import json
+    out = _bench("--gpus", "2", "--dist-backend", "gloo", "--check-launch")
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["rank_sum"] == 1.0
+
+
+def test_bench_rejects_a_world_size_mismatch():
+    out = _bench("--gpus", "4", "--check-launch", env_extra={"WORLD_SIZE": "2", "RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr

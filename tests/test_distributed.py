@@ -97,6 +97,17 @@ def bucket_worker(rank, world, port, queue):
             ((rank + 1) * (a.square().sum() + step * b * a.sum())).backward()
             all_reduce_gradients([a, b], dist.group.WORLD)
             out.append([torch.equal(x, y) for x, y in zip(got, [a.grad, b.grad])])
+        # the loss share rides in the same flat buffer: one all-reduce gives the global loss
+        lossy = GradientBucket([a, b], dist.group.WORLD, with_loss=True)
+        for p in (a, b):
+            p.grad = None
+        share = (rank + 1) * (a.square().sum() + b)
+        share.backward()
+        lossy.pack(share)
+        lossy.all_reduce()
+        lossy.bind()
+        want = 3 * (a.detach().square().sum() + b.detach())   # ranks 0 and 1: (1 + 2) * ...
+        out.append([torch.allclose(lossy.loss(), want), torch.equal(a.grad, 6 * a.detach())])
         queue.put((rank, out))
     finally:
         dist.destroy_process_group()

@@ -149,3 +149,59 @@ def test_graph_replays_fused_guide_draws(device):
     torch.testing.assert_close(torch.tensor(replays), torch.tensor(eager[2:]), rtol=1e-6, atol=0)
     for a, b in zip(eager_approx.parameters(), graph_approx.parameters()):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("family", ["bernoulli_linear", "bernoulli_group"])
+@pytest.mark.parametrize("host_looks", [True, False], ids=["polling", "unpolled"])
+def test_graph_never_loses_a_transient_violation(device, family, host_looks):
+    """
+    A rotating device-resident minibatch (C4 shape) where exactly one window holds a value outside
+    the Bernoulli support (2.0), replayed without ever blocking: the violation of that one replay
+    must still be raised, with the reference's message (core.py:186-188), even though later
+    replays evaluate valid windows (sticky validation words).
+    """
+    n_total, B, p, K = 4096, 256, 8, 32
+    windows = n_total // B
+    gen = torch.Generator().manual_seed(1)
+    X = torch.randn(n_total, p, generator=gen).to(device)
+    y = (torch.rand(n_total, generator=gen) < 0.5).float().to(device)
+    y[5 * B + 17] = 2.0               # window 5 only
+    counter = torch.zeros(1, dtype=torch.int64, device=device)
+    offsets = torch.arange(B, device=device)
+
+    def model():
+        theta = mi.sample("theta", Normal(0, 1), sample_shape=p)
+        if family == "bernoulli_linear":
+            Xb = mi.sample("X", Normal(0, 1), sample_shape=(B, p))
+            mi.sample("y", Bernoulli(logits=Xb @ theta))
+        else:
+            mi.sample("y", Bernoulli(logits=theta.sum()), sample_shape=[B])
+
+    module = mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(p),
+                                             scale=torch.ones(p)).to(device)
+    optimizer = torch.optim.Adam(module.parameters(), lr=0.01, capturable=True)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=3)
+
+    def step():
+        optimizer.zero_grad(set_to_none=True)
+        rows = (counter % windows) * B + offsets
+        counter.add_(1)
+        data = dict(y=y.index_select(0, rows))
+        if family == "bernoulli_linear":
+            data["X"] = X.index_select(0, rows)
+        loss = loss_fn(mi.condition(model, **data), {"theta": module()})
+        loss.backward()
+        optimizer.step()
+        return loss
+
+    captured = StepGraph(step, warmup=2)   # windows 0, 1 (eager); capture executes nothing
+    poll = captured._check
+    if not host_looks:   # the host never inspects a replay before the last one
+        captured._check = lambda block: None
+    with pytest.raises(ValueError, match="is not in the support"):
+        for _ in range(windows - 3):       # replays see windows 2 .. 14: window 5 once
+            captured()
+        captured._check = poll
+        captured.check()
+    captured()                             # cleared after raising: valid windows pass again
+    captured.check()

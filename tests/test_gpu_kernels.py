@@ -671,3 +671,164 @@ def test_bcast_side_job_matches_beta_dgrad(device, N, K):
     assert torch.equal(launcher.side_out, want)
     assert torch.equal(total.cpu(), base[0]) and torch.equal(slot.cpu(), base[2])
     assert int(flags.cpu().max()) == 0
+
+
+def test_interleaved_beta_elbos_keep_their_own_sums(device):
+    """
+    Two ELBO evaluations with absorbed Beta draws before one backward (loss1 + loss2, gradient
+    accumulation, a logging ELBO mid-step): each evaluation's forward sums (mi_factor.saved) stay
+    its own, also when the second needs a larger ELBO workspace than the first.
+    Gradients equal those of separate backwards.
+    """
+    rng = np.random.default_rng(5)
+    n, nv = 5000, 3000
+    x = torch.as_tensor((rng.random(n) < 0.7).astype(np.float32), device=device)
+    xv = torch.as_tensor((rng.random((nv,)) < 0.4).astype(np.float32), device=device)
+
+    def scalar_model():
+        theta = mi.sample("theta", Beta(2.0, 2.0))
+        mi.sample("x", Bernoulli(theta), sample_shape=[n])
+
+    def vector_model():   # per-element Beta guide: more blocks, more workspace
+        theta = mi.sample("theta", Beta(2.0, 2.0), sample_shape=[nv])
+        mi.sample("x", Bernoulli(theta))
+
+    a1 = mi.nn.ParameterizedFactorizedDistribution(
+        theta=mi.nn.ParameterizedDistribution(Beta, concentration1=1.7, concentration0=2.6)
+    ).to(device)
+    a2 = mi.nn.ParameterizedFactorizedDistribution(
+        theta=mi.nn.ParameterizedDistribution(Beta, concentration1=torch.full((nv,), 1.2),
+                                              concentration0=torch.full((nv,), 3.1))).to(device)
+    c1, c2 = mi.condition(scalar_model, x=x), mi.condition(vector_model, x=xv)
+
+    def losses():
+        l1 = mi.nn.EvidenceLowerBoundLoss(num_particles=2048, seed=3)(c1, a1())
+        l2 = mi.nn.EvidenceLowerBoundLoss(num_particles=64, seed=4)(c2, a2())
+        l3 = mi.nn.EvidenceLowerBoundLoss(num_particles=512, seed=5)(c1, a1())
+        return l1, l2, l3
+
+    def grads():
+        out = {f"a1.{k}": q.grad.detach().clone() for k, q in a1.named_parameters()}
+        out.update({f"a2.{k}": q.grad.detach().clone() for k, q in a2.named_parameters()})
+        for q in list(a1.parameters()) + list(a2.parameters()):
+            q.grad = None
+        return out
+
+    for l in losses():   # separate forward/backward pairs
+        l.backward()
+    separate = grads()
+    l1, l2, l3 = losses()   # all forwards first, then one backward
+    (l1 + l2 + l3).backward()
+    joint = grads()
+    for name in separate:
+        torch.testing.assert_close(joint[name], separate[name], rtol=1e-6, atol=1e-7)
+
+
+def _categorical_abi(logits, value, device, mask=None, scale=1.0, g0=-1.0):
+    """mi_categorical_forward on [K, N, C] logits: (total [K], dlogits [K, N, C], flags)."""
+    K, N, C = logits.shape
+    lib = nat.lib()
+    size = ctypes.c_size_t()
+    assert lib.mi_categorical_workspace_bytes(K, N, ctypes.byref(size)) == 0
+    ws = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+    total = torch.empty(K, dtype=torch.float32, device=device)
+    dlogits = torch.full_like(logits, float("nan"))   # every entry must be written
+    flags = torch.empty(1, dtype=torch.int32, device=device)
+    nat.check(lib.mi_categorical_forward(
+        logits.data_ptr(), *logits.stride(), K, N, C, value.data_ptr(), *value.stride(),
+        None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(0),
+        scale, g0, dlogits.data_ptr(), ws.data_ptr(), size.value, total.data_ptr(),
+        flags.data_ptr(), None), "mi_categorical_forward")
+    torch.cuda.synchronize()
+    return total.cpu(), dlogits.cpu(), int(flags.cpu()[0])
+
+
+@pytest.mark.parametrize("mode", ["particle", "dense"])
+def test_categorical_kernel_against_golden(device, mode):
+    """
+    k_categorical on the reference's raw logits (golden families.npz, torch Categorical(logits=.)
+    .log_prob and its autograd, categorical.py:74-78, 150-156): the kernel normalises, gathers and
+    writes g0 * (onehot - softmax), the gradient with respect to the raw logits.
+    """
+    f = golden("families.npz")
+    raw = torch.as_tensor(f["cat_logits"], device=device)            # [6, 5]
+    v = torch.as_tensor(f["cat_v"], device=device)
+    if mode == "particle":   # six particles, one element each
+        logits, value = raw.reshape(6, 1, 5).contiguous(), v.reshape(6, 1).contiguous()
+    else:                    # one particle, six elements
+        logits, value = raw.reshape(1, 6, 5).contiguous(), v.reshape(1, 6).contiguous()
+    total, dlogits, flags = _categorical_abi(logits, value, device)
+    assert flags == 0
+    want = f["cat_lp"] if mode == "particle" else np.array([f["cat_lp"].sum()])
+    np.testing.assert_allclose(total.numpy(), want, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(-dlogits.reshape(6, 5).numpy(), f["cat_dlogits"], rtol=1e-5,
+                               atol=1e-6)
+
+
+def test_categorical_kernel_mask_and_support(device):
+    """Masked rows contribute 0 to value and gradient (util.py:85-90); an observed value outside
+    [0, C) sets the support flag, a masked one does not."""
+    rng = np.random.default_rng(3)
+    K, N, C = 3, 2000, 7
+    logits = torch.as_tensor(rng.normal(size=(K, N, C)).astype(np.float32), device=device)
+    v = rng.integers(0, C, size=N)
+    mask = rng.random(N) > 0.3
+    value = torch.as_tensor(v, device=device).reshape(1, N).expand(K, N)
+    m = torch.as_tensor(mask.astype(np.uint8), device=device)
+    total, dlogits, flags = _categorical_abi(logits, value, device, mask=m, scale=2.5, g0=-0.5)
+    assert flags == 0
+    lp, dl = lpf.categorical(logits.cpu().numpy(), np.broadcast_to(v, (K, N)))
+    np.testing.assert_allclose(total.numpy(), 2.5 * (lp * mask).sum(1), rtol=1e-5)
+    np.testing.assert_allclose(dlogits.numpy(), -1.25 * dl * mask[None, :, None], rtol=1e-5,
+                               atol=1e-6)
+    bad = v.copy()
+    bad[np.flatnonzero(~mask)[0]] = C          # masked: ignored
+    _, _, flags = _categorical_abi(logits, torch.as_tensor(bad, device=device).reshape(1, N)
+                                   .expand(K, N), device, mask=m)
+    assert flags == 0
+    bad[np.flatnonzero(mask)[0]] = -1          # observed: flagged
+    _, _, flags = _categorical_abi(logits, torch.as_tensor(bad, device=device).reshape(1, N)
+                                   .expand(K, N), device, mask=m)
+    assert flags & nat.FLAG_SUPPORT
+
+
+@pytest.mark.parametrize("float_values", [False, True])
+def test_categorical_model_against_oracle(device, float_values):
+    """
+    A masked K-particle Categorical model through EvidenceLowerBoundLoss (mi_categorical_forward,
+    injected Normal noise) against the fp64 oracle at 1e-5; fractional values raise the reference's
+    support error (integer_interval, core.py:186-188) instead of being truncated.
+    """
+    from torch.distributions import Categorical
+    rng = np.random.default_rng(8)
+    n, C, K = 3000, 6, 32
+    y = rng.integers(0, C, size=n)
+    mask = rng.random(n) > 0.2
+    yt = torch.as_tensor(y.astype(np.float32) if float_values else y, device=device)
+    obs = torch.masked.as_masked_tensor(yt, torch.as_tensor(mask, device=device))
+
+    def model():
+        theta = mi.sample("theta", Normal(0.0, 1.0), sample_shape=[C])
+        mi.sample("y", Categorical(logits=theta), sample_shape=[n])
+
+    loc = rng.normal(size=C).astype(np.float32) * 0.3
+    scale = np.full(C, 0.4, np.float32)
+    approx = mi.nn.ParameterizedFactorizedDistribution(theta=mi.nn.ParameterizedDistribution(
+        Normal, loc=torch.as_tensor(loc), scale=torch.as_tensor(scale))).to(device)
+    eps = rng.normal(size=(K, C)).astype(np.float32)
+    loss = mi.nn.EvidenceLowerBoundLoss(num_particles=K)(
+        mi.condition(model, y=obs), approx(), _noise={"theta": torch.as_tensor(eps, device=device)})
+    loss.backward()
+    ref = oracle.categorical_masked_elbo(y, mask, loc, scale, eps)
+    assert abs(float(loss) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    params = approx["theta"].distribution_parameters
+    np.testing.assert_allclose(params["loc"].grad.cpu().numpy(), ref["grad_loc"], rtol=1e-5,
+                               atol=1e-5 * np.abs(ref["grad_loc"]).max())
+    np.testing.assert_allclose(params["scale"].grad.cpu().numpy(), ref["grad_u_scale"], rtol=1e-5,
+                               atol=1e-5 * np.abs(ref["grad_u_scale"]).max())
+    frac = yt.clone()
+    if float_values:
+        frac[np.flatnonzero(mask)[0]] = 1.5
+        bad = torch.masked.as_masked_tensor(frac, torch.as_tensor(mask, device=device))
+        with pytest.raises(ValueError, match="is not in the support"):
+            mi.nn.EvidenceLowerBoundLoss(num_particles=K)(mi.condition(model, y=bad), approx())

@@ -131,3 +131,30 @@ def test_cpu_port_matches_fixture():
                 return self.loc + _eps * self.scale
         losses.append(float(cpu_port.single_draw_loss(conditioned, {"theta": Injected(loc, scale)})))
     assert rel(np.mean(losses), g["loss"]) < RTOL
+
+
+def test_gram_and_chunked_oracles_match_direct_forms():
+    """The full-size oracle forms (sufficient statistics, particle chunks) equal the direct ones."""
+    rng = np.random.default_rng(4)
+    n, p, K = 500, 6, 9
+    X = rng.normal(size=(n, p)).astype(np.float32)
+    y = (X @ rng.normal(size=p) + rng.normal(size=n)).astype(np.float32)
+    loc, scale = rng.normal(size=p).astype(np.float32), np.full(p, 0.3, np.float32)
+    eps = rng.normal(size=(K, p)).astype(np.float32)
+    X64, y64 = X.astype(np.float64), y.astype(np.float64)
+    a = elbo.regression_elbo(X, y, loc, scale, eps, batch_scale=2.0)
+    b = elbo.regression_elbo_gram(X64.T @ X64, X64.T @ y64, y64 @ y64, n, loc, scale, eps, 2.0)
+    assert rel(b["loss"], a["loss"]) < 1e-12
+    assert rel(b["grad_loc"], a["grad_loc"]) < 1e-10
+    assert rel(b["grad_u_scale"], a["grad_u_scale"]) < 1e-10
+
+    m = rng.random(n) > 0.2
+    yy, bb = rng.normal(size=n), (rng.random(n) < 0.5).astype(np.float64)
+    zl, zs = np.linspace(-1, 1, n), np.linspace(0.5, 1.5, n).astype(np.float32)
+    em, ez = rng.normal(size=K), rng.normal(size=(K, n)).astype(np.float32)
+    a = elbo.hierarchical_masked_elbo(yy, bb, m, 0.2, 0.7, zl, zs, em, ez)
+    b = elbo.hierarchical_masked_elbo_chunked(yy, bb, m, 0.2, 0.7, zl, zs, em,
+                                              lambda k0, k1: ez[k0:k1], K, chunk=4)
+    assert rel(b["loss"], a["loss"]) < 1e-12
+    for key in ("grad_mu_loc", "grad_mu_scale", "grad_z_loc", "grad_z_scale"):
+        assert rel(b[key], a[key]) < 1e-10, key
