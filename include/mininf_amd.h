@@ -47,7 +47,11 @@ enum mi_family {
   MI_NORMAL = 0,            /* roles: loc, scale, value          torch/distributions/normal.py:88-103 */
   MI_BERNOULLI_LOGITS = 1,  /* roles: logits, -, value            torch/distributions/bernoulli.py:121-125 */
   MI_BERNOULLI_PROBS = 2,   /* roles: probs, -, value (clamped)   bernoulli.py:104-106, utils.py:101-137 */
-  MI_BETA = 3               /* roles: concentration1, concentration0, value  beta.py:88-92, dirichlet.py:90-97 */
+  MI_BETA = 3,              /* roles: concentration1, concentration0, value  beta.py:88-92, dirichlet.py:90-97 */
+  MI_GAMMA = 4,             /* roles: concentration, rate, value  torch/distributions/gamma.py:90-99 */
+  MI_POISSON = 5,           /* roles: rate, -, value              torch/distributions/poisson.py:60-65 */
+  MI_INVERSE_GAMMA = 6      /* roles: concentration, rate, value  mininf/distributions.py:5-11: Gamma
+                               through PowerTransform(-1), transformed_distribution.py:151-170 */
 };
 
 /* what to do with d(site total)/d(operand) */
@@ -277,6 +281,28 @@ int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const floa
 int mi_step_begin(uint64_t* counter, uint64_t* snapshot, uint32_t* flags, int64_t nflags,
                   void* stream);
 
+/* Gamma(concentration, rate) guide draws (replaces Gamma.rsample, gamma.py:80-88):
+ *   g[k, i] = standard Gamma(concentration[i]) draw (Marsaglia-Tsang, same counter scheme as
+ *             mi_beta_rsample, sub-stream 2), or g_in[k, i] when g_in != NULL (parity mode);
+ *   x[k, i] = max(g[k, i] / rate[i], FLT_MIN).
+ * g is the backward's input (torch saves _standard_gamma's result the same way). */
+int mi_gamma_rsample(const float* concentration, int64_t concentration_stride, const float* rate,
+                     int64_t rate_stride, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                     const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                     const float* g_in, float* g, float* x, void* stream);
+/* Backward for upstream dx[k, i] (strided), reduced over particles in fp64:
+ *   dconcentration[i] = sum_k dx / rate * standard_gamma_grad(concentration, g)
+ *                       (torch _standard_gamma_grad, Distributions.h:310, in double)
+ *   drate[i]          = sum_k -dx * g / rate^2 */
+int mi_gamma_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
+int mi_gamma_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
+                              const float* g, const float* concentration,
+                              int64_t concentration_stride, const float* rate,
+                              int64_t rate_stride, int64_t K, int64_t N, void* workspace,
+                              size_t workspace_bytes, float* dconcentration,
+                              int64_t dconcentration_stride, float* drate, int64_t drate_stride,
+                              void* stream);
+
 /* Constrained parameters of one guide factor in one launch, interleaved [n, m]:
  *   out[i * m + j] = exp(u[j][i * stride[j]])   (transform[j] MI_TRANSFORM_EXP: transform_to(positive),
  *                                                 torch constraint_registry.py:184-189)
@@ -362,6 +388,7 @@ int mi_linear_struct_size(size_t* bytes);
 /* One mean-field guide factor whose entropy enters the ELBO, viewed as n elements:
  *   MI_NORMAL: param[0] = loc (read only with an absorbed draw), param[1] = scale
  *   MI_BETA:   param[0] = concentration1, param[1] = concentration0
+ *   MI_GAMMA:  param[0] = concentration, param[1] = rate (gamma.py:101-107; draw_kind NONE only)
  * Parameters are fp32 with element stride `stride` (0 only when n == 1). mi_elbo_backward writes
  *   grad[j][i * grad_stride[j]] = d loss / d param_j(i)                  (transform[j] NONE)
  *                               = d loss / d u_j(i) = (d loss / d param_j) * param_j

@@ -27,7 +27,7 @@ MAX_BUFFERS = 16
 LINEAR_MAX_P = 64
 LINEAR_VALU = 2
 
-NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA = 0, 1, 2, 3
+NORMAL, BERNOULLI_LOGITS, BERNOULLI_PROBS, BETA, GAMMA, POISSON, INVERSE_GAMMA = 0, 1, 2, 3, 4, 5, 6
 GRAD_NONE, GRAD_DENSE, GRAD_PARTICLE = 0, 1, 2
 GROUP_FLAGS_ZEROED = 1
 GROUP_DRAW_PARTIALS = 2
@@ -183,6 +183,14 @@ _SIGNATURES = {
     "mi_beta_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                                                 c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp, c_i64,
                                                 c_vp, c_i64, c_vp]),
+    "mi_gamma_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
+                                        ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                        c_vp, c_vp]),
+    "mi_gamma_rsample_backward_workspace_bytes": (ctypes.c_int, [c_i64, c_i64,
+                                                                 ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_gamma_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                                 c_i64, c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp,
+                                                 c_i64, c_vp, c_i64, c_vp]),
     "mi_philox_normal": (ctypes.c_int, [c_i64, c_i64, ctypes.c_uint64, ctypes.c_uint64,
                                         ctypes.c_uint32, c_i64, c_vp, c_vp]),
     "mi_philox4x32": (ctypes.c_int, [c_vp, c_i64, ctypes.c_uint32, ctypes.c_uint32, c_vp, c_vp]),

@@ -385,7 +385,10 @@ class Value(Distribution):
         super().__init__(torch.Size(), torch.Size(), validate_args)
         self.value = value
         self._support = support or torch.distributions.constraints.real
-        if value is not None and not check_constraint(self._support, value).all():
+        # A default computed from particles inside the vmapped trace (e.g. `X @ theta`) cannot be
+        # checked eagerly; the particle tracers check it with the site's support instead.
+        if value is not None and not torch._C._functorch.is_batchedtensor(value) and \
+                not check_constraint(self._support, value).all():
             raise ValueError(f"Default value is not in the specified support {self._support}.")
 
     @property
@@ -466,7 +469,9 @@ def broadcast_samples(model: Callable, states: State | None = None, **params: to
         -> State:
     """
     Run ``model`` once per leading-dimension entry of the given samples and stack the resulting
-    states (reference ``core.py:548-584``).
+    states (reference ``core.py:548-584``). Samples on a ROCm device are broadcast in ONE run of the
+    model under ``torch.func.vmap`` (:func:`mininf_amd.particles.broadcast_particles`); host
+    samples take the reference's per-sample loop.
 
     Example:
 
@@ -479,6 +484,11 @@ def broadcast_samples(model: Callable, states: State | None = None, **params: to
     """
     states = states if states is not None else State()
     states.update(params)
+    if states and all(isinstance(v, torch.Tensor) and v.device.type != "cpu"
+                      for v in states.values()):
+        # device samples: one vmapped run of the model over the samples (particle machinery)
+        from .particles import broadcast_particles
+        return broadcast_particles(model, states)
     finished = []
     for state in transpose_states(states):
         with state:

@@ -214,11 +214,53 @@ MI_DEV void eval_beta(float a, float b, float v, Elem& e) {
   e.support_bad = !(v >= 0.0f && v <= 1.0f);
 }
 
+// Gamma(a, r): xlogy(a, r) + xlogy(a - 1, v) - r v - lgamma(a)
+// torch/distributions/gamma.py:90-99; support positive (v > 0), a > 0 and r > 0 (arg_constraints).
+MI_DEV void eval_gamma(float a, float r, float v, Elem& e) {
+  e.lp = xlogy(a, r) + xlogy(a - 1.0f, v) - r * v - lgammaf(a);
+  e.d[0] = logf(r) + logf(v) - (float)digamma((double)a);
+  e.d[1] = a / r - v;
+  e.d[2] = (a - 1.0f) / v - r;
+  e.param_bad = !(a > 0.0f) || !(r > 0.0f);
+  e.support_bad = !(v > 0.0f);
+}
+
+// Poisson(rate): xlogy(v, rate) - rate - lgamma(v + 1)
+// torch/distributions/poisson.py:60-65; support nonnegative integers, rate >= 0. d/dv is torch's
+// continuous derivative (log rate - digamma(v + 1)).
+MI_DEV void eval_poisson(float rate, float v, Elem& e) {
+  e.lp = xlogy(v, rate) - rate - lgammaf(v + 1.0f);
+  e.d[0] = v / rate - 1.0f;
+  e.d[1] = 0.0f;
+  e.d[2] = logf(rate) - (float)digamma((double)v + 1.0);
+  e.param_bad = !(rate >= 0.0f);
+  e.support_bad = !(v >= 0.0f && v == floorf(v));
+}
+
+// InverseGamma(a, r) = Gamma(a, r) pushed through y = x^-1 (mininf/distributions.py:5-11):
+// TransformedDistribution.log_prob (transformed_distribution.py) with x = y^-1 and
+// PowerTransform.log_abs_det_jacobian = log|-y / x| (transforms.py):
+//   Gamma.log_prob(x) - log|-y / x|;  support positive.
+MI_DEV void eval_inverse_gamma(float a, float r, float y, Elem& e) {
+  const float x = 1.0f / y;
+  Elem g;
+  eval_gamma(a, r, x, g);
+  e.lp = g.lp - logf(fabsf(-y / x));
+  e.d[0] = g.d[0];
+  e.d[1] = g.d[1];
+  e.d[2] = g.d[2] * (-x * x) - 2.0f / y;   // dx/dy = -x^2; d log(y / x) / dy = 2 / y
+  e.param_bad = g.param_bad;
+  e.support_bad = !(y > 0.0f);
+}
+
 MI_DEV void eval_family(int family, float r0, float r1, float r2, Elem& e) {
   switch (family) {
     case MI_NORMAL: eval_normal(r0, r1, r2, e); break;
     case MI_BERNOULLI_LOGITS: eval_bernoulli_logits(r0, r2, e); break;
     case MI_BERNOULLI_PROBS: eval_bernoulli_probs(r0, r2, e); break;
+    case MI_GAMMA: eval_gamma(r0, r1, r2, e); break;
+    case MI_POISSON: eval_poisson(r0, r2, e); break;
+    case MI_INVERSE_GAMMA: eval_inverse_gamma(r0, r1, r2, e); break;
     default: eval_beta(r0, r1, r2, e); break;
   }
 }

@@ -53,6 +53,10 @@ MI_DEV double factor_entropy(const mi_factor& f, int64_t i) {
   if (f.family == MI_NORMAL) {  // 0.5 + 0.5 log(2 pi) + log(scale)  (normal.py:112-113)
     return (double)(1.4189385332046727f + logf(f.param[1][i * f.stride[1]]));
   }
+  if (f.family == MI_GAMMA) {   // a - log(r) + lgamma(a) + (1 - a) psi(a)  (gamma.py:101-107)
+    const float a = f.param[0][i * f.stride[0]], r = f.param[1][i * f.stride[1]];
+    return (double)(a - logf(r)) + (double)lgammaf(a) + (double)((1.0f - a) * digammaf(a));
+  }
   // Beta(a, b) = Dirichlet([a, b]) (dirichlet.py:122-130 with k = 2, a0 = a + b):
   //   lgamma(a) + lgamma(b) - lgamma(a0) - (2 - a0) psi(a0) - (a - 1) psi(a) - (b - 1) psi(b)
   const float a = f.param[0][i * f.stride[0]], b = f.param[1][i * f.stride[1]];
@@ -68,6 +72,12 @@ MI_DEV void entropy_grad(const mi_factor& f, int64_t i, double& d0, double& d1) 
   if (f.family == MI_NORMAL) {
     d0 = 0.0;
     d1 = (double)(1.0f / f.param[1][i * f.stride[1]]);
+    return;
+  }
+  if (f.family == MI_GAMMA) {   // (1 + (1 - a) psi'(a), -1 / r)
+    const float a = f.param[0][i * f.stride[0]], r = f.param[1][i * f.stride[1]];
+    d0 = (double)(1.0f + (1.0f - a) * trigammaf(a));
+    d1 = (double)(-1.0f / r);
     return;
   }
   const float a = f.param[0][i * f.stride[0]], b = f.param[1][i * f.stride[1]];
@@ -289,7 +299,7 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
 
 // ---- forward --------------------------------------------------------------------------------
 // HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
-// of the common large-factor case small.
+// of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
 template <bool HAS_BETA>
 __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                                                const AbsorbPlan P,
@@ -401,8 +411,9 @@ namespace {
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 bool valid_factor(const mi_factor& F) {
-  if (F.n < 1 || (F.family != MI_NORMAL && F.family != MI_BETA) || F.param[1] == nullptr ||
-      (F.family == MI_BETA && F.param[0] == nullptr))
+  if (F.n < 1 || (F.family != MI_NORMAL && F.family != MI_BETA && F.family != MI_GAMMA) ||
+      F.param[1] == nullptr || ((F.family == MI_BETA || F.family == MI_GAMMA) && F.param[0] == nullptr) ||
+      (F.family == MI_GAMMA && F.draw_kind != MI_DRAW_NONE))
     return false;
   for (int j = 0; j < 2; ++j) {
     if (F.transform[j] != MI_TRANSFORM_NONE && F.transform[j] != MI_TRANSFORM_EXP) return false;
@@ -578,7 +589,7 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
   auto* counters = static_cast<unsigned*>(workspace);
   auto* work = reinterpret_cast<double*>(static_cast<char*>(workspace) + MI_ELBO_COUNTER_BYTES);
   bool has_beta = false;
-  for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family == MI_BETA;
+  for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family != MI_NORMAL;
   const dim3 grid((unsigned)(L.fwd.lead_blocks + L.fwd.first[L.fwd.num]));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (has_beta)

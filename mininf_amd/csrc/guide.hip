@@ -266,6 +266,70 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
   }
 }
 
+// Gamma(concentration, rate) draws (gamma.py:80-88): x = standard_gamma(concentration) / rate,
+// clamped below at the smallest normal float as torch does. The standard draws g are kept for the
+// backward (torch saves them as _standard_gamma's result). Injected g (parity mode) replaces the
+// generator.
+__global__ __launch_bounds__(kGuideThreads) void k_gamma_rsample(
+    const float* __restrict__ conc, int64_t conc_s, const float* __restrict__ rate, int64_t rate_s,
+    int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
+    uint32_t stream_id, int64_t poff, const float* __restrict__ g_in, float* __restrict__ g_out,
+    float* __restrict__ x) {
+  const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
+  if (t >= K * N) return;
+  const int64_t k = t / N, i = t - k * N;
+  float g;
+  if (g_in != nullptr) {
+    g = g_in[t];
+  } else {
+    if (step_dev != nullptr) step += *step_dev;
+    Stream r{seed, step, stream_id, 2u, (uint64_t)i, (uint64_t)(poff + k)};
+    g = sample_gamma(conc[i * conc_s], r);
+  }
+  g_out[t] = g;
+  x[t] = fmaxf(g / rate[i * rate_s], 1.17549435e-38f);
+}
+
+// Backward of k_gamma_rsample for upstream dx, reduced over particle rows [k0, k1) per element:
+//   d concentration = sum_k (dx / rate) * standard_gamma_grad(concentration, g)
+//   d rate          = sum_k -dx * g / rate^2
+// (autograd of `_standard_gamma(c) / r`: div backward, then _standard_gamma's backward).
+__global__ __launch_bounds__(kGuideThreads) void k_gamma_rsample_bwd(
+    const float* __restrict__ dx, int64_t dx_sk, int64_t dx_si, const float* __restrict__ g,
+    const float* __restrict__ conc, int64_t conc_s, const float* __restrict__ rate,
+    int64_t rate_s, int64_t K, int64_t N, float* __restrict__ out_c, int64_t oc_s,
+    float* __restrict__ out_r, int64_t or_s, int64_t out_stride, int64_t rows_per_block, int ti) {
+  __shared__ double red[kGuideThreads][2];
+  const int tx = threadIdx.x % ti, ty = threadIdx.x / ti, tk = kGuideThreads / ti;
+  const int64_t i = (int64_t)blockIdx.x * ti + tx;
+  const int64_t k0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t k1 = min(K, k0 + rows_per_block);
+  double sc = 0.0, sr = 0.0;
+  if (i < N) {
+    const float a = conc[i * conc_s], r = rate[i * rate_s];
+    for (int64_t k = k0 + ty; k < k1; k += tk) {
+      const float d = dx[k * dx_sk + i * dx_si];
+      if (d == 0.0f) continue;
+      const float gv = g[k * N + i];
+      const float dg = d / r;                       // grad of the standard draw (fp32, as torch)
+      sc += (double)(dg * (float)standard_gamma_grad((double)a, (double)gv));
+      sr += (double)(-d * gv / (r * r));
+    }
+  }
+  red[threadIdx.x][0] = sc;
+  red[threadIdx.x][1] = sr;
+  __syncthreads();
+  if (ty == 0 && i < N) {
+    double tc = 0.0, tr = 0.0;
+    for (int q = 0; q < tk; ++q) {
+      tc += red[q * ti + tx][0];
+      tr += red[q * ti + tx][1];
+    }
+    out_c[blockIdx.y * out_stride + i * oc_s] = (float)tc;
+    out_r[blockIdx.y * out_stride + i * or_s] = (float)tr;
+  }
+}
+
 // Per-draw implicit-gradient factors of Beta draws, independent of the upstream gradient:
 //   out[(k N + i) 2 + 0] =  dgrad(x, a, a+b) (1 - x),  out[... + 1] = -dgrad(1 - x, b, a+b) x
 // so that sum_k dx[k,i] out[k,i,j] is mi_beta_rsample_backward's dc1 / dc0. One thread per
@@ -485,6 +549,60 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);
   hipLaunchKernelGGL(mi::k_sum_slices, dim3(g), dim3(mi::kGuideThreads), 0, s, o1, o0, gy, N, dc1,
                      dc1_stride, dc0, dc0_stride);
+  return to_code(hipGetLastError());
+}
+
+int mi_gamma_rsample(const float* concentration, int64_t concentration_stride, const float* rate,
+                     int64_t rate_stride, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                     const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                     const float* g_in, float* g, float* x, void* stream) {
+  if (concentration == nullptr || rate == nullptr || g == nullptr || x == nullptr || K < 1 ||
+      N < 1 || stream_id > 0xFFFFFFu)
+    return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_gamma_rsample, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), concentration,
+                     concentration_stride, rate, rate_stride, K, N, seed, step, step_device,
+                     stream_id, particle_offset, g_in, g, x);
+  return to_code(hipGetLastError());
+}
+
+int mi_gamma_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes) {
+  return mi_beta_rsample_backward_workspace_bytes(K, N, bytes);   // same geometry
+}
+
+int mi_gamma_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_stride_i,
+                              const float* g, const float* concentration,
+                              int64_t concentration_stride, const float* rate,
+                              int64_t rate_stride, int64_t K, int64_t N, void* workspace,
+                              size_t workspace_bytes, float* dconcentration,
+                              int64_t dconcentration_stride, float* drate, int64_t drate_stride,
+                              void* stream) {
+  if (dx == nullptr || g == nullptr || concentration == nullptr || rate == nullptr ||
+      dconcentration == nullptr || drate == nullptr || K < 1 || N < 1)
+    return MI_EINVAL;
+  size_t need = 0;
+  mi_gamma_rsample_backward_workspace_bytes(K, N, &need);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const BwdGeometry geo = bwd_geometry(K, N);
+  const int64_t rows = geo.rows, gy = geo.slices;
+  float* oc = dconcentration;
+  float* orr = drate;
+  int64_t sc = dconcentration_stride, sr = drate_stride;
+  if (gy > 1) {
+    oc = static_cast<float*>(workspace);
+    orr = oc + gy * N;
+    sc = sr = 1;
+  }
+  hipLaunchKernelGGL(mi::k_gamma_rsample_bwd, dim3((unsigned)geo.gx, (unsigned)gy),
+                     dim3(mi::kGuideThreads), 0, s, dx, dx_stride_k, dx_stride_i, g, concentration,
+                     concentration_stride, rate, rate_stride, K, N, oc, sc, orr, sr, N, rows,
+                     geo.ti);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || gy == 1) return to_code(e);
+  const unsigned grid = (unsigned)ceil_div(N, mi::kGuideThreads);
+  hipLaunchKernelGGL(mi::k_sum_slices, dim3(grid), dim3(mi::kGuideThreads), 0, s, oc, orr, gy, N,
+                     dconcentration, dconcentration_stride, drate, drate_stride);
   return to_code(hipGetLastError());
 }
 

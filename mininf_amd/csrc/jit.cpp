@@ -52,13 +52,19 @@ const char* eval_fn(int family) {
     case MI_NORMAL: return "eval_normal";
     case MI_BERNOULLI_LOGITS: return "eval_bernoulli_logits";
     case MI_BERNOULLI_PROBS: return "eval_bernoulli_probs";
+    case MI_GAMMA: return "eval_gamma";
+    case MI_POISSON: return "eval_poisson";
+    case MI_INVERSE_GAMMA: return "eval_inverse_gamma";
     default: return "eval_beta";
   }
 }
 
-bool role_used(int family, int q) {
-  return !((family == MI_BERNOULLI_LOGITS || family == MI_BERNOULLI_PROBS) && q == 1);
+// Families whose density has no second parameter role (their eval_* take (r0, value)).
+bool one_param(int family) {
+  return family == MI_BERNOULLI_LOGITS || family == MI_BERNOULLI_PROBS || family == MI_POISSON;
 }
+
+bool role_used(int family, int q) { return !(one_param(family) && q == 1); }
 
 // Everything about a group that changes the generated code.
 struct Signature {
@@ -125,7 +131,7 @@ void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, const std::
     else r[q] = operand_var(g, st.operand[q]);
   }
   o << in << "{\n" << in << "  mi::Elem el;\n";
-  if (st.family == MI_BERNOULLI_LOGITS || st.family == MI_BERNOULLI_PROBS)
+  if (one_param(st.family))
     o << in << "  mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[2] << ", el);\n";
   else
     o << in << "  mi::" << eval_fn(st.family) << "(" << r[0] << ", " << r[1] << ", " << r[2]

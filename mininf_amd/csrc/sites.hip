@@ -926,7 +926,7 @@ bool validate_group(const mi_group* g) {
   if (g->num_slots < 0 || g->num_slots > MI_MAX_SLOTS) return false;
   for (int s = 0; s < g->num_sites; ++s) {
     const mi_site& st = g->sites[s];
-    if (st.family < MI_NORMAL || st.family > MI_BETA) return false;
+    if (st.family < MI_NORMAL || st.family > MI_INVERSE_GAMMA) return false;
     if (st.operand[2] < 0) return false;  // the value is always an operand
     for (int q = 0; q < 3; ++q)
       if (st.operand[q] >= g->num_operands) return false;
@@ -986,6 +986,7 @@ int row_elems() {
 bool bcast_eligible(const mi_group* g) {
   if (g->num_sites != 1 || g->N < 1024 || g->K < 64) return false;
   const mi_site& st = g->sites[0];
+  if (st.family > MI_BETA) return false;   // BCAST kernels exist for the first four families
   if (st.mask != nullptr && st.mask_stride_k != 0) return false;
   const mi_operand& v = g->operands[st.operand[2]];
   if (v.stride_k != 0 || v.stride_i == 0 || v.grad_mode != MI_GRAD_NONE) return false;

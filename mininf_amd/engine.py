@@ -40,6 +40,9 @@ FAMILY_CODES = {
     "bernoulli_logits": nat.BERNOULLI_LOGITS,
     "bernoulli_probs": nat.BERNOULLI_PROBS,
     "beta": nat.BETA,
+    "gamma": nat.GAMMA,
+    "poisson": nat.POISSON,
+    "inverse_gamma": nat.INVERSE_GAMMA,
 }
 
 
@@ -303,8 +306,8 @@ class _GroupLauncher:
         for index, (site, roles, mask) in enumerate(self.sites):
             desc = group.sites[index]
             desc.family = FAMILY_CODES[site.family]
-            if site.family.startswith("bernoulli"):
-                roles = [roles[0], (-1, 0.0), roles[1]]
+            if site.family.startswith("bernoulli") or site.family == "poisson":
+                roles = [roles[0], (-1, 0.0), roles[1]]   # one-parameter families
             for q in range(3):
                 desc.operand[q] = roles[q][0]
                 desc.constant[q] = roles[q][1]
@@ -752,6 +755,8 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
             if lazy is not None:   # exact-shape use, checked by _lazy_uses
                 views.append(_View(None, N, 1, None, lazy))
                 continue
+            if is_value and site.family == "poisson" and not t.is_floating_point():
+                t = t.to(torch.float32)   # integer counts (exact in fp32 below 2^24)
             moved, constant = _to_device(_float(t, site.name), K, device, f"site '{site.name}'",
                                          allow_constant=not is_value)
             views.append(_View(None, 0, 0, constant) if constant is not None
@@ -816,7 +821,7 @@ class EntropyFactor:
     """
     A guide factor whose entropy the ELBO kernels evaluate (``mi_factor``): ``tensor`` is the
     autograd input -- Normal: the scale as [n] (stride 1, or any stride when n == 1); Beta: the
-    interleaved [n, 2] concentration array. ``name`` / ``distribution`` identify the factor's
+    interleaved [n, 2] concentration array; Gamma: the interleaved [n, 2] (concentration, rate). ``name`` / ``distribution`` identify the factor's
     draw in the samples (for absorbing the draw's backward).
     """
     family: int
@@ -880,8 +885,9 @@ def _absorb_factor(factor: EntropyFactor, samples: Dict[str, torch.Tensor], laun
     does not come straight from a ParameterizedDistribution, ...).
     """
     dist = factor.distribution
-    if dist is None or factor.name is None or factor.name not in samples:
-        return None
+    if dist is None or factor.name is None or factor.name not in samples or \
+            factor.family not in _FACTOR_PARAMS:
+        return None   # Gamma draws keep their own backward (mi_gamma_rsample_backward)
     sources = getattr(dist, "_mininf_amd_sources", None) or {}
     params: List[Optional[Tuple[torch.Tensor, int]]] = []
     for pname in _FACTOR_PARAMS[factor.family]:
@@ -1088,7 +1094,7 @@ class _ElboPlan:
             d = E.factors[j]
             d.family, d.n = f.family, f.n
             base = f.tensor.data_ptr()
-            if f.family == nat.BETA:
+            if f.family in (nat.BETA, nat.GAMMA):
                 d.param[0], d.param[1] = base, base + 4
                 d.stride[0] = d.stride[1] = 2
             else:
@@ -1286,7 +1292,7 @@ class _ElboPlan:
                 continue
             grad = torch.empty_like(f.tensor)
             base = grad.data_ptr()
-            if f.family == nat.BETA:
+            if f.family in (nat.BETA, nat.GAMMA):
                 d.grad[0], d.grad[1] = base, base + 4
                 d.grad_stride[0] = d.grad_stride[1] = 2
             else:
@@ -1371,10 +1377,10 @@ def _lazy_uses(trace: ParticleTrace) -> Tuple[set, set]:
 
 def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
     """
-    Split a factorised guide into factors whose entropy the ELBO kernels evaluate (Normal, Beta)
-    and the rest (whose entropy torch.distributions evaluates).
+    Split a factorised guide into factors whose entropy the ELBO kernels evaluate (Normal, Beta,
+    Gamma) and the rest (whose entropy torch.distributions evaluates).
     """
-    from torch.distributions import Beta, Normal
+    from torch.distributions import Beta, Gamma, Normal
 
     from . import guide
     fused: List[EntropyFactor] = []
@@ -1388,6 +1394,11 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
             if n > 1 and scale.stride(0) != 1:
                 scale = scale.contiguous()
             fused.append(EntropyFactor(nat.NORMAL, n, scale, name, factor))
+        elif len(fused) < nat.MAX_FACTORS and cls is Gamma and factor.concentration.is_cuda and \
+                factor.concentration.dtype == torch.float32:
+            # interleaved [n, 2] (concentration, rate), the Beta layout (one stack kernel)
+            pair = torch.stack(torch.broadcast_tensors(factor.concentration, factor.rate), -1)
+            fused.append(EntropyFactor(nat.GAMMA, n, pair.reshape(n, 2).contiguous(), name, factor))
         elif len(fused) < nat.MAX_FACTORS and cls is Beta:
             conc = guide.beta_concentration(factor, n)
             if conc.is_cuda:

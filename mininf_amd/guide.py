@@ -2,14 +2,14 @@
 Reparameterised guide sampling over K particles (replaces ``FactorizedDistribution.rsample``,
 reference ``mininf/nn.py:133-145``, with ONE draw per call at ``nn.py:217``).
 
-Normal and Beta factors are drawn by HIP kernels from a counter-based Philox generator keyed by
-(seed, step, factor index, global particle index, element), so that K particles split over W GPUs
-draw exactly the union of what one GPU would draw. Other families (Gamma, MultivariateNormal, ...)
-use their own ``torch.distributions`` ``rsample`` on the device (outside the north-star families).
+Normal, Beta and Gamma factors are drawn by HIP kernels from a counter-based Philox generator keyed
+by (seed, step, factor index, global particle index, element), so that K particles split over W GPUs
+draw exactly the union of what one GPU would draw. Other families (MultivariateNormal, ...) use
+their own ``torch.distributions`` ``rsample`` on the device.
 
-Parity mode: ``noise[name]`` injects host-drawn standard normals (Normal factors, [K, *shape]) or
-the draws themselves (Beta factors), exactly as the oracle's sample-injection protocol does
-(SURVEY.md 8(c)).
+Parity mode: ``noise[name]`` injects host-drawn standard normals (Normal factors, [K, *shape]),
+the draws themselves (Beta factors) or the standard Gamma draws g with x = g / rate (Gamma
+factors), exactly as the oracle's sample-injection protocol does.
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import os
 from typing import Dict, Optional, Tuple
 
 import torch
-from torch.distributions import Beta, Distribution, Normal
+from torch.distributions import Beta, Distribution, Gamma, Normal
 
 from . import _native as nat
 
@@ -147,6 +147,56 @@ class _BetaRsampleFn(torch.autograd.Function):
             workspace.data_ptr(), size.value, out, 2, out + 4, 2, nat.stream_handle(device)),
             "mi_beta_rsample_backward")
         return None, dconc
+
+
+def gamma_params(distribution: Gamma, N: int) -> Tuple[torch.Tensor, int, torch.Tensor, int]:
+    """(concentration, stride, rate, stride) of a Gamma factor viewed as [N]."""
+    conc, conc_s = _flat_param(distribution.concentration, N)
+    rate, rate_s = _flat_param(distribution.rate, N)
+    return conc, conc_s, rate, rate_s
+
+
+class _GammaRsampleFn(torch.autograd.Function):
+    """
+    Gamma.rsample (gamma.py:80-88) over K particles: mi_gamma_rsample, and its backward through
+    torch._standard_gamma_grad restated in fp64 (mi_gamma_rsample_backward). ``cfg.noise`` injects
+    the standard Gamma draws g (x = g / rate), the oracle's protocol for Gamma factors.
+    """
+    @staticmethod
+    def forward(ctx, cfg: DrawConfig, conc: torch.Tensor, conc_s: int, rate: torch.Tensor,
+                rate_s: int):  # type: ignore[override]
+        N, K = conc.shape[0], cfg.K
+        x = torch.empty((K, N), dtype=torch.float32, device=conc.device)
+        g = torch.empty((K, N), dtype=torch.float32, device=conc.device)
+        seed, step = _philox_key(cfg)
+        nat.check(nat.lib().mi_gamma_rsample(
+            conc.data_ptr(), conc_s, rate.data_ptr(), rate_s, K, N, seed, step,
+            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
+            g.data_ptr(), x.data_ptr(), nat.stream_handle(conc.device)), "mi_gamma_rsample")
+        ctx.save_for_backward(g, conc, rate)
+        ctx.strides = (conc_s, rate_s)
+        ctx.K, ctx.N = K, N
+        return x
+
+    @staticmethod
+    def backward(ctx, dx: torch.Tensor):  # type: ignore[override]
+        g, conc, rate = ctx.saved_tensors
+        conc_s, rate_s = ctx.strides
+        K, N = ctx.K, ctx.N
+        device = dx.device
+        lib = nat.lib()
+        size = ctypes.c_size_t()
+        nat.check(lib.mi_gamma_rsample_backward_workspace_bytes(K, N, ctypes.byref(size)),
+                  "mi_gamma_rsample_backward_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        dconc = torch.empty(N, dtype=torch.float32, device=device)
+        drate = torch.empty(N, dtype=torch.float32, device=device)
+        nat.check(lib.mi_gamma_rsample_backward(
+            dx.data_ptr(), dx.stride(0), dx.stride(1), g.data_ptr(), conc.data_ptr(), conc_s,
+            rate.data_ptr(), rate_s, K, N, workspace.data_ptr(), size.value, dconc.data_ptr(), 1,
+            drate.data_ptr(), 1, nat.stream_handle(device)), "mi_gamma_rsample_backward")
+        # per element; a broadcast parameter's expand backward sums them
+        return None, dconc, None, drate, None
 
 
 @dataclasses.dataclass(eq=False)   # identity semantics: used in sets
@@ -328,6 +378,16 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
         x = _BetaRsampleFn.apply(cfg, conc)
         _DRAWN[x.data_ptr()] = Drawn(BETA_FAMILY, cfg, x, N, _beta_dgrad(x, conc, cfg.K, N),
                                      conc)
+        return x.reshape((cfg.K,) + tuple(shape))
+    if cls is Gamma:
+        shape = distribution.batch_shape
+        N = max(1, int(shape.numel()))
+        nat.require_device(distribution.concentration, "guide Gamma concentration")
+        conc, conc_s, rate, rate_s = gamma_params(distribution, N)
+        if cfg.noise is not None:   # injected standard draws g, [K, *shape]
+            cfg.noise = cfg.noise.to(device=conc.device, dtype=torch.float32).reshape(cfg.K, N) \
+                .contiguous()
+        x = _GammaRsampleFn.apply(cfg, conc, conc_s, rate, rate_s)
         return x.reshape((cfg.K,) + tuple(shape))
     if cfg.noise is not None:
         return cfg.noise

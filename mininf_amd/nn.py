@@ -390,11 +390,16 @@ class LogLikelihoodLoss(nn.Module):
             with LogProbTracer() as log_prob:
                 condition(model, **parameters)()
             return - log_prob.total
-        samples = {}
+        samples, observed = {}, {}
         for name, value in parameters.items():
+            if isinstance(value, torch.masked.MaskedTensor):
+                observed[name] = value   # masked observations: shared data, not a particle axis
+                continue
             if not isinstance(value, torch.Tensor):
                 value = torch.as_tensor(value, dtype=torch.get_default_dtype(), device=device)
             samples[name] = value.unsqueeze(0)
+        if observed:
+            model = condition(model, **observed)
         trace = particles.trace_particles(model, samples, 1)
         joint = engine.log_joint(trace, -1.0, device)
         collector = graph.deferred()

@@ -18,6 +18,7 @@ per-particle sum; they are outside the north-star families and listed in DESIGN.
 from __future__ import annotations
 
 import collections
+import contextlib
 import copy
 import dataclasses
 import os
@@ -25,12 +26,16 @@ import weakref
 from typing import Any, Callable, Dict, List, Optional, Tuple, cast
 
 import torch
-from torch.distributions import Bernoulli, Beta, Categorical, Distribution, Normal
+from torch.distributions import Bernoulli, Beta, Categorical, Distribution, Gamma, \
+    MultivariateNormal, Normal, Poisson, PowerTransform, TransformedDistribution
 from torch.distributions.constraints import Constraint
+from torch.distributions.utils import lazy_property
+from torch.overrides import TorchFunctionMode
+from torch.utils._pytree import tree_flatten, tree_map
 
 from . import core
 from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
-from .util import check_constraint, OptionalSize
+from .util import _normalize_shape, check_constraint, OptionalSize
 
 
 _functorch = torch._C._functorch
@@ -200,7 +205,30 @@ def classify(distribution: Distribution) -> Tuple[str, List[Any]]:
         return "beta", [distribution.concentration1, distribution.concentration0]
     if cls is Categorical:
         return "categorical", [distribution.logits]
+    if cls is Gamma:
+        return "gamma", [distribution.concentration, distribution.rate]
+    if cls is Poisson:
+        return "poisson", [distribution.rate]
+    if _is_inverse_gamma(distribution):
+        base = cast(Gamma, cast(TransformedDistribution, distribution).base_dist)
+        return "inverse_gamma", [base.concentration, base.rate]
     return "torch", []
+
+
+def _is_inverse_gamma(distribution: Distribution) -> bool:
+    """
+    Gamma through a single PowerTransform(-1) (mininf/distributions.py:5-11, or the same
+    construction spelled out) whose log_prob is TransformedDistribution's own.
+    """
+    if not isinstance(distribution, TransformedDistribution) or \
+            type(distribution).log_prob is not TransformedDistribution.log_prob or \
+            type(distribution.base_dist) is not Gamma or len(distribution.transforms) != 1:
+        return False
+    t = distribution.transforms[0]
+    if type(t) is not PowerTransform or is_batched(t.exponent):
+        return False
+    exponent = t.exponent
+    return bool((exponent == -1).all()) if isinstance(exponent, torch.Tensor) else exponent == -1
 
 
 class ParticleTracer(TracerMixin):
@@ -330,7 +358,12 @@ class ParticleTracer(TracerMixin):
         if self._validate_parameters:
             self._check_support(name, value, distribution, cast(Constraint, distribution.support))
             for param, constraint in distribution.arg_constraints.items():
-                if param not in distribution.__dict__ and not hasattr(type(distribution), param):
+                # as Distribution.__init__'s validation: parameters the distribution was not
+                # constructed with (lazy properties, e.g. MultivariateNormal.precision_matrix)
+                # are not checked
+                if param not in distribution.__dict__ and (
+                        not hasattr(type(distribution), param) or
+                        isinstance(getattr(type(distribution), param), lazy_property)):
                     continue
                 try:
                     tensor = getattr(distribution, param)
@@ -342,12 +375,75 @@ class ParticleTracer(TracerMixin):
                         f"Expected parameter {param} of distribution "
                         f"{type(distribution).__name__} for site '{name}' to satisfy the "
                         f"constraint {constraint}, but found invalid values")))
-        log_prob = distribution.log_prob(data)
+        if type(distribution) is MultivariateNormal and data.dtype == torch.float32 and \
+                data.device.type != "cpu":
+            # dense factorisations of float32 covariances are ill-conditioned in practice (the
+            # missing-observations example's GP prior): refactorise in float64 on the device
+            log_prob = _mvn_float64(distribution).log_prob(data.double()).float()
+        else:
+            log_prob = distribution.log_prob(data)
         if mask is not None:
             log_prob = torch.where(mask, log_prob, torch.zeros((), dtype=log_prob.dtype,
                                                                device=log_prob.device))
         total = log_prob.sum() * scale if scale != 1.0 else log_prob.sum()
         self.fallback_outputs.append((name, self._emit(total)))
+
+
+class TraceCompat(TorchFunctionMode):
+    """
+    Lets model code written for one draw on the host trace over device particles under vmap:
+
+    * host tensors: the reference's examples keep globals such as ``x = torch.linspace(0, 1, n)``
+      and build ``torch.eye(n)`` inside the model. Factory calls default to the particles' device
+      (a ``torch.device`` context entered beside this mode), and host tensors (other than 0-d
+      ones, which torch already mixes with device tensors) that meet a device tensor in an
+      operation are replaced by cached device copies;
+    * ``torch.linalg.cholesky`` (MultivariateNormal(loc, covariance_matrix)) checks its input on
+      the host, which vmap cannot do per particle: it runs as ``cholesky_ex`` and the
+      factorisation status becomes a deferred check with torch's message.
+
+    Used only when a plain trace failed on one of these.
+    """
+    def __init__(self, device: Optional[torch.device], tracer: "ParticleTracer") -> None:
+        super().__init__()
+        self.device = device
+        self.tracer = tracer
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if self.device is not None:
+            leaves = [x for x in tree_flatten((args, kwargs))[0] if isinstance(x, torch.Tensor)]
+            if any(x.device.type != "cpu" for x in leaves) and \
+                    any(x.device.type == "cpu" and x.dim() > 0 for x in leaves):
+                def lift(x):
+                    if not isinstance(x, torch.Tensor) or x.device.type != "cpu" or x.dim() == 0:
+                        return x
+                    return x.to(self.device) if is_batched(x) or x.requires_grad else \
+                        device_copy(x, self.device)
+                args, kwargs = tree_map(lift, (args, kwargs))
+        if func is torch.linalg.cholesky and not kwargs.get("upper", False) and "out" not in kwargs:
+            L, info = torch.linalg.cholesky_ex(*args, **kwargs)
+            ok = (info == 0).all()
+            self.tracer.checks.append(CheckRecord("cholesky", self.tracer._emit(ok), (
+                "linalg.cholesky: The factorization could not be completed because the input is "
+                "not positive-definite.")))
+            return L
+        return func(*args, **kwargs)
+
+
+def _needs_compat(error: RuntimeError) -> bool:
+    text = str(error)
+    return "same device" in text or ("device type" in text and "cpu" in text) or \
+        "data-dependent control flow" in text
+
+
+def _mvn_float64(distribution: MultivariateNormal) -> MultivariateNormal:
+    """The same MultivariateNormal, constructed in float64 from the parameter it was given."""
+    given = next(name for name in ("covariance_matrix", "precision_matrix", "scale_tril")
+                 if name in distribution.__dict__)
+    return MultivariateNormal(distribution.loc.double(),
+                              **{given: getattr(distribution, given).double()},
+                              validate_args=False)
 
 
 @dataclasses.dataclass
@@ -362,13 +458,30 @@ _NO_VALIDATE = object()
 
 
 def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
-                    validate: bool = True, defer_matmul: Optional[bool] = None) -> ParticleTrace:
+                    validate: bool = True, defer_matmul: Optional[bool] = None,
+                    lift_host: bool = False) -> ParticleTrace:
     """
     Run ``condition(model, **samples)`` once under ``vmap`` over the leading (particle) dimension of
     every sample and return the recorded sites with [K, ...] tensors. With ``defer_matmul``,
     ``X @ theta`` predictors of Normal / Bernoulli-logits sites are evaluated inside the site
-    kernels instead of by the model (:mod:`mininf_amd.linear`).
+    kernels instead of by the model (:mod:`mininf_amd.linear`). A model that mixes its own host
+    tensors with the device particles, or factorises a matrix, is traced again under
+    :class:`TraceCompat`.
     """
+    device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)), None)
+    lift = device if device is not None and device.type != "cpu" else None
+    if not lift_host:
+        try:
+            return _trace(model, samples, K, validate, defer_matmul, False, None)
+        except RuntimeError as error:
+            if not _needs_compat(error):
+                raise
+    return _trace(model, samples, K, validate, defer_matmul, True, lift)
+
+
+def _trace(model: Callable, samples: Dict[str, torch.Tensor], K: int, validate: bool,
+           defer_matmul: Optional[bool], compat: bool,
+           lift: Optional[torch.device]) -> ParticleTrace:
     from .linear import DeferredMatmul
 
     if defer_matmul is None:
@@ -382,7 +495,11 @@ def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
     def per_particle(*values):
         mode = DeferredMatmul(K, defer_matmul) if use_mode else None
         tracer.deferred = mode
-        with tracer:
+        with tracer, contextlib.ExitStack() as stack:
+            if lift is not None:
+                stack.enter_context(torch.device(lift))
+            if compat:
+                stack.enter_context(TraceCompat(lift, tracer))
             if mode is not None:
                 with mode:
                     core.condition(model, **dict(zip(names, values)))()
@@ -411,3 +528,86 @@ def trace_particles(model: Callable, samples: Dict[str, torch.Tensor], K: int,
     checks = [(check, outputs[check.output]) for check in tracer.checks]
     fallback = [(name, outputs[index]) for name, index in tracer.fallback_outputs]
     return ParticleTrace(sites=tracer.sites, checks=checks, fallback=fallback, K=K)
+
+
+# ------------------------------------------------------------------------------------------------
+# Posterior predictive on the particle machinery (reference core.py:495-584 broadcast_samples,
+# SampleTracer core.py:192-204).
+# ------------------------------------------------------------------------------------------------
+class BroadcastTracer(ParticleTracer):
+    """
+    The reference's SampleTracer for a model running once under ``vmap`` over the samples' leading
+    dimension: a site missing from the state is drawn with the distribution's own ``sample``
+    (``vmap(randomness="different")``: independent per sample) and recorded; shapes are checked as
+    the reference does; support checks become device outputs raised after the vmap.
+    """
+    def sample(self, state: State, name: str, distribution: Distribution,
+               sample_shape: OptionalSize = None) -> torch.Tensor:
+        sample_shape = _normalize_shape(sample_shape)
+        value = state.get(name)
+        if value is None:
+            value = distribution.sample(sample_shape)
+            state[name] = value
+        if self._validate_parameters:
+            value = self._coerce(value, name)
+            validate_shape(value, name, distribution, sample_shape)
+            self._check_support(name, value, distribution,
+                                cast(Constraint, distribution.support))
+        return value
+
+
+def broadcast_particles(model: Callable, states: Dict[str, torch.Tensor]) -> State:
+    """
+    ``broadcast_samples`` (reference core.py:548-584) as ONE traced run of ``model`` under
+    ``torch.func.vmap`` over the samples' leading dimension instead of a Python loop over samples:
+    deterministic values are computed batched, missing sites are drawn batched. Every value of the
+    result lives on the samples' device. Returns a :class:`State` of [S, ...] tensors (Python
+    numbers as [S] tensors, as the reference's transpose_states makes them).
+    """
+    core._assert_same_batch_size(cast(State, states))
+    names = list(states)
+    device = next((v.device for v in states.values() if isinstance(v, torch.Tensor)),
+                  torch.device("cpu"))
+
+    lift = device if device.type != "cpu" else None
+
+    def run(compat: bool):
+        tracer = BroadcastTracer()
+        keys: List[str] = []
+
+        def per_sample(*values):
+            inner = State(dict(zip(names, values)))
+            with tracer, inner, contextlib.ExitStack() as stack:
+                if compat:
+                    if lift is not None:
+                        stack.enter_context(torch.device(lift))
+                    stack.enter_context(TraceCompat(lift, tracer))
+                model()
+            keys[:] = list(inner)
+            out = [torch.as_tensor(inner[k]) for k in keys]
+            return tuple(out) + tuple(tracer.outputs)
+
+        previous = Distribution._validate_args
+        Distribution.set_default_validate_args(False)
+        try:
+            outputs = torch.func.vmap(per_sample, randomness="different")(
+                *[states[name] for name in names])
+        finally:
+            Distribution.set_default_validate_args(previous)
+        return tracer, keys, outputs
+
+    try:
+        tracer, keys, outputs = run(False)
+    except RuntimeError as error:
+        if not _needs_compat(error):
+            raise
+        tracer, keys, outputs = run(True)
+    values = outputs[:len(keys)]
+    failed = [check for check in tracer.checks
+              if not bool(outputs[len(keys) + check.output].all())]
+    if failed:
+        raise ValueError(failed[0].message)
+    for check in tracer.checks:
+        if check.memo is not None:
+            memo_commit(check.memo)
+    return State({k: v.to(device) for k, v in zip(keys, values)})

@@ -73,6 +73,8 @@ def check_constraint(constraint: Constraint, value: T) -> T:
         Elementwise indicator (aggregated over event dimensions) whether the constraint holds.
     """
     if not isinstance(value, torch.masked.MaskedTensor):
+        if isinstance(constraint, _PositiveDefinite):
+            return _positive_definite(value)
         return constraint.check(value)
 
     mask = value.get_mask()
@@ -121,3 +123,16 @@ def maybe_as_tensor(value: Any) -> torch.Tensor | None:
     if value is not None and isinstance(value, numbers.Number):
         return torch.as_tensor(value)
     return value
+
+
+from torch.distributions.constraints import _PositiveDefinite  # noqa: E402
+
+
+def _positive_definite(value: torch.Tensor) -> torch.Tensor:
+    """
+    ``constraints.positive_definite.check`` (torch constraints.py) without its host branch
+    (``if not sym_check.all()``), so that it also runs per particle under ``vmap``: symmetric
+    within torch's tolerance AND a successful Cholesky factorisation -- the same result.
+    """
+    symmetric = torch.isclose(value, value.mT, atol=1e-6).all(-2).all(-1)
+    return symmetric & torch.linalg.cholesky_ex(value).info.eq(0)

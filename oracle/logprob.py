@@ -217,3 +217,102 @@ def beta_draw_grads(x, c1, c0):
     d1 = dirichlet_grad(x, c1, tot) * (1.0 - x)
     d0 = -dirichlet_grad(w, c0, tot) * x
     return d1, d0
+
+
+# ---- families of the reference's examples (round 2) -------------------------------------------
+
+def gamma(a, r, v):
+    """
+    TORCH/distributions/gamma.py:90-99: xlogy(a, r) + xlogy(a - 1, v) - r v - lgamma(a).
+    Returns (lp, da, dr, dv).
+    """
+    a, r, v = (np.asarray(t, np.float64) for t in (a, r, v))
+    lp = _xlogy(a, r) + _xlogy(a - 1.0, v) - r * v - special.gammaln(a)
+    return lp, np.log(r) + np.log(v) - special.digamma(a), a / r - v, (a - 1.0) / v - r
+
+
+def poisson(rate, v):
+    """
+    TORCH/distributions/poisson.py:60-65: xlogy(v, rate) - rate - lgamma(v + 1).
+    Returns (lp, drate, dv) (dv: torch's continuous derivative).
+    """
+    rate, v = np.asarray(rate, np.float64), np.asarray(v, np.float64)
+    lp = _xlogy(v, rate) - rate - special.gammaln(v + 1.0)
+    return lp, v / rate - 1.0, np.log(rate) - special.digamma(v + 1.0)
+
+
+def inverse_gamma(a, r, y):
+    """
+    mininf/distributions.py:5-11 (Gamma through PowerTransform(-1)), i.e. TORCH
+    transformed_distribution.py log_prob: Gamma.log_prob(1 / y) - log|-y / x|, x = 1 / y.
+    Returns (lp, da, dr, dy).
+    """
+    a, r, y = (np.asarray(t, np.float64) for t in (a, r, y))
+    x = 1.0 / y
+    lp, da, dr, dx = gamma(a, r, x)
+    return lp - np.log(y / x), da, dr, -dx * x * x - 2.0 / y
+
+
+def gamma_entropy(a, r):
+    """
+    TORCH/distributions/gamma.py:101-107: a - log r + lgamma(a) + (1 - a) psi(a).
+    Returns (H, dH/da, dH/dr).
+    """
+    a, r = np.asarray(a, np.float64), np.asarray(r, np.float64)
+    h = a - np.log(r) + special.gammaln(a) + (1.0 - a) * special.digamma(a)
+    return h, 1.0 + (1.0 - a) * special.polygamma(1, a), -1.0 / r
+
+
+def standard_gamma_grad(alpha, x):
+    """
+    d x / d alpha of standard Gamma draws: TORCH/include/ATen/native/Distributions.h:310
+    (standard_gamma_grad_one, accumulation in double as on the CPU). Vectorised over inputs.
+    """
+    alpha = np.asarray(alpha, np.float64)
+    x = np.asarray(x, np.float64)
+    alpha, x = np.broadcast_arrays(alpha, x)
+    out = np.empty(alpha.shape)
+    f = np.float32
+    for idx in np.ndindex(alpha.shape):
+        a, xv = float(alpha[idx]), float(x[idx])
+        if xv < float(f(0.8)):
+            numer, denom = 1.0, a
+            s1, s2 = numer / denom, numer / (denom * denom)
+            for i in range(1, 6):
+                numer *= -xv / i
+                denom += 1.0
+                s1 += numer / denom
+                s2 += numer / (denom * denom)
+            pxa = xv ** a
+            pdf = xv ** (a - 1.0) * math.exp(-xv)
+            cdf = pxa * s1
+            cdf_a = (math.log(xv) - float(special.digamma(a))) * cdf - pxa * s2
+            res = -cdf_a / pdf
+            out[idx] = 0.0 if math.isnan(res) else res
+        elif a > 8.0:
+            if float(f(0.9)) * a <= xv <= float(f(1.1)) * a:
+                n1 = 1 + 24 * a * (1 + 12 * a)
+                n2 = 1440 * a * a + 6 * xv * (53 - 120 * xv) - 65 * xv * xv / a + \
+                    a * (107 + 3600 * xv)
+                out[idx] = n1 * n2 / (1244160 * a * a * a * a)
+            else:
+                den = math.sqrt(8 * a)
+                t2 = den / (a - xv)
+                t3 = (xv - a - a * math.log(xv / a)) ** -1.5
+                t23 = t2 - t3 if xv < a else t2 + t3
+                t1 = math.log(xv / a) * t23 - math.sqrt(2 / a) * (a + xv) / ((a - xv) ** 2)
+                stirling = 1 + 1 / (12 * a) * (1 + 1 / (24 * a))
+                out[idx] = -stirling * xv * t1 / den
+        else:
+            u, v = math.log(xv / a), math.log(a)
+            coef = ((0.16009398, -0.094634809, 0.025146376, -0.0030648343, 1, 0.32668115,
+                     0.10406089, 0.0014179084),
+                    (0.53487893, 0.1298071, 0.065735949, -0.0015649758, 0.16639465, 0.020070113,
+                     -0.0035938915, -0.00058392623),
+                    (0.040121004, -0.0065914022, -0.0026286047, -0.0013441777, 0.017050642,
+                     -0.0021309326, 0.00085092367, -1.5247877e-07))
+            c = [coef[0][i] + u * (coef[1][i] + u * coef[2][i]) for i in range(8)]
+            p = c[0] + v * (c[1] + v * (c[2] + v * c[3]))
+            q = c[4] + v * (c[5] + v * (c[6] + v * c[7]))
+            out[idx] = math.exp(p / q)
+    return out
