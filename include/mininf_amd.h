@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 5
+#define MI_ABI_VERSION 6
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -190,6 +190,40 @@ int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_by
 int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
                            float* total, double* site_lp, float* slot_grad, uint32_t* flags,
                            void* start_event, void* stop_event, void* stream);
+
+/* ---- deferred finalize reductions --------------------------------------------------------------
+ * A site launch ends with a fixed-order fp64 reduction of its per-(segment, particle) partials
+ *   part[(v * nseg + seg) * K + k],  v < num_sites: site log densities, then num_slots slot values
+ * into total[k] = sum_v scale[v] * sum_seg part (site_lp[v * K + k] the same per site, when
+ * non-NULL) and slot_grad[j * K + k] = slot_scale * sum_seg part[num_sites + j]. The *_deferred
+ * forms of the site launches skip that reduction when the segment list is at most
+ * MI_REDUCE_MAX_SEG long and describe it in *reduce instead (reduce->part == NULL: the launch
+ * reduced itself); mi_elbo_forward then runs it (mi_elbo.reduce) in the same launch as the ELBO's
+ * own reduction -- one kernel launch less per site launch. The partials live in the site launch's
+ * workspace, which must stay untouched until then. mi_reduce_launch runs a described reduction on
+ * its own (a caller that cannot hand it to the ELBO). */
+#define MI_MAX_REDUCE 4
+#define MI_REDUCE_MAX_SEG 1024
+typedef struct mi_reduce {
+  const float* part;
+  int64_t nseg;
+  int64_t K;
+  int32_t num_sites;
+  int32_t num_slots;
+  double scale[MI_MAX_SITES];
+  double slot_scale;
+  float* total;          /* [K] */
+  double* site_lp;       /* [num_sites, K] or NULL */
+  float* slot_grad;      /* [num_slots, K] (num_slots > 0) */
+} mi_reduce;
+
+/* mi_group_forward_timed with the finalize handed to the caller through *reduce (see above). */
+int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t workspace_bytes,
+                              float* total, double* site_lp, float* slot_grad, uint32_t* flags,
+                              void* start_event, void* stop_event, void* stream, mi_reduce* reduce);
+
+/* Run a deferred reduction as its own launch. */
+int mi_reduce_launch(const mi_reduce* reduce, void* stream);
 
 /* Where a fused-draw group leaves its partial sums (MI_GROUP_DRAW_PARTIALS): dloc partials are
  * rows [rows, N] at workspace + offset_bytes, dscale partials the next rows * N floats. */
@@ -378,6 +412,10 @@ int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t works
                             float* total, float* dslots, uint32_t* flags, void* start_event,
                             void* stop_event, void* stream);
 int mi_linear_struct_size(size_t* bytes);
+/* mi_linear_forward_timed with the finalize handed to the caller through *reduce (see mi_reduce). */
+int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
+                               float* total, float* dslots, uint32_t* flags, void* start_event,
+                               void* stop_event, void* stream, mi_reduce* reduce);
 
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 
@@ -457,7 +495,7 @@ typedef struct mi_elbo {
   int32_t num_terms;
   int32_t num_factors;
   int32_t num_buffers;
-  int32_t pad0;
+  int32_t num_reduce;
   float g0;
   float pad1;
   double entropy_scale;
@@ -465,7 +503,23 @@ typedef struct mi_elbo {
   mi_factor factors[MI_MAX_FACTORS];
   float* buffers[MI_MAX_BUFFERS];
   int64_t buffer_len[MI_MAX_BUFFERS];
+  /* deferred site finalize reductions (same K): mi_elbo_forward writes their outputs and adds
+   * g0 * sum_k total[k] of each to the loss (their totals are not listed in `terms`). Forward-
+   * absorbed Beta factors (MI_DRAW_SOURCES) must then have `dgrad`: their sums over the particles
+   * (which read slot gradients the reductions write) move to mi_elbo_backward. */
+  mi_reduce reduce[MI_MAX_REDUCE];
+  /* step_counter != NULL: after everything else, the launch's last block sets
+   * *step_snapshot = *step_counter and *step_counter += 1 (the generator step of this ELBO
+   * evaluation's draws -- read from step_counter in the forward, from step_snapshot afterwards). */
+  uint64_t* step_counter;
+  uint64_t* step_snapshot;
+  /* flags_mirror != NULL: the last block copies flags[0 .. nflags) there (e.g. host-mapped memory:
+   * the validation words of this evaluation without a separate device-to-host copy). */
+  const uint32_t* flags;
+  uint32_t* flags_mirror;
+  int64_t nflags;
 } mi_elbo;
+
 
 /* sizeof(mi_factor), sizeof(mi_elbo) as compiled. */
 int mi_elbo_struct_sizes(size_t* factor, size_t* elbo);
@@ -478,7 +532,8 @@ int mi_elbo_struct_sizes(size_t* factor, size_t* elbo);
 int mi_elbo_workspace_bytes(const mi_elbo* elbo, size_t* bytes);
 int mi_elbo_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 
-/* Writes the scalar loss (fp32, reduced in fp64 in a fixed order). */
+/* Writes the scalar loss (fp32, reduced in fp64 in a fixed order). MI_EUNSUPPORTED when num_reduce
+ * > 0 and a forward-absorbed Beta factor has no dgrad (see mi_elbo.reduce). */
 int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes, float* loss,
                     void* stream);
 

@@ -34,8 +34,10 @@ GROUP_DRAW_PARTIALS = 2
 TRANSFORM_NONE, TRANSFORM_EXP = 0, 1
 DRAW_NONE, DRAW_SOURCES, DRAW_PARTIALS = 0, 1, 2
 MAX_SOURCES = 4
+MAX_REDUCE = 4
+REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 5   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 6   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -126,13 +128,25 @@ class Params(ctypes.Structure):
                 ("transform", ctypes.c_int32 * MAX_PARAMS)]
 
 
+class Reduce(ctypes.Structure):
+    _fields_ = [
+        ("part", c_vp), ("nseg", c_i64), ("K", c_i64),
+        ("num_sites", ctypes.c_int32), ("num_slots", ctypes.c_int32),
+        ("scale", ctypes.c_double * MAX_SITES), ("slot_scale", ctypes.c_double),
+        ("total", c_vp), ("site_lp", c_vp), ("slot_grad", c_vp),
+    ]
+
+
 class Elbo(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("num_terms", ctypes.c_int32), ("num_factors", ctypes.c_int32),
-        ("num_buffers", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("num_buffers", ctypes.c_int32), ("num_reduce", ctypes.c_int32),
         ("g0", ctypes.c_float), ("pad1", ctypes.c_float), ("entropy_scale", ctypes.c_double),
         ("terms", c_vp * MAX_TERMS), ("factors", Factor * MAX_FACTORS),
         ("buffers", c_vp * MAX_BUFFERS), ("buffer_len", c_i64 * MAX_BUFFERS),
+        ("reduce", Reduce * MAX_REDUCE),
+        ("step_counter", c_vp), ("step_snapshot", c_vp),
+        ("flags", c_vp), ("flags_mirror", c_vp), ("nflags", c_i64),
     ]
 
 
@@ -146,6 +160,10 @@ _SIGNATURES = {
                                         c_vp, c_vp, c_vp]),
     "mi_group_forward_timed": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp,
                                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mi_group_forward_deferred": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t,
+                                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                 ctypes.POINTER(Reduce)]),
+    "mi_reduce_launch": (ctypes.c_int, [ctypes.POINTER(Reduce), c_vp]),
     "mi_group_draw_partials": (ctypes.c_int, [ctypes.POINTER(Group),
                                               ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(c_i64)]),
@@ -202,6 +220,9 @@ _SIGNATURES = {
                                          c_vp, c_vp]),
     "mi_linear_forward_timed": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t, c_vp,
                                                c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mi_linear_forward_deferred": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t,
+                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                  ctypes.POINTER(Reduce)]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

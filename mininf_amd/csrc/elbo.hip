@@ -16,6 +16,7 @@
 #include "beta_grad.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mi {
 
@@ -171,12 +172,27 @@ template <bool BETA>
 MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int tk,
                       double& s0, double& s1) {
   const int64_t n = F.n;
-  if (BETA && F.dgrad != nullptr) {   // factors precomputed by mi_beta_dgrad
-    for (int64_t k = r0; k < r1; k += tk) {
-      const double g = (double)source_sum(F, k, i);
-      if (g == 0.0) continue;   // as the evaluating branch: a zero upstream never meets the factor
-      s0 += g * F.dgrad[2 * (k * n + i)];
-      s1 += g * F.dgrad[2 * (k * n + i) + 1];
+  if ((BETA || F.family == MI_BETA) && F.dgrad != nullptr) {   // factors precomputed (mi_side,
+                                                               // mi_beta_dgrad)
+    // eight rows' loads in flight per lane, then the sums in row order
+    constexpr int kU = 8;
+    for (int64_t k0 = r0; k0 < r1; k0 += kU * (int64_t)tk) {
+      float g[kU];
+      double2 d[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t k = k0 + (int64_t)u * tk;
+        g[u] = k < r1 ? source_sum(F, k, i) : 0.0f;
+        d[u] = k < r1 ? *reinterpret_cast<const double2*>(F.dgrad + 2 * (k * n + i))
+                      : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (g[u] == 0.0f) continue;   // as the evaluating branch: a zero upstream never meets
+                                      // the factor
+        s0 += (double)g[u] * d[u].x;
+        s1 += (double)g[u] * d[u].y;
+      }
     }
   } else if (BETA) {
     const float a = F.param[0][i * F.stride[0]], b = F.param[1][i * F.stride[1]];
@@ -251,12 +267,18 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   red[threadIdx.x][0] = s0;
   red[threadIdx.x][1] = s1;
   __syncthreads();
-  if (ty == 0) {   // fixed-order sum over the block's particle lanes
-    s0 = s1 = 0.0;
-    for (int r = 0; r < tk; ++r) {
-      s0 += red[r * ti + tx][0];
-      s1 += red[r * ti + tx][1];
+  // fixed pairwise tree over the block's particle lanes (log2(tk) steps; a serial sum over 256
+  // lanes is a 256-long chain of dependent LDS reads and fp64 adds)
+  for (int half = tk >> 1; half > 0; half >>= 1) {
+    if (ty < half) {
+      red[threadIdx.x][0] += red[threadIdx.x + half * ti][0];
+      red[threadIdx.x][1] += red[threadIdx.x + half * ti][1];
     }
+    __syncthreads();
+  }
+  if (ty == 0) {
+    s0 = red[tx][0];
+    s1 = red[tx][1];
   }
   unsigned* counter = nullptr;
   if (slices > 1) {
@@ -265,13 +287,15 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
       part[((int64_t)slice * F.n + i) * 2] = s0;
       part[((int64_t)slice * F.n + i) * 2 + 1] = s1;
     }
-    __threadfence();
     __syncthreads();
     counter = counters + pick(P.counter, a) + col;
-    if (threadIdx.x == 0) *last = atomicAdd(counter, 1u) == (unsigned)slices - 1u;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the block's partials, then the count
+      *last = atomicAdd(counter, 1u) == (unsigned)slices - 1u;
+    }
     __syncthreads();
     if (!*last) return;
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (ty == 0 && i < F.n) {   // the column's last block: slices in a fixed order
       s0 = s1 = 0.0;
       for (int s = 0; s < slices; ++s) {
@@ -297,71 +321,323 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   if (counter != nullptr && threadIdx.x == 0) *counter = 0u;
 }
 
+// ---- deferred site finalize reductions (mi_elbo.reduce) ---------------------------------------
+// Block (job a, particle block kb, value v) sums part[v][seg][k] over the job's segments for 64
+// particles: 4 segment groups of 64 lanes, eight loads in flight per lane, partial sums in fp64
+// combined in a fixed order -- the arithmetic of sites.hip k_finalize, fused into this launch.
+// Jobs with one site value split their values over blocks (as k_finalize's split mode).
+// Long segment lists use blocks of 32 particles x 8 segment groups (more blocks, fewer serial load
+// rounds per lane; MININF_AMD_ELBO_KRED), short ones 64 particles x 4 groups.
+constexpr int kRedKWide = 64;
+
+// Completion counting of the forward's share-writing blocks in two levels: blocks count into the
+// counter of their group of kGroupBlocks, the last of a group into the launch counter -- a few
+// hundred blocks contending for one address would serialise on it.
+#ifndef MI_ELBO_RELEASE_FENCE
+#define MI_ELBO_RELEASE_FENCE 0
+#endif
+constexpr int kGroupBlocks = 32;
+constexpr int kGroupCounters = 64;        // groups: at most kGroupCounters * kGroupBlocks blocks
+constexpr int kGroupCounterWord = 16;     // first group counter (uint32 word)
+constexpr int kGroupCounterStride = 16;   // words between group counters (64 bytes)
+
+// Forward-absorbed Beta factors of one element (a global parameter's K draws, e.g. the coin's
+// theta) whose precomputed implicit-gradient factors dgrad[k] this launch sums against their
+// upstream g_k = sum_s source_s[k]: by linearity, every block that writes a source row (the slot
+// values of the reductions) or reads one written earlier (the lead blocks) adds its particles'
+// sum_k g_sk dgrad[k] to its own partial, and the last block adds the partials in a fixed order.
+constexpr int kMaxTails = 2;
+
+struct ReducePlan {
+  int external;                   // 1: the reductions ran as their own launches; add their totals
+  int num;
+  int first[MI_MAX_REDUCE + 1];   // first block of each job
+  int vblocks[MI_MAX_REDUCE];     // blocks per particle block: num values (split) or 1
+  int kred[MI_MAX_REDUCE];        // particles per block
+  int tails;                      // tail factors
+  int tail_slot[MI_MAX_REDUCE * MI_MAX_SLOTS];   // [a * MI_MAX_SLOTS + j], bit t: job a's slot
+                                                 // j is a source of tail t
+  int tail_ext[kMaxTails];        // bit s: source s of tail t is read by the lead blocks
+  int64_t tail_part;              // offset (doubles) of the [tails][nshare][2] partials
+  const double* tail_dgrad[kMaxTails];   // [K, 1, 2]
+  const float* tail_src[kMaxTails][MI_MAX_SOURCES];
+  int64_t tail_src_stride[kMaxTails][MI_MAX_SOURCES];
+  const float* tail_c1[kMaxTails];       // concentrations (n = 1)
+  const float* tail_c0[kMaxTails];
+  double* tail_saved[kMaxTails];
+};
+
+// Fixed-order tree sum over the first `n` (a power of two) entries of lds; result in lds[0].
+MI_DEV void lds_tree(double* lds, int n) {
+  for (int half = n >> 1; half > 0; half >>= 1) {
+    if ((int)threadIdx.x < half) lds[threadIdx.x] += lds[threadIdx.x + half];
+    __syncthreads();
+  }
+}
+
+// Block partials (c0, c1) of the tails from per-lane contributions (fixed-order wave sums, then the
+// waves in order); thread 0 stores them.
+MI_DEV void tail_partials(const ReducePlan& R, int bid, int nshare, const double (&c)[kMaxTails][2],
+                          double (*red)[2], double* work) {
+  constexpr int kWaves = kElboThreads / kWave;
+  double* lds = &red[0][0];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kMaxTails; ++t)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const double v = wave_sum(c[t][q]);
+      if (lane == 0) lds[(t * 2 + q) * kWaves + wave] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int t = 0; t < R.tails; ++t)
+      for (int q = 0; q < 2; ++q) {
+        double v = 0.0;
+        for (int w = 0; w < kWaves; ++w) v += lds[(t * 2 + q) * kWaves + w];
+        __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + bid) * 2 + q], v,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  __syncthreads();
+}
+
+// Writes job J's outputs for one block's particles (local block `local` of the job) and returns
+// g0 * the sum of its (fp32) totals (0 from blocks that do not write totals): the block's share of
+// the loss.
+MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kRedK,
+                         const ReducePlan& R, int a, double (&c)[kMaxTails][2],
+                         double (*red)[2]) {
+  const int kRedG = kElboThreads / kRedK;
+  const int nv = J.num_sites + J.num_slots;
+  const int64_t kb = local / vb;
+  const int v0 = vb > 1 ? local % vb : 0, v1 = vb > 1 ? v0 + 1 : nv;
+  const int kl = threadIdx.x % kRedK, gl = threadIdx.x / kRedK;
+  const int64_t K = J.K;
+  const int64_t k = kb * kRedK + kl;
+  const int64_t kc = k < K ? k : K - 1;
+  double* lds = &red[0][0];   // [kRedG][kRedK] doubles
+  double t = 0.0;
+  for (int v = v0; v < v1; ++v) {
+    const float* __restrict__ p = J.part + (int64_t)v * J.nseg * K + kc;
+    double acc = 0.0;
+    int64_t g = gl;
+    for (; g + 7 * kRedG < J.nseg; g += 8 * kRedG) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * K];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += (double)x[j];
+    }
+    for (; g < J.nseg; g += kRedG) acc += (double)p[g * K];
+    __syncthreads();
+    lds[gl * kRedK + kl] = acc;
+    __syncthreads();
+    if (gl == 0 && k < K) {
+      double s = 0.0;
+      for (int j = 0; j < kRedG; ++j) s += lds[j * kRedK + kl];
+      if (v < J.num_sites) {
+        s *= pick(J.scale, v);
+        if (J.site_lp != nullptr) J.site_lp[(int64_t)v * K + k] = s;
+        t += s;
+      } else {
+        const int j = v - J.num_sites;
+        const float gv = (float)(s * J.slot_scale);
+        J.slot_grad[(int64_t)j * K + k] = gv;
+        const int mask = j < MI_MAX_SLOTS ? pick(R.tail_slot, a * MI_MAX_SLOTS + j) : 0;
+#pragma unroll
+        for (int q = 0; q < kMaxTails; ++q)
+          if (((mask >> q) & 1) && gv != 0.0f) {   // a zero upstream never meets the factor
+            const double2 d = *reinterpret_cast<const double2*>(pick(R.tail_dgrad, q) + 2 * k);
+            c[q][0] += (double)gv * d.x;
+            c[q][1] += (double)gv * d.y;
+          }
+      }
+    }
+  }
+  double share = 0.0;
+  if (v0 == 0 && gl == 0 && k < K) {
+    const float tf = (float)t;
+    J.total[k] = tf;
+    share = (double)tf;
+  }
+  return (double)g0 * share;
+}
+
+MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
+                           double (&c)[kMaxTails][2], double (*red)[2]) {
+  int a = 0;
+#pragma unroll
+  for (int q = 1; q < MI_MAX_REDUCE; ++q)
+    if (q < R.num && bid >= R.first[q]) a = q;
+  const int local = bid - pick(R.first, a);
+  const int vb = pick(R.vblocks, a);
+  const int kred = pick(R.kred, a);
+  double share;
+  // constant descriptor indices (a run-time index into the by-value kernel argument would copy
+  // it to scratch memory)
+  switch (a) {
+    case 1: share = reduce_job(E.g0, E.reduce[1], local, vb, kred, R, 1, c, red); break;
+    case 2: share = reduce_job(E.g0, E.reduce[2], local, vb, kred, R, 2, c, red); break;
+    case 3: share = reduce_job(E.g0, E.reduce[3], local, vb, kred, R, 3, c, red); break;
+    default: share = reduce_job(E.g0, E.reduce[0], local, vb, kred, R, 0, c, red); break;
+  }
+  return share;
+}
+
 // ---- forward --------------------------------------------------------------------------------
 // HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
 // of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
-template <bool HAS_BETA>
+// ABSORB: the launch has forward-absorbed Beta blocks (absorbed_block<true>, inline fp64 implicit
+// gradients: a large register footprint the other variants do not pay for).
+template <bool HAS_BETA, bool ABSORB>
 __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                                                const AbsorbPlan P,
+                                                               const ReducePlan R,
                                                                double* __restrict__ work,
                                                                unsigned* __restrict__ counters,
                                                                float* __restrict__ loss) {
   __shared__ double red[kElboThreads][2];
   __shared__ bool last;
+  const int nred = R.first[R.num];
   const int nloss = P.lead_blocks;
-  if (HAS_BETA && (int)blockIdx.x >= nloss) {
-    absorbed_block<true>(E, P, (int)blockIdx.x - nloss, 1.0f, counters, work, red, &last);
+  const int nshare = nred + nloss;   // blocks that write a loss share
+  if (ABSORB && (int)blockIdx.x >= nshare) {
+    absorbed_block<true>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
     return;
   }
   double* rsum = &red[0][0];
-  const int64_t stride = (int64_t)nloss * kElboThreads;
-  const int64_t first = (int64_t)blockIdx.x * kElboThreads + threadIdx.x;
-  double lp = 0.0, h = 0.0;
-  for (int t = 0; t < E.num_terms; ++t)
-    for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
-  for (int f = 0; f < E.num_factors; ++f) {
-    const mi_factor& F = E.factors[f];
-    if (!HAS_BETA || F.family == MI_NORMAL) {
-      // sum_i (0.5 + 0.5 log(2 pi) + log scale_i): the constant once, the logs per element
-      const float* __restrict__ sc = F.param[1];
-      const int64_t ss = F.stride[1];
-      float hf = 0.0f;   // per-thread partial of a few terms, then fp64
-      int64_t head = 0;
-      if (ss == 1 && (reinterpret_cast<uintptr_t>(sc) & 15) == 0) {
-        // 16-byte loads, all issued before the logs
-        const int64_t nq = F.n >> 2;
-        const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
-        for (int64_t q = first; q < nq; q += stride) {
-          const float4 v = sq[q];
-          hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
+  double share;
+  double c[kMaxTails][2] = {};   // this lane's tail contributions
+  if (!ABSORB && (int)blockIdx.x < nred) {   // (ABSORB launches have no deferred reductions)
+    share = reduce_block(E, R, (int)blockIdx.x, c, red);
+    __syncthreads();
+  } else {
+    const int64_t lead = (int64_t)blockIdx.x - nred;
+    const int64_t stride = (int64_t)nloss * kElboThreads;
+    const int64_t first = lead * kElboThreads + threadIdx.x;
+    double lp = 0.0, h = 0.0;
+    for (int t = 0; t < E.num_terms; ++t)
+      for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
+    if (R.external) {
+#pragma unroll
+      for (int a = 0; a < MI_MAX_REDUCE; ++a)
+        if (a < R.num)
+          for (int64_t k = first; k < E.K; k += stride) lp += (double)E.reduce[a].total[k];
+    }
+    for (int f = 0; f < E.num_factors; ++f) {
+      const mi_factor& F = E.factors[f];
+      if (!HAS_BETA || F.family == MI_NORMAL) {
+        // sum_i (0.5 + 0.5 log(2 pi) + log scale_i): the constant once, the logs per element
+        const float* __restrict__ sc = F.param[1];
+        const int64_t ss = F.stride[1];
+        float hf = 0.0f;   // per-thread partial of a few terms, then fp64
+        int64_t head = 0;
+        if (ss == 1 && (reinterpret_cast<uintptr_t>(sc) & 15) == 0) {
+          // 16-byte loads, all issued before the logs
+          const int64_t nq = F.n >> 2;
+          const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
+          for (int64_t q = first; q < nq; q += stride) {
+            const float4 v = sq[q];
+            hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
+          }
+          head = nq << 2;
         }
-        head = nq << 2;
+        for (int64_t i = head + first; i < F.n; i += stride) hf += logf(sc[i * ss]);
+        h += (double)hf;
+        if (first == 0) h += 1.4189385332046727 * (double)F.n;
+      } else {
+        for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i);
       }
-      for (int64_t i = head + first; i < F.n; i += stride) hf += logf(sc[i * ss]);
-      h += (double)hf;
-      if (first == 0) h += 1.4189385332046727 * (double)F.n;
-    } else {
-      for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i);
+    }
+    share = (double)E.g0 * lp - E.entropy_scale * h;
+    if (!ABSORB) {   // tail sources written by earlier launches
+#pragma unroll
+      for (int q = 0; q < kMaxTails; ++q) {
+        const int mask = q < R.tails ? R.tail_ext[q] : 0;
+        if (mask == 0) continue;
+        for (int64_t k = first; k < E.K; k += stride) {
+          float g = 0.0f;
+#pragma unroll
+          for (int src = 0; src < MI_MAX_SOURCES; ++src)
+            if ((mask >> src) & 1) g += R.tail_src[q][src][k * R.tail_src_stride[q][src]];
+          if (g == 0.0f) continue;   // a zero upstream never meets the factor
+          const double2 d = *reinterpret_cast<const double2*>(R.tail_dgrad[q] + 2 * k);
+          c[q][0] += (double)g * d.x;
+          c[q][1] += (double)g * d.y;
+        }
+      }
     }
   }
-  const double s = block_sum((double)E.g0 * lp - E.entropy_scale * h, rsum);
+  if (!ABSORB && R.tails > 0) tail_partials(R, (int)blockIdx.x, nshare, c, red, work);
+  const double s = block_sum(share, rsum);
   if (threadIdx.x == 0) {
-    work[blockIdx.x] = s;
-    __threadfence();
-    last = atomicAdd(counters, 1u) == (unsigned)nloss - 1u;
+    // The shares (and the slot gradients the tail reads) are device-coherent stores, complete
+    // (s_waitcnt) before the barrier / the counter update: no per-block L2 write-back fence,
+    // which serialises over a few hundred reducing blocks.
+    __hip_atomic_store(&work[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MI_ELBO_RELEASE_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_s_waitcnt(0);
+    const int group = (int)blockIdx.x / kGroupBlocks;
+    const int ngroups = (nshare + kGroupBlocks - 1) / kGroupBlocks;
+    const unsigned in_group = (unsigned)min(kGroupBlocks, nshare - group * kGroupBlocks);
+    unsigned* gc = counters + kGroupCounterWord + group * kGroupCounterStride;
+    bool done = true;
+    if (ngroups > 1) {
+      done = atomicAdd(gc, 1u) == in_group - 1u;
+      if (done) *gc = 0u;   // reset for the next launch (no other block of the group is left)
+    }
+    last = done && atomicAdd(counters, 1u) == (unsigned)(ngroups > 1 ? ngroups : nshare) - 1u;
   }
   __syncthreads();
-  if (last) {
-    // the last block adds the partials: each thread a fixed strided subset, then a fixed-order
-    // block sum -- deterministic, and no serial chain of dependent loads
-    __threadfence();
-    double t = 0.0;
-    for (int b = threadIdx.x; b < nloss; b += kElboThreads) t += work[b];
-    const double total = block_sum(t, rsum + kElboThreads / kWave);
-    if (threadIdx.x == 0) {
-      *loss = (float)total;
-      *counters = 0u;
+  if (!last) return;
+  // the last block adds the shares: each thread a fixed strided subset, then a fixed-order block
+  // sum -- deterministic, and no serial chain of dependent loads
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double t = 0.0;
+  for (int b = threadIdx.x; b < nshare; b += kElboThreads)
+    t += __hip_atomic_load(&work[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double total = block_sum(t, rsum + kElboThreads / kWave);
+  if (threadIdx.x == 0) {
+    *loss = (float)total;
+    *counters = 0u;
+  }
+  if (!ABSORB) {
+#pragma unroll
+    for (int q = 0; q < kMaxTails; ++q) {
+      if (q >= R.tails) break;
+      double sum[2];
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        double acc = 0.0;
+        for (int b = threadIdx.x; b < nshare; b += kElboThreads)
+          acc += __hip_atomic_load(&work[R.tail_part + ((int64_t)q * nshare + b) * 2 + c2],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        rsum[threadIdx.x] = acc;
+        __syncthreads();
+        lds_tree(rsum, kElboThreads);
+        sum[c2] = rsum[0];
+      }
+      if (threadIdx.x == 0) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
+        const float a = *R.tail_c1[q], b = *R.tail_c0[q];
+        const float tsum = a + b;
+        const float tt = (tsum - 2.0f) * trigammaf(tsum);
+        double* pre = R.tail_saved[q];
+        pre[0] = sum[0];
+        pre[1] = sum[1];
+        pre[2] = (double)(tt - (a - 1.0f) * trigammaf(a));
+        pre[3] = (double)(tt - (b - 1.0f) * trigammaf(b));
+      }
     }
+  }
+  static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=
+                    MI_ELBO_COUNTER_BYTES / sizeof(unsigned), "counter area");
+  for (int64_t i = threadIdx.x; i < E.nflags; i += kElboThreads) E.flags_mirror[i] = E.flags[i];
+  if (threadIdx.x == 0 && E.step_counter != nullptr) {
+    const uint64_t c = *E.step_counter;
+    *E.step_snapshot = c;
+    *E.step_counter = c + 1;
   }
 }
 
@@ -440,11 +716,21 @@ bool forward_absorbed(const mi_factor& F) {
   return F.family == MI_BETA && F.draw_kind == MI_DRAW_SOURCES;
 }
 
+bool valid_reduce(const mi_elbo* e, const mi_reduce& r) {
+  return r.part != nullptr && r.total != nullptr && r.K == e->K && r.nseg >= 1 &&
+         r.nseg <= MI_REDUCE_MAX_SEG && r.num_sites >= 1 && r.num_sites <= MI_MAX_SITES &&
+         r.num_slots >= 0 && (r.num_slots == 0 || r.slot_grad != nullptr);
+}
+
 bool valid(const mi_elbo* e) {
   if (e == nullptr || e->K < 1 || e->num_terms < 0 || e->num_terms > MI_MAX_TERMS ||
       e->num_factors < 0 || e->num_factors > MI_MAX_FACTORS || e->num_buffers < 0 ||
-      e->num_buffers > MI_MAX_BUFFERS)
+      e->num_buffers > MI_MAX_BUFFERS || e->num_reduce < 0 || e->num_reduce > MI_MAX_REDUCE ||
+      e->nflags < 0 || (e->nflags > 0 && (e->flags == nullptr || e->flags_mirror == nullptr)) ||
+      ((e->step_counter == nullptr) != (e->step_snapshot == nullptr)))
     return false;
+  for (int r = 0; r < e->num_reduce; ++r)
+    if (!valid_reduce(e, e->reduce[r])) return false;
   for (int t = 0; t < e->num_terms; ++t)
     if (e->terms[t] == nullptr) return false;
   for (int f = 0; f < e->num_factors; ++f)
@@ -470,8 +756,9 @@ int64_t longest_factor(const mi_elbo* e) {
 
 
 // Counter words (uint32) of the workspace: [0] the forward loss counter, absorbed-draw columns
-// from kCounterFirst on.
-constexpr int64_t kCounterFirst = 64;
+// from kCounterFirst on; the forward's group counters (kGroupCounters words, 64 bytes apart) in
+// between.
+constexpr int64_t kCounterFirst = mi::kGroupCounterWord + mi::kGroupCounters * mi::kGroupCounterStride;
 constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned);
 
 // Launch plans of both kernels and the layout of the fp64 work area that follows the counters:
@@ -479,17 +766,20 @@ constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned);
 // of one launch; what the backward needs from the forward lives in the caller's mi_factor.saved.
 struct Layout {
   mi::AbsorbPlan fwd, bwd;
+  mi::ReducePlan red;
   int64_t doubles;
 };
 
-void add_absorbed(const mi_elbo* e, int f, bool forward, mi::AbsorbPlan& P, int64_t& counters,
-                  int64_t& doubles, int& blocks) {
+// finish: the backward only combines the sums the forward left in F.saved
+void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::AbsorbPlan& P,
+                  int64_t& counters, int64_t& doubles, int& blocks) {
   const mi_factor& F = e->factors[f];
   const int a = P.num++;
   P.index[a] = f;
   P.first[a] = blocks;
   P.pre[a] = 0;
-  if (!forward && forward_absorbed(F)) {   // finish only: one element per thread
+  if (!forward && finish) {   // finish only: one element per thread
+    P.pre[a] = 1;
     P.ti[a] = mi::kElboThreads;
     P.gx[a] = (int)ceil_div(F.n, mi::kElboThreads);
     P.slices[a] = 1;
@@ -502,9 +792,9 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, mi::AbsorbPlan& P, int6
   while (ti < 64 && ti < F.n) ti <<= 1;
   const int tk = mi::kElboThreads / ti;
   const int64_t gx = ceil_div(F.n, ti);
-  // rows per particle lane: one Beta gradient per thread (long fp64 chains) unless mi_beta_dgrad
-  // precomputed them, a few otherwise
-  const int64_t per_lane = (forward_absorbed(F) && F.dgrad == nullptr) ? 1 : 4;
+  // rows per particle lane: one Beta gradient per thread (long fp64 chains) unless they were
+  // precomputed (then 16: a column's sums usually fit one block, no cross-block completion)
+  const int64_t per_lane = !forward_absorbed(F) ? 4 : (F.dgrad == nullptr ? 1 : 16);
   int64_t slices = ceil_div(rows, (int64_t)tk * per_lane);
   slices = std::max<int64_t>(1, std::min<int64_t>(slices, ceil_div(2048, gx)));
   if (slices > 1 && counters + gx > kMaxCounters) slices = 1;
@@ -523,6 +813,16 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, mi::AbsorbPlan& P, int6
   blocks += (int)(gx * slices);
 }
 
+// particles per reducing block for long segment lists (MININF_AMD_ELBO_KRED: 16, 32 or 64)
+int env_kred() {
+  static const int v = [] {
+    const char* e = getenv("MININF_AMD_ELBO_KRED");
+    const int n = e != nullptr ? atoi(e) : 32;   // measured on MI355X (C2): 16 / 32 / 64
+    return (n == 16 || n == 32 || n == 64) ? n : 32;
+  }();
+  return v;
+}
+
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
   L.fwd.lead_blocks = (int)blocks_for(std::max(e->K, longest_factor(e)), mi::kElboMaxBlocks);
@@ -531,21 +831,75 @@ Layout make_layout(const mi_elbo* e) {
     if (e->factors[f].draw_kind == MI_DRAW_NONE) longest = std::max(longest, e->factors[f].n);
   for (int b = 0; b < e->num_buffers; ++b) longest = std::max(longest, e->buffer_len[b]);
   L.bwd.lead_blocks = (int)blocks_for(longest, 2048);
+  int nred = 0;
+  L.red.num = e->num_reduce;
+  for (int r = 0; r < e->num_reduce; ++r) {
+    const mi_reduce& J = e->reduce[r];
+    L.red.first[r] = nred;
+    L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
+    L.red.kred[r] = (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred() : mi::kRedKWide;
+    nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
+  }
+  L.red.first[L.red.num] = nred;
+  if (nred + L.fwd.lead_blocks > mi::kGroupCounters * mi::kGroupBlocks) {
+    // too many blocks for the completion counters: mi_elbo_forward launches the reductions on
+    // their own first and the lead blocks add the totals
+    L.red.external = 1;
+    for (int r = 0; r <= L.red.num; ++r) L.red.first[r] = 0;
+    nred = 0;
+  }
+  // With deferred reductions, forward-absorbed Beta factors (which read slot gradients the
+  // reductions write) are summed in this launch when they are tails (one element, dgrad
+  // precomputed), else in the backward launch (mi_elbo_forward checked that they have dgrad).
+  const bool deferred = e->num_reduce > 0;
+  const int nshare = nred + L.fwd.lead_blocks;
+  bool tail[MI_MAX_FACTORS] = {};
+  if (deferred)
+    for (int f = 0; f < e->num_factors; ++f) {
+      const mi_factor& F = e->factors[f];
+      if (!forward_absorbed(F) || F.dgrad == nullptr || F.n != 1 || L.red.tails >= mi::kMaxTails)
+        continue;
+      const int t = L.red.tails++;
+      tail[f] = true;
+      L.red.tail_dgrad[t] = F.dgrad;
+      L.red.tail_c1[t] = F.param[0];
+      L.red.tail_c0[t] = F.param[1];
+      L.red.tail_saved[t] = F.saved;
+      for (int src = 0; src < F.num_sources; ++src) {
+        const mi_source& S = F.source[src];
+        bool matched = false;
+        for (int r = 0; r < e->num_reduce && !L.red.external && S.stride_k == 1; ++r) {
+          const mi_reduce& J = e->reduce[r];
+          for (int j = 0; j < J.num_slots && j < MI_MAX_SLOTS; ++j)
+            if (S.ptr == J.slot_grad + (int64_t)j * J.K) {
+              L.red.tail_slot[r * MI_MAX_SLOTS + j] |= 1 << t;
+              matched = true;
+            }
+        }
+        if (!matched) {
+          L.red.tail_ext[t] |= 1 << src;
+          L.red.tail_src[t][src] = S.ptr;
+          L.red.tail_src_stride[t][src] = S.stride_k;
+        }
+      }
+    }
   int64_t counters = kCounterFirst;
-  int64_t doubles = (L.fwd.lead_blocks + 31) / 32 * 32;
+  int64_t doubles = (nshare + 31) / 32 * 32;
+  L.red.tail_part = doubles;
+  doubles += (int64_t)L.red.tails * nshare * 2;
   int blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
-    if (forward_absorbed(e->factors[f]))
-      add_absorbed(e, f, true, L.fwd, counters, doubles, blocks);
+    if (forward_absorbed(e->factors[f]) && !deferred)
+      add_absorbed(e, f, true, false, L.fwd, counters, doubles, blocks);
   L.fwd.first[L.fwd.num] = blocks;
   for (int a = 0; a < L.fwd.num; ++a) L.fwd.pre[a] = 1;   // writes F.saved
   blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind != MI_DRAW_NONE) {
-      add_absorbed(e, f, false, L.bwd, counters, doubles, blocks);
-      if (forward_absorbed(e->factors[f]))
-        for (int a = 0; a < L.fwd.num; ++a)
-          if (L.fwd.index[a] == f) L.bwd.pre[L.bwd.num - 1] = L.fwd.pre[a];
+      // the forward left the sums in F.saved: its absorbed blocks (no deferred reductions) or
+      // its tail partials
+      const bool finish = forward_absorbed(e->factors[f]) && (!deferred || tail[f]);
+      add_absorbed(e, f, false, finish, L.bwd, counters, doubles, blocks);
     }
   L.bwd.first[L.bwd.num] = blocks;
   L.doubles = doubles;
@@ -585,19 +939,32 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
                     void* stream) {
   if (!valid(elbo) || loss == nullptr || workspace == nullptr) return MI_EINVAL;
   if (workspace_bytes < workspace_need(elbo)) return MI_EWORKSPACE;
+  if (elbo->num_reduce > 0)
+    for (int f = 0; f < elbo->num_factors; ++f)
+      if (forward_absorbed(elbo->factors[f]) && elbo->factors[f].dgrad == nullptr)
+        return MI_EUNSUPPORTED;
   const Layout L = make_layout(elbo);
   auto* counters = static_cast<unsigned*>(workspace);
   auto* work = reinterpret_cast<double*>(static_cast<char*>(workspace) + MI_ELBO_COUNTER_BYTES);
+  if (L.red.external)
+    for (int r = 0; r < elbo->num_reduce; ++r) {
+      const int rc = mi_reduce_launch(&elbo->reduce[r], stream);
+      if (rc != 0) return rc;
+    }
   bool has_beta = false;
   for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family != MI_NORMAL;
-  const dim3 grid((unsigned)(L.fwd.lead_blocks + L.fwd.first[L.fwd.num]));
+  const dim3 grid((unsigned)(L.red.first[L.red.num] + L.fwd.lead_blocks + L.fwd.first[L.fwd.num]));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (has_beta)
-    hipLaunchKernelGGL(mi::k_elbo_forward<true>, grid, dim3(mi::kElboThreads), 0, s, *elbo,
-                       L.fwd, work, counters, loss);
+  const dim3 block(mi::kElboThreads);
+  if (L.fwd.num > 0)
+    hipLaunchKernelGGL((mi::k_elbo_forward<true, true>), grid, block, 0, s, *elbo, L.fwd, L.red,
+                       work, counters, loss);
+  else if (has_beta)
+    hipLaunchKernelGGL((mi::k_elbo_forward<true, false>), grid, block, 0, s, *elbo, L.fwd, L.red,
+                       work, counters, loss);
   else
-    hipLaunchKernelGGL(mi::k_elbo_forward<false>, grid, dim3(mi::kElboThreads), 0, s, *elbo,
-                       L.fwd, work, counters, loss);
+    hipLaunchKernelGGL((mi::k_elbo_forward<false, false>), grid, block, 0, s, *elbo, L.fwd,
+                       L.red, work, counters, loss);
   return to_code(hipGetLastError());
 }
 

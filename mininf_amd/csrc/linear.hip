@@ -590,6 +590,14 @@ int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes) {
 int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t workspace_bytes,
                             float* total, float* dslots, uint32_t* flags, void* start_event,
                             void* stop_event, void* stream) {
+  return mi_linear_forward_deferred(site, workspace, workspace_bytes, total, dslots, flags,
+                                    start_event, stop_event, stream, nullptr);
+}
+
+int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
+                               float* total, float* dslots, uint32_t* flags, void* start_event,
+                               void* stop_event, void* stream, mi_reduce* reduce) {
+  if (reduce != nullptr) *reduce = mi_reduce{};
   if (!valid(site) || total == nullptr || flags == nullptr ||
       (site->compute_grads && dslots == nullptr))
     return MI_EINVAL;
@@ -615,6 +623,18 @@ int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t works
   if (stop_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s)) != hipSuccess)
     return to_code(e);
   const double scale = site->site_scale;
+  if (reduce != nullptr && g.ntile <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
+    reduce->part = part;
+    reduce->nseg = g.ntile;
+    reduce->K = site->K;
+    reduce->num_sites = 1;
+    reduce->num_slots = site->compute_grads ? g.nv - 1 : 0;
+    reduce->scale[0] = scale;
+    reduce->slot_scale = (double)site->grad_scale;
+    reduce->total = total;
+    reduce->slot_grad = dslots;
+    return 0;
+  }
   double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) + partial_bytes(site, g));
   return mi_launch_finalize(part, g.ntile, site->K, 1, site->compute_grads ? g.nv - 1 : 0, &scale,
                             (double)site->grad_scale, total, nullptr, dslots, scratch, s);

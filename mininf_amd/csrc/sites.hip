@@ -1227,6 +1227,15 @@ int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_by
 int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
                            float* total, double* site_lp, float* slot_grad, uint32_t* flags,
                            void* start_event, void* stop_event, void* stream) {
+  return mi_group_forward_deferred(group, workspace, workspace_bytes, total, site_lp, slot_grad,
+                                   flags, start_event, stop_event, stream, nullptr);
+}
+
+int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t workspace_bytes,
+                              float* total, double* site_lp, float* slot_grad, uint32_t* flags,
+                              void* start_event, void* stop_event, void* stream,
+                              mi_reduce* reduce) {
+  if (reduce != nullptr) *reduce = mi_reduce{};
   if (!validate_group(group) || total == nullptr || flags == nullptr) return MI_EINVAL;
   if (group->num_slots > 0 && slot_grad == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -1348,10 +1357,34 @@ int mi_group_forward_timed(const mi_group* group, void* workspace, size_t worksp
   }
   double scales[MI_MAX_SITES];
   for (int i = 0; i < reduced_lp; ++i) scales[i] = prescaled ? 1.0 : G.sites[i].scale;
+  if (reduce != nullptr && p.nseg <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
+    reduce->part = part;
+    reduce->nseg = p.nseg;
+    reduce->K = G.K;
+    reduce->num_sites = reduced_lp;
+    reduce->num_slots = G.num_slots;
+    for (int i = 0; i < reduced_lp; ++i) reduce->scale[i] = scales[i];
+    reduce->slot_scale = (double)G.grad_scale;
+    reduce->total = total;
+    reduce->site_lp = site_lp;
+    reduce->slot_grad = slot_grad;
+    return 0;
+  }
   double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) +
                                               finalize_offset(group, p));
   return mi_launch_finalize(part, p.nseg, G.K, reduced_lp, G.num_slots, scales,
                             (double)G.grad_scale, total, site_lp, slot_grad, scratch, s);
+}
+
+int mi_reduce_launch(const mi_reduce* r, void* stream) {
+  if (r == nullptr || r->part == nullptr || r->nseg < 1 || r->K < 1 || r->total == nullptr ||
+      r->num_sites < 1 || r->num_sites > MI_MAX_SITES || r->num_slots < 0 ||
+      (r->num_slots > 0 && r->slot_grad == nullptr) || r->nseg > MI_REDUCE_MAX_SEG)
+    return MI_EINVAL;
+  // nseg <= MI_REDUCE_MAX_SEG: the one-launch finalize (no chunk scratch)
+  return mi_launch_finalize(r->part, r->nseg, r->K, r->num_sites, r->num_slots, r->scale,
+                            r->slot_scale, r->total, r->site_lp, r->slot_grad, nullptr,
+                            static_cast<hipStream_t>(stream));
 }
 
 int mi_group_draw_partials(const mi_group* group, size_t* offset_bytes, int64_t* rows) {

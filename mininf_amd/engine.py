@@ -342,10 +342,13 @@ class _GroupLauncher:
             raise nat.NativeError("site program failed to compile:\n" + log.value.decode())
         return log.value.decode()
 
-    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None):
+    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None,
+            defer: bool = False):
         """
         Launch the group. ``flags``: an already-zeroed int32 slice (one word per site) to write the
-        validation flags into, e.g. part of one buffer for every group of a step.
+        validation flags into, e.g. part of one buffer for every group of a step. ``defer``: leave
+        the finalize reduction to the caller when the library allows (``self.reduce``, an
+        ``mi_reduce``; None when the launch reduced itself).
         """
         device = self.device
         K, N = self.K, self.N
@@ -384,11 +387,14 @@ class _GroupLauncher:
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
-        nat.check(lib.mi_group_forward_timed(
+        reduce = nat.Reduce()
+        nat.check(lib.mi_group_forward_deferred(
             ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
             nat.ptr(site_lp), slot_grad.data_ptr(), flags.data_ptr(),
             None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
-            nat.stream_handle(device)), "mi_group_forward_timed")
+            nat.stream_handle(device), ctypes.byref(reduce) if defer else None),
+            "mi_group_forward_deferred")
+        self.reduce = reduce if defer and reduce.part else None
         self.workspace = workspace
         self.partials = None
         if group.options & nat.GROUP_DRAW_PARTIALS:
@@ -552,7 +558,8 @@ class _LinearLauncher:
         L.compute_grads = int(compute_grads)
         return L
 
-    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None):
+    def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None,
+            defer: bool = False):
         device = self.device
         L = self.describe(compute_grads)
         size = ctypes.c_size_t()
@@ -571,11 +578,14 @@ class _LinearLauncher:
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
-        nat.check(lib.mi_linear_forward_timed(
+        reduce = nat.Reduce()
+        nat.check(lib.mi_linear_forward_deferred(
             ctypes.byref(L), workspace.data_ptr(), size.value, total.data_ptr(), nat.ptr(dslots),
             flags.data_ptr(), None if start is None else start.cuda_event,
-            None if stop is None else stop.cuda_event, nat.stream_handle(device)),
-            "mi_linear_forward_timed")
+            None if stop is None else stop.cuda_event, nat.stream_handle(device),
+            ctypes.byref(reduce) if defer else None), "mi_linear_forward_deferred")
+        self.reduce = reduce if defer and reduce.part else None
+        self.workspace = workspace   # holds the deferred partials
         return total, dslots, flags
 
     def grads(self, dslots: Optional[torch.Tensor]) -> List[Optional[torch.Tensor]]:
@@ -662,6 +672,7 @@ class LogJoint:
     checks: list
     flags: Optional[torch.Tensor] = None      # int32, one word per pending site, in order
     sticky: bool = False                      # flags are never zeroed by a replay (graph mode)
+    mirror: Optional[torch.Tensor] = None     # host copy of `flags` the ELBO forward writes
 
     def flag_vector(self) -> Optional[torch.Tensor]:
         """
@@ -1035,9 +1046,16 @@ class _ElboPlan:
                  fallback: List[torch.Tensor], factors: List[EntropyFactor],
                  entropy_scale: float, linears: Optional[List[_LinearLauncher]] = None,
                  absorbed: Optional[Dict[int, _Absorbed]] = None,
-                 zeroed_flags: Optional[torch.Tensor] = None) -> None:
+                 zeroed_flags: Optional[torch.Tensor] = None,
+                 step_words: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                 mirror: Optional[torch.Tensor] = None) -> None:
         self.K, self.g0, self.device = K, g0, device
         self.zeroed_flags = zeroed_flags
+        # (counter, snapshot): the generator words the ELBO forward advances (mi_elbo.step_counter)
+        self.step_words = step_words
+        # host-mapped copy of the validation words written by the ELBO forward (mi_elbo.flags_mirror)
+        self.mirror = mirror
+        self.recompute = False
         self.launchers = launchers
         self.categorical = categorical
         self.linears = linears or []
@@ -1140,7 +1158,7 @@ class _ElboPlan:
             else:
                 d.eps = nat.ptr(cfg.noise)
                 d.seed, d.step = guide._philox_key(cfg)
-                d.step_device = nat.ptr(cfg.step_device)
+                d.step_device = nat.ptr(guide.backward_step(cfg))   # read by the ELBO backward
                 d.stream_id = cfg.stream_id
                 d.particle_offset = cfg.particle_offset
             d.num_sources = len(plan.uses)
@@ -1165,6 +1183,7 @@ class _ElboPlan:
         terms: List[torch.Tensor] = []
         buffers: List[torch.Tensor] = []
         results = []
+        deferred: List[Tuple[nat.Reduce, torch.Tensor]] = []   # finalize reductions left to us
         # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
         sizes = [1] * (len(self.categorical) + len(self.linears)) + \
             [len(l.sites) for l in self.launchers]
@@ -1190,7 +1209,9 @@ class _ElboPlan:
                 job.drawn.base.reshape(self.K, job.drawn.N), job.drawn.conc)
             part = self.flags[cursor:cursor + len(launcher.sites)]
             cursor += len(launcher.sites)
-            total, site_lp, grads, slot_grad, flags = launcher.run(need, part)
+            total, site_lp, grads, slot_grad, flags = launcher.run(need, part, defer=True)
+            if launcher.reduce is not None:
+                deferred.append((launcher.reduce, total))
             if job is not None and launcher.side_out is not None:
                 job.side_dgrad = launcher.side_out
                 side_jobs.pop(0)
@@ -1231,7 +1252,9 @@ class _ElboPlan:
         base = len(self.categorical)
         for j, (linear, holder) in enumerate(zip(self.linears, self.lin_holders)):
             total, dslots, flags = linear.run(linear.needs_grads(),
-                                              self.flags[base + j:base + j + 1])
+                                              self.flags[base + j:base + j + 1], defer=True)
+            if linear.reduce is not None:
+                deferred.append((linear.reduce, total))
             holder["flags"] = flags
             terms.append(total)
             if dslots is not None:
@@ -1246,6 +1269,20 @@ class _ElboPlan:
                         buffers.append(dslots[linear.P:])
             lin_results.append(dslots)
         terms.extend(t.contiguous() for t in self.fallback)
+        # The deferred reductions run inside the ELBO forward (their totals then leave `terms`)
+        # unless there are too many, or a forward-absorbed Beta factor lacks its precomputed
+        # implicit-gradient factors (mi_elbo.reduce); otherwise each runs as its own launch.
+        fused = self._reduce_ok() and len(deferred) <= nat.MAX_REDUCE and \
+            os.environ.get("MININF_AMD_FUSE_REDUCE", "1") != "0"
+        lib = nat.lib()
+        if fused:
+            reduced = {id(t) for _, t in deferred}
+            terms = [t for t in terms if id(t) not in reduced]
+        else:
+            stream = nat.stream_handle(self.device)
+            for job, _ in deferred:
+                nat.check(lib.mi_reduce_launch(ctypes.byref(job), stream), "mi_reduce_launch")
+            deferred = []
         if len(terms) > nat.MAX_TERMS:
             head = nat.MAX_TERMS - 1
             terms = terms[:head] + [torch.stack(terms[head:]).sum(0)]
@@ -1253,8 +1290,17 @@ class _ElboPlan:
         buffers = buffers[:nat.MAX_BUFFERS]
         E = self._describe(terms, buffers)
         self._describe_absorbed(E, results, lin_results)
+        E.num_reduce = len(deferred)
+        for j, (job, _) in enumerate(deferred):
+            E.reduce[j] = job
+        if self.step_words is not None and not self.recompute:
+            E.step_counter = self.step_words[0].data_ptr()
+            E.step_snapshot = self.step_words[1].data_ptr()
+        if self.mirror is not None:
+            E.flags = self.flags.data_ptr()
+            E.flags_mirror = self.mirror.data_ptr()
+            E.nflags = min(self.flags.numel(), self.mirror.numel())
         size = ctypes.c_size_t()
-        lib = nat.lib()
         nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
                   "mi_elbo_workspace_bytes")
         ws = _elbo_workspace(self.device, size.value)
@@ -1265,8 +1311,28 @@ class _ElboPlan:
         self.state = (E, results, cat_results, lin_results, extra, terms)
         return loss
 
+    def _reduce_ok(self) -> bool:
+        """
+        Whether the deferred reductions can join the ELBO forward: every forward-absorbed Beta
+        factor has its implicit-gradient factors precomputed (its particle sums then move to the
+        ELBO backward).
+        """
+        for index, plan in self.absorbed.items():
+            f = self.factors[index]
+            if f.family != nat.BETA or plan.kind == nat.DRAW_PARTIALS:
+                continue
+            dgrad = plan.side_dgrad if plan.side_dgrad is not None else plan.drawn.dgrad
+            if dgrad is None:
+                return False
+        return True
+
     def backward(self, u: torch.Tensor) -> List[Optional[torch.Tensor]]:
         if self.state is None:   # a second backward through the same graph: recompute
+            # with this evaluation's generator step (the snapshot) and without advancing it again
+            self.recompute = True
+            for launcher in self.launchers:
+                if launcher.draw is not None:
+                    guide.use_snapshot(launcher.draw.cfg)
             self.forward()
         E, results, cat_results, lin_results, extra, _ = self.state
         self.state = None
@@ -1412,13 +1478,17 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
 
 def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[EntropyFactor],
          entropy_scale: float, samples: Optional[Dict[str, torch.Tensor]] = None,
-         flags: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, LogJoint]:
+         flags: Optional[torch.Tensor] = None,
+         step_words: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+         mirror: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, LogJoint]:
     """
     ``g0 * sum_k log p(x, z_k) - entropy_scale * H[factors]`` as one autograd node: the site
     kernels, the entropy and the reduction run in ``mi_group_forward`` / ``mi_elbo_forward``;
     backward is one ``mi_elbo_backward`` launch (plus the guide samplers' own backward).
-    ``flags``: already-zeroed int32 validation words for the step (``mi_step_begin``), used when
-    the plan's sites fit.
+    ``flags``: already-zeroed int32 validation words for the step, used when the plan's sites fit.
+    ``step_words``: (counter, snapshot) generator words; the ELBO forward copies the counter to the
+    snapshot and advances it. ``mirror``: host-mapped int32 words the ELBO forward copies the
+    validation words into.
     """
     _, bad = _lazy_uses(trace)
     if bad:
@@ -1433,7 +1503,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
-                     entropy_scale, linears, absorbed, flags)
+                     entropy_scale, linears, absorbed, flags, step_words, mirror)
     loss = _ElboFn.apply(plan, *plan.inputs())
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):
@@ -1442,4 +1512,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         pending.append(("linear", holder, [linear.site]))
     for launcher, holder in zip(launchers, plan.holders):
         pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
-    return loss, LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)
+    joint = LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)
+    if mirror is not None and plan.flags is not None and plan.flags.numel() <= mirror.numel():
+        joint.mirror = mirror[:plan.flags.numel()]
+    return loss, joint

@@ -14,7 +14,8 @@ What makes the ELBO capturable:
   and the loss increments that word on the device, so every replay draws fresh particles;
 * inside :func:`graph_safe` the engine does not synchronise to raise validation errors: the
   per-site flag words are accumulated on the device (never cleared by a replay, so a violation in
-  any replay persists), copied to pinned host memory after each replay, and checked once that
+  any replay persists), copied to pinned host memory by each replay (the ELBO forward writes them
+  there itself when it can, else one D2H copy follows the replay), and checked once that
   replay has finished (:meth:`StepGraph.check`, or non-blockingly before the next replay) --
   errors are raised with the reference's messages, a few steps late at most, and never lost;
 * ``torch.distributions`` argument validation (a host sync per check) is off inside the captured
@@ -139,10 +140,12 @@ class StepGraph:
             self.output = step()
             flags = [joint.flag_vector() for joint in self._joints]
             flags = [f for f in flags if f is not None]
+            mirror = None
             if len(self._joints) == 1 and flags and self._joints[0].sticky and \
                     flags[0] is self._joints[0].flags:
                 self._flags_device = flags[0]
                 self._accumulator = None
+                mirror = self._joints[0].mirror
             elif flags:
                 vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
                     else flags[0]
@@ -154,10 +157,15 @@ class StepGraph:
             else:
                 self._flags_device = None
                 self._accumulator = None
-        # Pinned host memory cannot be allocated while capturing: the copy of the flags is enqueued
-        # after each replay instead (one small asynchronous D2H copy).
+        # The ELBO forward of a sticky step writes its words to pinned host memory itself (the
+        # mirror); otherwise the copy is enqueued after each replay (one small asynchronous D2H
+        # copy: pinned host memory cannot be allocated while capturing).
         self._flags_host = None
-        if self._flags_device is not None:
+        self._mirrored = mirror is not None and self._flags_device is not None and \
+            mirror.numel() == self._flags_device.numel()
+        if self._mirrored:
+            self._flags_host = mirror
+        elif self._flags_device is not None:
             self._flags_host = torch.empty(self._flags_device.shape, dtype=self._flags_device.dtype,
                                            pin_memory=True)
         self._done = torch.cuda.Event()
@@ -166,7 +174,7 @@ class StepGraph:
     def __call__(self):
         self._check(block=False)
         self.graph.replay()
-        if self._flags_host is not None:
+        if self._flags_host is not None and not self._mirrored:
             self._flags_host.copy_(self._flags_device, non_blocking=True)
         self._done.record()
         self._pending = self._flags_device is not None
@@ -190,6 +198,7 @@ class StepGraph:
         if any(values):   # raising: clear the accumulated words for a caller that carries on
             self._done.synchronize()
             self._flags_device.zero_()
+            self._flags_host.zero_()
         cursor = 0
         for joint in self._joints:
             count = joint.flag_count()

@@ -33,6 +33,20 @@ class DrawConfig:
     particle_offset: int
     noise: Optional[torch.Tensor] = None
     step_device: Optional[torch.Tensor] = None   # uint64 word added to `step` on the device
+    # The word holding this evaluation's step once the forward has advanced `step_device`
+    # (mi_elbo.step_snapshot): read by every kernel that runs after the ELBO forward.
+    step_snapshot: Optional[torch.Tensor] = None
+
+
+def backward_step(cfg: DrawConfig) -> Optional[torch.Tensor]:
+    """The device step word of a draw's backward (regenerated noise)."""
+    return cfg.step_snapshot if cfg.step_snapshot is not None else cfg.step_device
+
+
+def use_snapshot(cfg: DrawConfig) -> None:
+    """Re-evaluate a forward after its ELBO advanced the generator: draw from the snapshot."""
+    if cfg.step_snapshot is not None:
+        cfg.step_device = cfg.step_snapshot
 
 
 def _flat_param(t: torch.Tensor, N: int) -> Tuple[torch.Tensor, int]:
@@ -91,7 +105,7 @@ class _NormalRsampleFn(torch.autograd.Function):
         seed, step = _philox_key(cfg)
         nat.check(lib.mi_normal_rsample_backward(
             dz.data_ptr(), dz.stride(0), dz.stride(1), K, N, seed, step,
-            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
+            nat.ptr(backward_step(cfg)), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
             workspace.data_ptr(), size.value,
             dloc.data_ptr(), deps_scale.data_ptr(), nat.stream_handle(device)),
             "mi_normal_rsample_backward")
@@ -397,7 +411,8 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
 def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: int,
              particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None,
              step_device: Optional[torch.Tensor] = None,
-             lazy: bool = False) -> Dict[str, torch.Tensor]:
+             lazy: bool = False,
+             step_snapshot: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """
     Draw every factor of a factorised guide (dict order = stream id order). With ``lazy``, large
     Normal factors become :class:`LazyDraw` placeholders evaluated inside the site kernels.
@@ -409,6 +424,6 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
                          particle_offset=particle_offset,
                          noise=None if noise is None else noise.get(name),
-                         step_device=step_device)
+                         step_device=step_device, step_snapshot=step_snapshot)
         samples[name] = draw(factor, cfg, lazy)
     return samples

@@ -250,6 +250,7 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.process_group = process_group
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
         self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
+        self._mirror: Optional[torch.Tensor] = None   # their pinned host copy
 
     # validation words zeroed with the step counter's advance; plans with more sites zero their own
     FLAG_WORDS = 64
@@ -280,26 +281,31 @@ class EvidenceLowerBoundLoss(nn.Module):
             device = _guide_device(approximation)
             if self._counter is None or self._counter.device != device:
                 self._counter = torch.zeros(1, dtype=torch.int64, device=device)
-            # The draws (and their regeneration in backward) use a snapshot of the device counter,
-            # which is advanced on the device -- replays of a captured step draw anew -- by the
-            # same launch that zeroes the call's validation words (mi_step_begin).
+            # The forward's draws read the device counter; the ELBO forward copies it into this
+            # call's snapshot (read by everything after it: the draws' backward) and advances it,
+            # so replays of a captured step draw anew without a separate launch.
             sticky = False
+            mirror = None
+            step_words = None
+            snapshot = None
             if device.type == "cuda":
-                step = torch.empty(1, dtype=torch.int64, device=device)
+                step = self._counter
+                snapshot = torch.empty(1, dtype=torch.int64, device=device)
+                step_words = (self._counter, snapshot)
                 if graph.deferred() is not None:
                     # Graph mode: validation words that no replay zeroes. Violations accumulate
                     # until the host reads them (StepGraph), so a replay that the host never
-                    # inspects cannot lose one; StepGraph clears them when it raises.
+                    # inspects cannot lose one; StepGraph clears them when it raises. The ELBO
+                    # forward also copies them into pinned host memory (no separate copy).
                     if self._sticky_flags is None or self._sticky_flags.device != device:
                         self._sticky_flags = torch.zeros(self.FLAG_WORDS, dtype=torch.int32,
                                                          device=device)
-                    flags, zero, sticky = self._sticky_flags, 0, True
+                    if self._mirror is None and not torch.cuda.is_current_stream_capturing():
+                        self._mirror = torch.zeros(self.FLAG_WORDS, dtype=torch.int32,
+                                                   pin_memory=True)
+                    flags, sticky, mirror = self._sticky_flags, True, self._mirror
                 else:
-                    flags = torch.empty(self.FLAG_WORDS, dtype=torch.int32, device=device)
-                    zero = self.FLAG_WORDS
-                _native.check(_native.lib().mi_step_begin(
-                    self._counter.data_ptr(), step.data_ptr(), flags.data_ptr(),
-                    zero, _native.stream_handle(device)), "mi_step_begin")
+                    flags = torch.zeros(self.FLAG_WORDS, dtype=torch.int32, device=device)
             else:   # the samplers reject host guides with the engine's device error
                 step, flags = self._counter.clone(), None
                 self._counter.add_(1)
@@ -307,13 +313,13 @@ class EvidenceLowerBoundLoss(nn.Module):
             # (mi_draw). If the model uses a draw in any other operation, the trace is repeated
             # with real draws (same counter, same values).
             samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
-                                     step_device=step, lazy=True)
+                                     step_device=step, lazy=True, step_snapshot=snapshot)
             try:
                 trace = particles.trace_particles(model, samples, K, validate=self.validate)
             except linear.NeedsDraws:
                 guide.release_lazy()
                 samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
-                                         step_device=step)
+                                         step_device=step, step_snapshot=snapshot)
                 trace = particles.trace_particles(model, samples, K, validate=self.validate)
         else:
             samples = approximation.rsample(torch.Size([K]))
@@ -330,7 +336,7 @@ class EvidenceLowerBoundLoss(nn.Module):
             factors, rest = engine.entropy_factors(approximation)
             try:
                 loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples,
-                                          flags=flags)
+                                          flags=flags, step_words=step_words, mirror=mirror)
                 joint.sticky = sticky and joint.flags is not None and not joint.checks and \
                     joint.flags.data_ptr() == flags.data_ptr()
             finally:
