@@ -117,18 +117,26 @@ def workload(name, device, world, rank):
 
             def conditioned():
                 return static
-        else:
-            # Device-resident minibatches (replaces the host DataLoader of examples/minibatch.md:78):
-            # a device counter picks the window, rows are gathered on the device, so a captured
-            # step draws a new minibatch on every replay.
-            counter = torch.zeros(1, dtype=torch.int64, device=device)
-            offsets = torch.arange(n_obs, device=device)
+        elif device.type == "cuda":
+            # Device-resident minibatches (mininf_amd.DeviceDataLoader, replacing the host
+            # DataLoader(TensorDataset(X, y), batch_size, shuffle=True) of
+            # examples/minibatch.md:78): the rows of each batch are drawn on the device and read
+            # by the linear site kernel through the index, so a captured step trains on a new
+            # shuffled batch on every replay.
+            loader = mininf_amd.DeviceDataLoader(X, y, batch_size=n_obs, shuffle=True,
+                                                 drop_last=True, seed=0)
 
             def conditioned():
-                rows = (counter * 7919) % blocks * n_obs + offsets
-                counter.add_(1)
-                return mininf_amd.condition(model, X=X.index_select(0, rows),
-                                            y=y.index_select(0, rows))
+                Xb, yb = loader.next()
+                return mininf_amd.condition(model, X=Xb, y=yb)
+        else:   # the CPU baseline: the reference's host semantics, contiguous windows
+            counter = [0]
+
+            def conditioned():
+                start = (counter[0] * 7919) % blocks * n_obs
+                counter[0] += 1
+                return mininf_amd.condition(model, X=X[start:start + n_obs],
+                                            y=y[start:start + n_obs])
 
         return dict(
             desc=(f"{name.upper()} Bayesian linear regression, {n_total}x{p} (minibatch {n_obs}), "

@@ -401,6 +401,8 @@ typedef struct mi_linear {
   double site_scale;      /* minibatch scale (core.py:267-271) */
   int32_t compute_grads;  /* write dtheta (and dsigma when `scale` is non-NULL) */
   int32_t pad0;
+  const int32_t* row_index; /* NULL, or row i of the site reads row row_index[i] of x, value and
+                               mask (a device-resident minibatch, mi_minibatch_rows) */
 } mi_linear;
 
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes);
@@ -416,6 +418,26 @@ int mi_linear_struct_size(size_t* bytes);
 int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
                                float* total, float* dslots, uint32_t* flags, void* start_event,
                                void* stop_event, void* stream, mi_reduce* reduce);
+
+/* ---- device-resident minibatches (replaces examples/minibatch.md:78-88, the host DataLoader) ---- */
+
+/* Row indices of the next minibatch of an n-row dataset: with c = counter[0] (then counter[0] =
+ * c + 1, in the same launch; counter[1] is the launch's completion count and must be zero
+ * initially -- every launch leaves it at zero), epoch e = c / batches_per_epoch and batch
+ * b = c % batches_per_epoch,
+ *   rows[j] = perm_e(b * batch + j)  (shuffle)   or   b * batch + j,   j < count,
+ * where perm_e is a keyed Feistel permutation of [0, n) (seed, e): a fresh random order every
+ * epoch, like DataLoader(..., shuffle=True) (dataloader.py RandomSampler), computed on the device.
+ * count is batch, or the shorter last batch of an epoch (batch b * batch + count <= n; positions
+ * past the data are not permuted). batches_per_epoch is ceil or floor of n / batch. n < 2^31. */
+int mi_minibatch_rows(uint64_t* counter, int64_t n, int64_t batch, int64_t batches_per_epoch,
+                      int32_t shuffle, uint64_t seed, int32_t* rows, int64_t count, void* stream);
+
+/* out[j] = base[rows[j]]: count rows of row_bytes bytes (multiples of 4) -- a minibatch
+ * materialised for uses other than the site kernels that read rows through the index. */
+int mi_gather_rows(const void* base, int64_t base_stride_bytes, int64_t row_bytes,
+                   const int32_t* rows, int64_t count, void* out, int64_t out_stride_bytes,
+                   void* stream);
 
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 

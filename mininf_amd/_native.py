@@ -99,6 +99,7 @@ class Linear(ctypes.Structure):
         ("scale_constant", ctypes.c_float), ("grad_scale", ctypes.c_float),
         ("site_scale", ctypes.c_double),
         ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("row_index", c_vp),
     ]
 
 
@@ -223,6 +224,9 @@ _SIGNATURES = {
     "mi_linear_forward_deferred": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t,
                                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                   ctypes.POINTER(Reduce)]),
+    "mi_minibatch_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, ctypes.c_int32,
+                                         ctypes.c_uint64, c_vp, c_i64, c_vp]),
+    "mi_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

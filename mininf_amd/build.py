@@ -17,7 +17,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = [os.path.join(CSRC, name)
-           for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "jit.cpp")]
+           for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "minibatch.hip",
+                        "jit.cpp")]
 HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "beta_grad.hpp", "jit.hpp",
                                                  "internal.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]

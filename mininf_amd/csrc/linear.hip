@@ -69,12 +69,13 @@ __global__ __launch_bounds__(kLinThreads) void k_linear(const mi_linear L, int k
     __syncthreads();
     for (int e = tid; e < kLinChunk * PMAX; e += kLinThreads) {
       const int r = e / PMAX, j = e % PMAX;
-      xs[r][j] = (r < rows && j < P) ? L.x[(c0 + r) * L.x_stride_i + j * L.x_stride_j] : 0.0f;
+      const int64_t src = (r < rows && L.row_index != nullptr) ? L.row_index[c0 + r] : c0 + r;
+      xs[r][j] = (r < rows && j < P) ? L.x[src * L.x_stride_i + j * L.x_stride_j] : 0.0f;
     }
     for (int r = tid; r < kLinChunk; r += kLinThreads) {
       float y = 0.0f, m = 0.0f;
       if (r < rows) {
-        const int64_t i = c0 + r;
+        const int64_t i = L.row_index != nullptr ? L.row_index[c0 + r] : c0 + r;
         y = L.value[i * L.value_stride_i];
         m = (L.mask == nullptr || L.mask[i * L.mask_stride_i] != 0) ? 1.0f : 0.0f;
         const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
@@ -264,14 +265,16 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
       const int64_t i = row0 + row;
+      const int64_t src = (i < N && L.row_index != nullptr) ? L.row_index[i] : i;
       xq[q] = (i < N && 4 * c4 < P)
-                  ? *reinterpret_cast<const float4*>(L.x + i * L.x_stride_i + 4 * c4)
+                  ? *reinterpret_cast<const float4*>(L.x + src * L.x_stride_i + 4 * c4)
                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (tid < S::CH) {
-      const int64_t i = row0 + tid;
+      const int64_t row = row0 + tid;
+      const int64_t i = (row < N && L.row_index != nullptr) ? L.row_index[row] : row;
       float y = 0.0f, m = 0.0f;
-      if (i < N) {
+      if (row < N) {
         y = L.value[i * L.value_stride_i];
         m = (L.mask == nullptr || L.mask[i * L.mask_stride_i] != 0) ? 1.0f : 0.0f;
         const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
@@ -382,45 +385,84 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   }
 
-  // ---- partials of tile (block, row subset) ---------------------------------------------------
-  const int64_t tile_id = row_block * rs_count + rs;
+  // ---- partials --------------------------------------------------------------------------------
+  // val: [r * PT + t] dtheta (row r of the accumulator, feature tile t), then the log density and
+  // dsigma of particle k0 + c (lanes h == 0). One tile per (block, row subset), or -- when the
+  // block has several row subsets and their values fit the (now idle) X staging buffer -- the
+  // subsets are combined through LDS in a fixed order and the block writes one tile (ntile = gx:
+  // a smaller partial slab, short enough for mi_elbo_forward to reduce, mi_reduce).
+  constexpr int kItems = 16 * PT + 2;
+  float val[kItems];
   const float wscale = (float)L.site_scale;
   lpd += __shfl_xor(lpd, 32, kWave);
   cnt += __shfl_xor(cnt, 32, kWave);
-  if (h == 0) {
+  val[16 * PT] = val[16 * PT + 1] = 0.0f;
+  if (h == 0 && k0 + c < K) {
     const int64_t kk = k0 + c;
-    if (kk < K) {
-      if (FAMILY == MI_NORMAL) {
-        // -(y - loc)^2 / (2 sigma^2) - log(sigma) - log(sqrt(2 pi))   (normal.py:88-103)
-        const float sigma = per_particle_sigma ? L.scale[kk * L.scale_stride_k] : L.scale_constant;
-        fl |= !(sigma > 0.0f) ? MI_FLAG_PARAM : 0u;
-        const double inv2 = 1.0 / ((double)sigma * (double)sigma);
-        const double cst = -(double)logf(sigma) - (double)kHalfLog2Pi;
-        part[tile_id * K + kk] = (float)(-0.5 * lpd * inv2 + (double)cnt * cst);
-        if (per_particle_sigma && grads)
-          part[((int64_t)(1 + P) * ntile + tile_id) * K + kk] =
-              (float)((double)wscale * (lpd * inv2 - (double)cnt) / (double)sigma);
-      } else {
-        part[tile_id * K + kk] = (float)lpd;
-      }
+    if (FAMILY == MI_NORMAL) {
+      // -(y - loc)^2 / (2 sigma^2) - log(sigma) - log(sqrt(2 pi))   (normal.py:88-103)
+      const float sigma = per_particle_sigma ? L.scale[kk * L.scale_stride_k] : L.scale_constant;
+      fl |= !(sigma > 0.0f) ? MI_FLAG_PARAM : 0u;
+      const double inv2 = 1.0 / ((double)sigma * (double)sigma);
+      const double cst = -(double)logf(sigma) - (double)kHalfLog2Pi;
+      val[16 * PT] = (float)(-0.5 * lpd * inv2 + (double)cnt * cst);
+      if (per_particle_sigma)
+        val[16 * PT + 1] = (float)((double)wscale * (lpd * inv2 - (double)cnt) / (double)sigma);
+    } else {
+      val[16 * PT] = (float)lpd;
     }
   }
-  if (grads) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t kk = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (kk >= K) continue;
-      double w = (double)wscale;
-      if (FAMILY == MI_NORMAL) {
-        const double sigma =
-            per_particle_sigma ? (double)L.scale[kk * L.scale_stride_k] : (double)L.scale_constant;
-        w /= sigma * sigma;
+  for (int r = 0; r < 16; ++r) {
+    const int64_t kk = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    double w = (double)wscale;
+    if (FAMILY == MI_NORMAL && grads && kk < K) {
+      const double sigma =
+          per_particle_sigma ? (double)L.scale[kk * L.scale_stride_k] : (double)L.scale_constant;
+      w /= sigma * sigma;
+    }
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const double v = kFlush64 ? dth[kFlush64 ? t : 0][kFlush64 ? r : 0] : (double)acc2[t][r];
+      val[r * PT + t] = grads ? (float)(v * w) : 0.0f;
+    }
+  }
+  const bool combine = rs_count > 1 && (rs_count - 1) * wt * kWave * kItems <= S::CH * S::RSTR;
+  int64_t tile_id = row_block * rs_count + rs;
+  if (combine) {
+    // (the stage loop ended with a barrier: xs is free)
+    if (rs > 0) {
+      float* dst = xs + (((rs - 1) * wt + pt) * kWave + lane) * kItems;
+#pragma unroll
+      for (int q = 0; q < kItems; ++q) dst[q] = val[q];
+    }
+    __syncthreads();
+    if (rs == 0) {
+#pragma unroll
+      for (int q = 0; q < kItems; ++q) {
+        double d = (double)val[q];
+        for (int o = 1; o < rs_count; ++o) d += (double)xs[(((o - 1) * wt + pt) * kWave + lane) * kItems + q];
+        val[q] = (float)d;
       }
+    }
+    tile_id = row_block;
+  }
+  if (!combine || rs == 0) {
+    if (h == 0 && k0 + c < K) {
+      part[tile_id * K + k0 + c] = val[16 * PT];
+      if (per_particle_sigma && grads)
+        part[((int64_t)(1 + P) * ntile + tile_id) * K + k0 + c] = val[16 * PT + 1];
+    }
+    if (grads) {
 #pragma unroll
-      for (int t = 0; t < PT; ++t) {
-        const int p = 32 * t + c;
-        const double v = kFlush64 ? dth[kFlush64 ? t : 0][kFlush64 ? r : 0] : (double)acc2[t][r];
-        if (p < P) part[((int64_t)(1 + p) * ntile + tile_id) * K + kk] = (float)(v * w);
+      for (int r = 0; r < 16; ++r) {
+        const int64_t kk = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (kk >= K) continue;
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+          const int p = 32 * t + c;
+          if (p < P) part[((int64_t)(1 + p) * ntile + tile_id) * K + kk] = val[r * PT + t];
+        }
       }
     }
   }
@@ -500,7 +542,13 @@ Geometry geometry(const mi_linear* L) {
     const int64_t target = std::max<int64_t>(1, (v.threads >= 512 ? 512 : 1024) / g.gy);
     g.stages_per_block = ceil_div(nstage, target);
     g.gx = ceil_div(ceil_div(nstage, g.stages_per_block), 8) * 8;
-    g.ntile = g.gx * (waves / wt);
+    // row subsets combined in the block when their values fit the X staging buffer
+    // (k_linear_mfma's epilogue)
+    const int rs_count = waves / wt;
+    const int items = 16 * g.pt + 2;
+    const int64_t lds_floats = ch * (32 * g.pt + 4);
+    const bool combine = rs_count > 1 && (int64_t)(rs_count - 1) * wt * 64 * items <= lds_floats;
+    g.ntile = combine ? g.gx : g.gx * rs_count;
     return g;
   }
   int kb = 1;

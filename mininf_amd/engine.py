@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from . import _native as nat
-from . import guide, particles
+from . import data, graph, guide, particles
 from .particles import ParticleTrace, SiteRecord
 
 
@@ -78,6 +78,11 @@ def _to_device(t: torch.Tensor, K: int, device: torch.device, what: str,
     version). Returns (tensor, None) or (None, constant).
     """
     if t.device == device:
+        if allow_constant and not t.requires_grad and (t.dim() == 0 or t.stride(0) == 0):
+            # a number of a distribution built in a captured step (mininf_amd.graph)
+            value = graph.CONSTANT_VALUES.get(t.data_ptr())
+            if value is not None and (t.dim() == 0 or t[0].numel() == 1):
+                return None, value
         return t, None
     if t.device.type != "cpu":
         raise nat.NativeError(f"{what} lives on {t.device}, expected {device}")
@@ -290,6 +295,7 @@ class _GroupLauncher:
                     grad = (dloc, dscale)
                 grads.append(grad)
                 continue
+            data.ensure_filled(view.tensor)   # a minibatch read directly: gather its rows
             desc.data = view.tensor.data_ptr()
             desc.stride_k, desc.stride_i = view.sk, view.si
             if mode == nat.GRAD_DENSE:
@@ -312,6 +318,7 @@ class _GroupLauncher:
                 desc.operand[q] = roles[q][0]
                 desc.constant[q] = roles[q][1]
             if mask is not None:
+                data.ensure_filled(mask.tensor)
                 desc.mask = mask.tensor.data_ptr()
                 desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
             desc.scale = site.scale
@@ -514,6 +521,10 @@ class _LinearLauncher:
         self.site, self.K, self.g0, self.device = site, K, g0, device
         self.X = site.linear_X
         self.N, self.P = self.X.shape
+        # device-resident minibatch read through its row index (mininf_amd.data): the dataset
+        # columns of X and the value, and the batch's rows
+        self.rows: Optional[torch.Tensor] = None
+        self.X_src, self.value_src = self.X, None
         self.theta = theta
         self.sigma = sigma
         self.sigma_input = None
@@ -538,12 +549,19 @@ class _LinearLauncher:
         L = nat.Linear()
         L.K, L.N, L.P = self.K, self.N, self.P
         L.family = FAMILY_CODES[self.site.family]
-        L.x = self.X.data_ptr()
-        L.x_stride_i, L.x_stride_j = self.X.stride()
+        L.x = self.X_src.data_ptr()
+        L.x_stride_i, L.x_stride_j = self.X_src.stride()
         L.theta = self.theta.data_ptr()
         L.theta_stride_k, L.theta_stride_j = self.theta.stride()
-        L.value = self.value.tensor.data_ptr()
-        L.value_stride_i = self.value.si
+        if self.rows is not None:
+            L.row_index = self.rows.data_ptr()
+            L.value = self.value_src.data_ptr()
+            L.value_stride_i = self.value_src.stride(0)
+        else:
+            data.ensure_filled(self.X)
+            data.ensure_filled(self.value.tensor)
+            L.value = self.value.tensor.data_ptr()
+            L.value_stride_i = self.value.si
         if self.mask is not None:
             L.mask = self.mask.data_ptr()
             L.mask_stride_i = self.mask.stride(0) if self.N > 1 else 1
@@ -653,6 +671,13 @@ def plan_linear(trace: ParticleTrace, g0: float, device: torch.device) -> List[_
                 mask = site.mask.to(device).bool().expand(shape).reshape(-1)
             if ok:
                 launcher = _LinearLauncher(site, K, g0, device, theta, sigma, value, mask)
+                xb, vb = data.lookup(site.linear_X), data.lookup(value.tensor)
+                if xb is not None and vb is not None and xb[0] is vb[0] and mask is None and \
+                        value.si == 1:
+                    batch = xb[0]
+                    launcher.rows = batch.rows
+                    launcher.X_src = batch.loader.columns[xb[1]]
+                    launcher.value_src = batch.loader.columns[vb[1]]
         if launcher is None:
             # materialise the predictor as the model would have: [K, N] = theta @ X^T
             site.tensors[0] = theta @ site.linear_X.t()
@@ -703,22 +728,28 @@ class LogJoint:
         Raise the reference's errors (core.py:186-188 for values, torch validate_args for
         parameters) from host copies of :meth:`flag_vector`.
         """
+        # every violation, then the first in model order (the reference raises at the first
+        # sample statement that fails, core.py:142-189)
+        found = []
         cursor = 0
         for kind, holder, sites in self.pending:
             for site in sites:
                 bits = int(values[cursor])
                 cursor += 1
                 if bits & nat.FLAG_PARAM:
-                    raise ValueError(f"Expected parameters of distribution {site.description} for "
-                                     f"site '{site.name}' to satisfy their constraints, but found "
-                                     "invalid values.")
-                if bits & nat.FLAG_SUPPORT:
-                    raise ValueError(f"Parameter '{site.name}' is not in the support of "
-                                     f"{site.description}.")
+                    found.append((site.order, len(found), (
+                        f"Expected parameters of distribution {site.description} for site "
+                        f"'{site.name}' to satisfy their constraints, but found invalid values.")))
+                elif bits & nat.FLAG_SUPPORT:
+                    found.append((site.order, len(found),
+                                  f"Parameter '{site.name}' is not in the support of "
+                                  f"{site.description}."))
         for check, _ in self.checks:
             if int(values[cursor]):
-                raise ValueError(check.message)
+                found.append((check.order, len(found), check.message))
             cursor += 1
+        if found:
+            raise ValueError(min(found)[2])
         for check, _ in self.checks:
             if check.memo is not None:
                 particles.memo_commit(check.memo)

@@ -43,11 +43,35 @@ _STATE = threading.local()
 _ORIGINAL_BROADCAST_ALL = distribution_utils.broadcast_all
 
 
+# Device scalars for the Python numbers of distributions built inside warm-up / captured steps,
+# created once by a warm-up step (a real fill) and reused by the capture, so the captured step has
+# no fill node per number; CONSTANT_VALUES maps their addresses to the numbers, so the site kernels
+# take them as compile-time constants (mininf_amd.engine._to_device).
+_CONSTANTS: dict = {}
+CONSTANT_VALUES: dict = {}
+
+
+def _device_constant(value: Number, options: dict) -> torch.Tensor:
+    device = options.get("device")
+    if device is None or torch.device(device).type == "cpu":
+        return torch.full((), value, **options)
+    key = (float(value), options["dtype"], str(device))
+    hit = _CONSTANTS.get(key)
+    if hit is not None:
+        return hit
+    out = torch.full((), value, **options)
+    if not torch.cuda.is_current_stream_capturing():   # a recorded fill has not run yet
+        _CONSTANTS[key] = out
+        CONSTANT_VALUES[out.data_ptr()] = float(value)
+    return out
+
+
 def _capture_safe_broadcast_all(*values):
     """
     torch.distributions.utils.broadcast_all with Python numbers materialised by a device fill
-    (``torch.full``) instead of a host-to-device copy (``torch.tensor(v, device=...)``), which a
-    capturing stream does not permit -- e.g. the ``1`` of ``Normal(X @ theta, 1)``.
+    (``torch.full``, cached across steps) instead of a host-to-device copy
+    (``torch.tensor(v, device=...)``), which a capturing stream does not permit -- e.g. the ``1``
+    of ``Normal(X @ theta, 1)``.
     """
     if not all(is_tensor_like(v) or isinstance(v, Number) for v in values):
         return _ORIGINAL_BROADCAST_ALL(*values)
@@ -58,7 +82,7 @@ def _capture_safe_broadcast_all(*values):
         if isinstance(value, torch.Tensor):
             options = dict(dtype=value.dtype, device=value.device)
             break
-    return torch.broadcast_tensors(*[v if is_tensor_like(v) else torch.full((), v, **options)
+    return torch.broadcast_tensors(*[v if is_tensor_like(v) else _device_constant(v, options)
                                      for v in values])
 
 
@@ -119,7 +143,7 @@ class StepGraph:
         with torch.cuda.stream(side):
             for _ in range(max(1, warmup)):
                 collector: List = []
-                with graph_safe(collector):
+                with graph_safe(collector), _capture_safe_distributions():
                     step()
                 for joint in collector:
                     joint.raise_on_violation()

@@ -373,7 +373,8 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
             cfg.noise = cfg.noise.to(device=loc.device, dtype=torch.float32).reshape(cfg.K, N) \
                 .contiguous()
         elif lazy and _fusable_normal(distribution, N):
-            buffer = torch.zeros(1, dtype=torch.float32, device=loc.device)
+            # never read (recognised by its address; other uses re-trace with real draws)
+            buffer = torch.empty(1, dtype=torch.float32, device=loc.device)
             placeholder = buffer.expand((cfg.K,) + tuple(shape))
             _LAZY[buffer.data_ptr()] = LazyDraw(cfg, loc, loc_s, scale, scale_s, N,
                                                 torch.Size(shape), placeholder)

@@ -105,7 +105,8 @@ class DeferredMatmul(TorchFunctionMode):
 
     def _placeholder(self, like: torch.Tensor, shape: torch.Size, info: Deferred) -> torch.Tensor:
         level = _functorch.maybe_get_level(like)
-        base = torch.zeros((), dtype=torch.float32, device=info.X.device)
+        # never read (any value-reading use materialises the product): no initialising kernel
+        base = torch.empty((), dtype=torch.float32, device=info.X.device)
         base = base.expand((self.K,) + tuple(shape))
         out = _functorch._add_batch_dim(base, 0, level)
         self.deferred[id(out)] = info

@@ -33,7 +33,7 @@ from torch.distributions.utils import lazy_property
 from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_flatten, tree_map
 
-from . import core
+from . import core, data
 from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
 from .util import _normalize_shape, check_constraint, OptionalSize
 
@@ -68,6 +68,7 @@ class SiteRecord:
     linear_X: Optional[torch.Tensor] = None
     linear_theta_index: int = -1
     linear_theta: Optional[torch.Tensor] = None
+    order: int = 0   # position of the sample statement in the model (errors raise in this order)
 
 
 @dataclasses.dataclass
@@ -81,6 +82,7 @@ class CheckRecord:
     output: int
     message: str
     memo: Optional[Tuple] = None
+    order: int = 0
 
 
 # Unbatched (conditioned) data is validated once per tensor version instead of on every step:
@@ -243,6 +245,7 @@ class ParticleTracer(TracerMixin):
         self.checks: List[CheckRecord] = []
         self.fallback_outputs: List[Tuple[str, int]] = []
         self.deferred = None   # the DeferredMatmul mode of the trace, if any
+        self.order = 0         # sample statements seen so far
 
     def _emit(self, tensor: torch.Tensor) -> int:
         self.outputs.append(tensor)
@@ -257,6 +260,11 @@ class ParticleTracer(TracerMixin):
         """
         if not self._validate_parameters:
             return
+        # A device-resident minibatch is a subset of its dataset column: the column is checked
+        # (once per version) instead of every batch (mininf_amd.data).
+        column = data.dataset_column(_plain(value))
+        if column is not None:
+            value = column
         memo = None
         if not (is_batched(value) or is_batched(_plain(value))):
             memo = memo_lookup(value, constraint)
@@ -268,10 +276,11 @@ class ParticleTracer(TracerMixin):
             described = type(distribution).__name__
         ok = device_check(constraint, value)
         self.checks.append(CheckRecord(name, self._emit(ok), str(core.support_error(
-            name, described)), memo))
+            name, described)), memo, self.order))
 
     def sample(self, state: State, name: str, distribution: Distribution,
                sample_shape: OptionalSize = None) -> torch.Tensor:
+        self.order += 1
         if isinstance(distribution, Value):
             value = state.get(name, distribution.value)
             if self._validate_parameters:
@@ -344,7 +353,7 @@ class ParticleTracer(TracerMixin):
         # parameters as well (MI_FLAG_PARAM), replacing torch's validate_args at construction.
         roles = [self._emit(p) for p in params] + [self._emit(data)]
         record = SiteRecord(name=name, family=family, roles=roles, site_shape=shape, scale=scale,
-                            mask=mask, description=type(distribution).__name__)
+                            mask=mask, description=type(distribution).__name__, order=self.order)
         if linear is not None:
             record.linear_X = linear.X
             record.linear_theta_index = self._emit(linear.theta)
@@ -374,7 +383,7 @@ class ParticleTracer(TracerMixin):
                     self.checks.append(CheckRecord(name, self._emit(ok), (
                         f"Expected parameter {param} of distribution "
                         f"{type(distribution).__name__} for site '{name}' to satisfy the "
-                        f"constraint {constraint}, but found invalid values")))
+                        f"constraint {constraint}, but found invalid values"), order=self.order))
         if type(distribution) is MultivariateNormal and data.dtype == torch.float32 and \
                 data.device.type != "cpu":
             # dense factorisations of float32 covariances are ill-conditioned in practice (the
@@ -426,7 +435,7 @@ class TraceCompat(TorchFunctionMode):
             ok = (info == 0).all()
             self.tracer.checks.append(CheckRecord("cholesky", self.tracer._emit(ok), (
                 "linalg.cholesky: The factorization could not be completed because the input is "
-                "not positive-definite.")))
+                "not positive-definite."), order=self.tracer.order))
             return L
         return func(*args, **kwargs)
 

@@ -1,0 +1,144 @@
+"""
+Device-resident minibatches (mininf_amd.data.DeviceDataLoader, csrc/minibatch.hip) on the GPU:
+
+* the rows kernel against its restatement (oracle/minibatch.py), bit for bit, across epochs,
+  sequential and shuffled, with a ragged last batch;
+* gathered values against torch indexing of the dataset;
+* the reference's minibatch regression (examples/minibatch.md:24-33) through the fused linear
+  site reading X and y through the row index, against the same model conditioned on plain copies
+  of the same rows (identical kernels on identical values: equal losses and gradients);
+* a captured training loop drawing a new batch per replay against the eager loop;
+* validation: an invalid value is reported with the reference's message.
+"""
+import pytest
+import torch
+from torch.distributions import Normal
+
+import mininf_amd as mi
+from mininf_amd.data import DeviceDataLoader, Minibatch
+from mininf_amd.graph import StepGraph
+from oracle import minibatch as oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rows_match_oracle(device):
+    n, batch = 1003, 100
+    X = torch.arange(n, dtype=torch.float32, device=device)
+    for shuffle in (False, True):
+        loader = DeviceDataLoader(X, batch_size=batch, shuffle=shuffle, seed=5)
+        batches = len(loader)
+        assert batches == 11
+        for epoch in range(2):
+            seen = []
+            for b, (xb,) in enumerate(loader):
+                count = min(batch, n - b * batch)
+                want = oracle.batch_rows(epoch * batches + b, n, batch, batches, shuffle, 5, count)
+                got = xb._mininf_batch.rows.cpu().tolist()
+                assert got == want
+                # a value-reading op gathers the rows
+                assert isinstance(xb, Minibatch)
+                assert torch.equal(xb.clone().as_subclass(torch.Tensor).cpu(),
+                                   torch.tensor(want, dtype=torch.float32))
+                seen += got
+            assert sorted(seen) == list(range(n))
+
+
+def test_next_crosses_epochs_with_drop_last(device):
+    n, batch = 1000, 128
+    loader = DeviceDataLoader(torch.zeros(n, 4, device=device), batch_size=batch, shuffle=True,
+                              drop_last=True, seed=3)
+    assert len(loader) == 7
+    for c in range(16):
+        (xb,) = loader.next()
+        want = oracle.batch_rows(c, n, batch, 7, True, 3, batch)
+        assert xb._mininf_batch.rows.cpu().tolist() == want
+    with pytest.raises(ValueError, match="drop_last"):
+        DeviceDataLoader(torch.zeros(n, device=device), batch_size=batch).next()
+
+
+def regression(device, n=4096, p=8, seed=0):
+    gen = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, p, generator=gen)
+    y = X @ torch.randn(p, generator=gen) + torch.randn(n, generator=gen)
+
+    def model():
+        theta = mi.sample("theta", Normal(0, 1), sample_shape=p)
+        with mi.batch(n):
+            with mi.no_log_prob():
+                Xs = mi.sample("X", Normal(0, 1), sample_shape=(n, p))
+            mi.sample("y", Normal(Xs @ theta, 1))
+
+    return model, X.to(device), y.to(device)
+
+
+def guide_module(device, p=8):
+    gen = torch.Generator().manual_seed(9)
+    return mi.nn.ParameterizedDistribution(Normal, loc=1e-3 * torch.randn(p, generator=gen),
+                                           scale=torch.ones(p)).to(device)
+
+
+def test_indexed_linear_site_matches_plain_rows(device):
+    model, X, y = regression(device)
+    loader = DeviceDataLoader(X, y, batch_size=512, shuffle=True, seed=1)
+    Xb, yb = next(iter(loader))
+    rows = Xb._mininf_batch.rows.long()
+    results = []
+    for values in ((Xb, yb), (X[rows].clone(), y[rows].clone())):
+        module = guide_module(device)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=64, seed=2)
+        loss = loss_fn(mi.condition(model, X=values[0], y=values[1]), {"theta": module()})
+        loss.backward()
+        results.append((float(loss), [q.grad.clone() for q in module.parameters()]))
+    (l0, g0), (l1, g1) = results
+    assert l0 == l1
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    # the indexed run never gathered X or y
+    assert Xb._mininf_batch.filled == [False, False]
+
+
+def test_captured_loop_draws_a_batch_per_replay(device):
+    model, X, y = regression(device, n=8192)
+
+    def setup():
+        loader = DeviceDataLoader(X, y, batch_size=1024, shuffle=True, drop_last=True, seed=4)
+        module = guide_module(device)
+        optimizer = torch.optim.Adam(module.parameters(), lr=0.01, capturable=True)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=32, seed=6)
+
+        def step():
+            optimizer.zero_grad(set_to_none=True)
+            Xb, yb = loader.next()
+            loss = loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": module()})
+            loss.backward()
+            optimizer.step()
+            return loss.detach()
+        return step, module
+
+    eager, eager_module = setup()
+    eager_losses = [float(eager()) for _ in range(8)]
+    body, graph_module = setup()
+    captured = StepGraph(body, warmup=3)
+    graph_losses = [float(captured()) for _ in range(4)]
+    captured.check()
+    torch.testing.assert_close(torch.tensor(graph_losses), torch.tensor(eager_losses[3:7]),
+                               rtol=1e-6, atol=0)
+    assert len(set(eager_losses)) == len(eager_losses)   # a new batch (and draw) every step
+
+
+def test_invalid_values_raise_reference_message(device):
+    model, X, y = regression(device)
+    y = y.clone()
+    y[17] = float("nan")
+    loader = DeviceDataLoader(X, y, batch_size=4096, seed=1)
+    Xb, yb = next(iter(loader))
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=8)
+    with pytest.raises(ValueError, match="is not in the support"):
+        loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": guide_module(device)()})
+    X = X.clone()
+    X[5, 1] = float("nan")
+    loader = DeviceDataLoader(X, y, batch_size=64, seed=1)
+    Xb, yb = next(iter(loader))
+    with pytest.raises(ValueError, match="is not in the support"):
+        loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": guide_module(device)()})

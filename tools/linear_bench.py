@@ -21,14 +21,24 @@ def main():
     ap.add_argument("--valu", action="store_true")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default=None, help="run one shape (C3, C3-bern, C4, P64)")
+    ap.add_argument("--shape", action="append", default=[],
+                    help="extra N,P,K shape (Normal); repeatable")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = nat.lib()
-    for name, N, P, K, fam in [("C3", 1_000_000, 32, 256, nat.NORMAL),
-                               ("C3-bern", 1_000_000, 32, 256, nat.BERNOULLI_LOGITS),
-                               ("C4", 65536, 32, 32, nat.NORMAL),
-                               ("P64", 1_000_000, 64, 128, nat.NORMAL)]:
-        if args.only is not None and name != args.only:
+    shapes = [("C3", 1_000_000, 32, 256, nat.NORMAL),
+              ("C3-bern", 1_000_000, 32, 256, nat.BERNOULLI_LOGITS),
+              ("C4", 65536, 32, 32, nat.NORMAL),
+              ("P64", 1_000_000, 64, 128, nat.NORMAL)]
+    for text in args.shape:
+        N, P, K = (int(v) for v in text.split(","))
+        shapes.append((text, N, P, K, nat.NORMAL))
+    if args.shape and args.only is None:
+        args.only = "__shapes__"
+    for name, N, P, K, fam in shapes:
+        if args.only == "__shapes__" and name in ("C3", "C3-bern", "C4", "P64"):
+            continue
+        if args.only not in (None, "__shapes__") and name != args.only:
             continue
         X = torch.randn(N, P, device=dev)
         theta = 0.3 * torch.randn(K, P, device=dev)
