@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import mininf_amd  # noqa: E402
+import mininf_amd.optim  # noqa: E402
 from mininf_amd import engine  # noqa: E402
 from mininf_amd.distributed import GradientBucket  # noqa: E402
 from mininf_amd.graph import StepGraph  # noqa: E402
@@ -286,6 +287,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo lets "
                          "several ranks share one GPU to exercise the sharded path)")
+    ap.add_argument("--optimizer", choices=("mi", "torch"), default="mi",
+                    help="Adam implementation: mininf_amd.optim.Adam (one HIP launch, default) or "
+                         "torch.optim.Adam(fused=True, capturable=True)")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile 20 extra steps and print the hottest host functions to stderr")
     ap.add_argument("--check-launch", action="store_true",
@@ -317,7 +321,10 @@ def main():
 
     w = workload(args.config, device, world, rank)
     module = w["module"]
-    optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
+    if args.optimizer == "torch":
+        optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
+    else:   # the same Adam in one HIP launch (mininf_amd.optim, bit-identical to torch's fused)
+        optimizer = mininf_amd.optim.Adam(module.parameters(), lr=w["lr"])
     loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(
         num_particles=w["k_local"] * world, seed=1, validate=not args.no_validate,
         process_group=group)
@@ -450,7 +457,9 @@ def main():
                        (" + RCCL grad all-reduce" if args.dist_backend == "nccl" else
                         f" + {args.dist_backend} grad all-reduce") if world > 1 else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
-                   "step_mode": mode, "eager_ms_per_step": eager_ms},
+                   "step_mode": mode, "eager_ms_per_step": eager_ms,
+                   "optimizer": ("mininf_amd.optim.Adam (one HIP launch)" if args.optimizer == "mi"
+                                 else "torch.optim.Adam(fused=True)")},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -439,6 +439,37 @@ int mi_gather_rows(const void* base, int64_t base_stride_bytes, int64_t row_byte
                    const int32_t* rows, int64_t count, void* out, int64_t out_stride_bytes,
                    void* stream);
 
+/* ---- optimizer step (replaces torch.optim.Adam.step of the training loop, README.md:66-69) ----- */
+
+/* One Adam step for up to MI_ADAM_MAX_TENSORS fp32 parameters in one launch, arithmetic of torch's
+ * fused Adam (fused_adam_utils.cuh adam_math: ADAM_MODE::ORIGINAL, no AMSGrad):
+ *   s = *step + 1;  g = (maximize ? -grad : grad) + weight_decay * param
+ *   m = beta1 m + (1 - beta1) g;  v = beta2 v + (1 - beta2) g^2
+ *   param -= lr / (1 - beta1^s) * m / (sqrt(v) / sqrt(1 - beta2^s) + eps);  *step = s
+ * per tensor (its own step word, fp32 as torch keeps it). `counters`: MI_ADAM_COUNTER_WORDS uint32
+ * words, zero before first use; every launch leaves them zero. */
+#define MI_ADAM_MAX_TENSORS 8
+#define MI_ADAM_COUNTER_WORDS (MI_ADAM_MAX_TENSORS * 33)
+typedef struct mi_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;
+  int64_t numel;          /* contiguous */
+} mi_adam_tensor;
+typedef struct mi_adam {
+  int32_t num;
+  int32_t maximize;
+  double lr;
+  double beta1;
+  double beta2;
+  double eps;
+  double weight_decay;
+  mi_adam_tensor tensors[MI_ADAM_MAX_TENSORS];
+} mi_adam;
+int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream);
+
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 
 #define MI_MAX_TERMS 8

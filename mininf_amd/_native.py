@@ -151,6 +151,21 @@ class Elbo(ctypes.Structure):
     ]
 
 
+ADAM_MAX_TENSORS = 8
+ADAM_COUNTER_WORDS = ADAM_MAX_TENSORS * 33
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_vp), ("grad", c_vp), ("exp_avg", c_vp), ("exp_avg_sq", c_vp),
+                ("step", c_vp), ("numel", c_i64)]
+
+
+class Adam(ctypes.Structure):
+    _fields_ = [("num", ctypes.c_int32), ("maximize", ctypes.c_int32), ("lr", ctypes.c_double),
+                ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+                ("weight_decay", ctypes.c_double), ("tensors", AdamTensor * ADAM_MAX_TENSORS)]
+
+
 # name -> (restype, argtypes). Mirrors include/mininf_amd.h one to one.
 _SIGNATURES = {
     "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
@@ -227,6 +242,7 @@ _SIGNATURES = {
     "mi_minibatch_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, ctypes.c_int32,
                                          ctypes.c_uint64, c_vp, c_i64, c_vp]),
     "mi_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mi_adam_step": (ctypes.c_int, [ctypes.POINTER(Adam), c_vp, c_vp]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

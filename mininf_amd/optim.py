@@ -1,0 +1,97 @@
+"""
+MI355X optimizer step: :class:`Adam`, a drop-in ``torch.optim.Adam`` whose ``step()`` is one HIP
+launch (``mi_adam_step``, ``csrc/adam.hip``) for up to eight parameters, step-count increment
+included -- torch's capturable fused Adam needs a ``_foreach_add_`` launch for the step counts
+plus the fused update. Same arithmetic as ``torch.optim.Adam(fused=True)`` (bit-identical
+updates), same ``state`` layout (``step``, ``exp_avg``, ``exp_avg_sq``), so ``state_dict`` moves
+between the two.
+
+The reference trains with ``torch.optim.Adam`` (``README.md:66-69``); this class is the same call
+with the same arguments.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Iterable, Tuple
+
+import torch
+
+from . import _native as nat
+
+
+class Adam(torch.optim.Optimizer):
+    """
+    Adam (Kingma & Ba) on fp32 device parameters. ``amsgrad`` and differentiable steps are not
+    supported (use ``torch.optim.Adam``).
+    """
+    def __init__(self, params: Iterable, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, *, maximize: bool = False,
+                 amsgrad: bool = False) -> None:
+        if amsgrad:
+            raise NotImplementedError("mininf_amd.optim.Adam does not implement amsgrad")
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 0: {betas[0]}")
+        if not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      maximize=maximize, amsgrad=False))
+        self._counters: Dict[torch.device, torch.Tensor] = {}
+
+    def _counter_words(self, device: torch.device) -> torch.Tensor:
+        words = self._counters.get(device)
+        if words is None:
+            words = torch.zeros(nat.ADAM_COUNTER_WORDS, dtype=torch.int32, device=device)
+            self._counters[device] = words
+        return words
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = nat.lib()
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            batch = []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("Adam does not support sparse gradients")
+                nat.require_device(p, "Adam parameter")
+                if p.dtype != torch.float32 or not p.is_contiguous() or \
+                        not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                    raise nat.NativeError("mininf_amd.optim.Adam takes contiguous float32 "
+                                          "parameters and gradients")
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p,
+                                                           memory_format=torch.preserve_format)
+                batch.append((p, state))
+            for start in range(0, len(batch), nat.ADAM_MAX_TENSORS):
+                chunk = batch[start:start + nat.ADAM_MAX_TENSORS]
+                desc = nat.Adam()
+                desc.num = len(chunk)
+                desc.maximize = int(group["maximize"])
+                desc.lr, desc.beta1, desc.beta2 = float(group["lr"]), float(beta1), float(beta2)
+                desc.eps, desc.weight_decay = float(group["eps"]), float(group["weight_decay"])
+                for j, (p, state) in enumerate(chunk):
+                    t = desc.tensors[j]
+                    t.param, t.grad = p.data_ptr(), p.grad.data_ptr()
+                    t.exp_avg, t.exp_avg_sq = (state["exp_avg"].data_ptr(),
+                                               state["exp_avg_sq"].data_ptr())
+                    t.step, t.numel = state["step"].data_ptr(), p.numel()
+                device = chunk[0][0].device
+                nat.check(lib.mi_adam_step(ctypes.byref(desc),
+                                           self._counter_words(device).data_ptr(),
+                                           nat.stream_handle(device)), "mi_adam_step")
+        return loss

@@ -173,3 +173,14 @@ def test_elbo_value_and_backprop(device):
     assert all(p.grad is None for p in approximation.distribution_parameters.values())
     value.backward()
     assert all(p.grad is not None for p in approximation.distribution_parameters.values())
+
+
+def test_optim_adam_argument_checks():
+    import mininf_amd.optim as optim
+    p = [torch.zeros(2, requires_grad=True)]
+    with pytest.raises(ValueError, match="learning rate"):
+        optim.Adam(p, lr=-1.0)
+    with pytest.raises(ValueError, match="beta parameter at index 1"):
+        optim.Adam(p, betas=(0.9, 1.0))
+    with pytest.raises(NotImplementedError):
+        optim.Adam(p, amsgrad=True)
