@@ -207,13 +207,29 @@ def measured_traffic(name):
     return entry["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def host_cpus():
+    """
+    The CPUs this process may use: its affinity set, capped by a cgroup CPU quota when one is set
+    (os.cpu_count() counts every CPU of the machine, also those a container cannot run on).
+    """
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(name, budget_s=12.0):
     """
     The reference's semantics on the host cores (oracle/cpu_port.py): K_cpu single-draw losses per
-    step, timed on a bounded sample; reported as evals/s of the same workload.
+    step, timed on a bounded sample; reported as evals/s of the same workload. Every CPU this
+    process may use runs torch's intra-op threads.
     """
     from oracle import cpu_port
-    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(host_cpus())
     cpu = torch.device("cpu")
     w = workload(name, cpu, 1, 0)
     k_cpu = min(w["k_local"], 16)
@@ -239,7 +255,9 @@ def cpu_baseline(name, budget_s=12.0):
     return {"value": rate, "unit": UNIT, "cores": torch.get_num_threads(), "kind": "port",
             "sample": (f"{steps} steps x {k_cpu} single-draw particles of {w['desc']} in "
                        f"{elapsed:.1f} s (reference semantics, torch {torch.__version__} CPU, "
-                       f"os.cpu_count()={os.cpu_count()}, {model_name})"),
+                       f"{torch.get_num_threads()} threads = the CPUs available to this process "
+                       f"(affinity and cgroup quota; os.cpu_count()={os.cpu_count()}), "
+                       f"{model_name})"),
             "ms_per_step_extrapolated": 1e3 * elapsed / steps * w["k_local"] / k_cpu}
 
 
@@ -274,52 +292,9 @@ def check_launch(args, world, rank):
     return 0
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c2")
-    ap.add_argument("--no-validate", action="store_true")
-    ap.add_argument("--eager", dest="graph", action="store_false",
-                    help="launch every step from Python instead of replaying a captured hipGraph")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo lets "
-                         "several ranks share one GPU to exercise the sharded path)")
-    ap.add_argument("--optimizer", choices=("mi", "torch"), default="mi",
-                    help="Adam implementation: mininf_amd.optim.Adam (one HIP launch, default) or "
-                         "torch.optim.Adam(fused=True, capturable=True)")
-    ap.add_argument("--profile-host", action="store_true",
-                    help="cProfile 20 extra steps and print the hottest host functions to stderr")
-    ap.add_argument("--check-launch", action="store_true",
-                    help="rendezvous and one all-reduce only, no GPU work: prints the line's "
-                         "n_gpus (tests the --gpus launch path on a CPU host)")
-    args = ap.parse_args()
-
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # `python bench.py --gpus N` on its own: start the N ranks as child processes (one per
-        # GPU) before this process touches the GPU, and exit with their status.
-        raise SystemExit(launch_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
-    if args.check_launch:
-        raise SystemExit(check_launch(args, world, rank))
-    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(device)
-    group = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(args.dist_backend)
-        group = dist.group.WORLD
-
-    w = workload(args.config, device, world, rank)
+def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budget):
+    """Measure one workload (all ranks); rank 0 gets the bench line's dict."""
+    w = workload(config, device, world, rank)
     module = w["module"]
     if args.optimizer == "torch":
         optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
@@ -384,15 +359,15 @@ def main():
         return loss.detach()   # keep no autograd graph alive across steps (graph capture needs it)
 
     # Eager steps: every kernel launched from Python (the kernel timing comes from these).
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         eager_step()
     timer.active = True
-    eager_steps = max(3, args.steps // 3) if args.graph else args.steps
+    eager_steps = max(3, steps // 3) if args.graph else steps
     eager_elapsed, loss = timed(eager_step, eager_steps)
     timer.active = False
     eager_ms = 1e3 * eager_elapsed / eager_steps
     torch.cuda.synchronize()
-    elapsed, mode = eager_elapsed * args.steps / eager_steps, "eager"
+    elapsed, mode = eager_elapsed * steps / eager_steps, "eager"
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
         captured = StepGraph(forward_backward, warmup=2)
@@ -406,9 +381,9 @@ def main():
                 return bucket.loss()
             return out
 
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             graph_step()
-        elapsed, loss = timed(graph_step, args.steps)
+        elapsed, loss = timed(graph_step, steps)
         captured.check()
         mode = "hipGraph replay"
 
@@ -423,8 +398,8 @@ def main():
         profiler.disable()
         pstats.Stats(profiler, stream=sys.stderr).sort_stats("tottime").print_stats(30)
 
-    ms = 1e3 * elapsed / args.steps
-    value = w["evals"] * world * args.steps / elapsed
+    ms = 1e3 * elapsed / steps
+    value = w["evals"] * world * steps / elapsed
     kernel_ms, launches = timer.mean_ms(w["dominant_N"])
     kernel_s = kernel_ms * 1e-3
     if w["bound"] in ("valu", "mfma"):
@@ -443,13 +418,13 @@ def main():
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": w["kernel"],
                 "kernel_ms": kernel_ms, "launches_timed": launches,
                 "algorithmic_per_launch": f"{nbytes:.4g} B"}
-    traffic, source = measured_traffic(args.config)
+    traffic, source = measured_traffic(config)
     roof["traffic"] = traffic
     if traffic is not None:
         roof["traffic_source"] = f"{source} (rocprofv3 --pmc, bytes per launch)"
     out = {
-        "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "metric": METRIC, "value": value, "unit": UNIT, "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": w["data"],
         "config": {"workload": w["desc"], "particles_per_gpu": w["k_local"],
                    "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
@@ -462,8 +437,70 @@ def main():
                                  else "torch.optim.Adam(fused=True)")},
         "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.config)
+    if rank == 0 and world == 1 and cpu_budget > 0:
+        out["cpu_baseline"] = cpu_baseline(config, cpu_budget)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="launch every step from Python instead of replaying a captured hipGraph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="default C2 run: skip measuring C3 / C4 / C5 after it")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo lets "
+                         "several ranks share one GPU to exercise the sharded path)")
+    ap.add_argument("--optimizer", choices=("mi", "torch"), default="mi",
+                    help="Adam implementation: mininf_amd.optim.Adam (one HIP launch, default) or "
+                         "torch.optim.Adam(fused=True, capturable=True)")
+    ap.add_argument("--profile-host", action="store_true",
+                    help="cProfile 20 extra steps and print the hottest host functions to stderr")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="rendezvous and one all-reduce only, no GPU work: prints the line's "
+                         "n_gpus (tests the --gpus launch path on a CPU host)")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` on its own: start the N ranks as child processes (one per
+        # GPU) before this process touches the GPU, and exit with their status.
+        raise SystemExit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
+    if args.check_launch:
+        raise SystemExit(check_launch(args, world, rank))
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(device)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
+        group = dist.group.WORLD
+
+    out = run_config(args.config, args, world, rank, device, group, args.steps, args.warmup,
+                     0.0 if args.no_cpu_baseline else 12.0)
+    if world == 1 and args.config == "c2" and not args.no_other_configs:
+        # the other single-GPU configurations of BASELINE.json, measured in the same run
+        # (shorter: 10 graph-replayed steps each; CPU baseline only for C3)
+        out["other_configs"] = {}
+        for name in ("c3", "c4", "c5"):
+            sub = run_config(name, args, world, rank, device, group, min(args.steps, 10), 3,
+                             0.0 if (args.no_cpu_baseline or name != "c3") else 8.0)
+            out["other_configs"][name] = {key: sub[key] for key in (
+                "value", "unit", "ms_per_step", "config", "roofline", "cpu_baseline")
+                if key in sub}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -198,7 +198,10 @@ struct MfShape {
 // Grid: one dimension of gx * gy blocks, gx (row blocks) a multiple of 8. Blocks are dealt to the
 // 8 XCDs round-robin, so block b's row block is chosen such that the gy particle groups of one row
 // block run on one XCD (b, b + 8, ...) and share its L2 copy of the X rows.
-template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW, bool GRADS>
+// ONESTAGE: every block stages one row block (small N, e.g. a 65536-row minibatch): no stage
+// loop, no prefetch and no software pipeline over tiles -- a third of the code, which matters
+// when each wave runs through it once (the cold instruction fetch dominates such launches).
+template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW, bool GRADS, bool ONESTAGE>
 __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int wt, int gy,
                                                           int64_t stages_per_block,
                                                           int64_t ntile,
@@ -347,12 +350,39 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   };
 
-  if (st0 < st1) {
+  if constexpr (ONESTAGE) {
+    if (st0 < st1) {
+      load_stage(st0);
+      store_stage();
+    }
+    __syncthreads();
+    if (st0 < st1) {
+      const int ntl = (S::TILES - rs + rs_count - 1) / rs_count;
+#pragma unroll 1
+      for (int j = 0; j < ntl; ++j) {
+        const int tile = rs + j * rs_count;
+        f32x16 cur = gemm1(tile);
+        elementwise(cur, tile);
+        if (GRADS) gemm2(cur, tile);
+      }
+      if (kFlush64) {
+#pragma unroll
+        for (int t = 0; t < PT; ++t) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dth[kFlush64 ? t : 0][kFlush64 ? r : 0] += (double)acc2[t][r];
+          acc2[t] = f32x16{};
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!ONESTAGE && st0 < st1) {
     load_stage(st0);
     store_stage();
   }
-  __syncthreads();
-  for (int64_t st = st0; st < st1; ++st) {
+  if (!ONESTAGE) __syncthreads();
+  for (int64_t st = st0; !ONESTAGE && st < st1; ++st) {
     if (st + 1 < st1) load_stage(st + 1);   // in flight during this stage's MFMAs
     // Software pipeline over this wave's tiles: the first product of tile j + 1 is issued before
     // the elementwise step of tile j, so its MFMAs run while the VALU evaluates the densities.
@@ -574,12 +604,16 @@ template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW>
 void launch_mfma(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
                  hipStream_t s) {
   const dim3 grid((unsigned)(g.gx * g.gy));
-  if (L.compute_grads)
-    hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, true>), grid, dim3(NT),
-                       0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags);
-  else
-    hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, false>), grid, dim3(NT),
-                       0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags);
+  const bool one = g.stages_per_block == 1;
+#define MI_LAUNCH_MFMA(GRADS, ONE)                                                              \
+  hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, GRADS, ONE>), grid,      \
+                     dim3(NT), 0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags)
+  if (L.compute_grads) {
+    if (one) MI_LAUNCH_MFMA(true, true); else MI_LAUNCH_MFMA(true, false);
+  } else {
+    if (one) MI_LAUNCH_MFMA(false, true); else MI_LAUNCH_MFMA(false, false);
+  }
+#undef MI_LAUNCH_MFMA
 }
 
 template <int FAMILY, int PT>

@@ -574,17 +574,26 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 }
 
 
+// Grid (1-D): gy particle blocks of each chunk, chunks padded to a multiple of 8, dealt so that
+// every particle block of chunk c runs on the same XCD (workgroups go to the 8 XCDs round-robin:
+// block b -> XCD b % 8 = c % 8) and the chunk is fetched into that XCD's L2 once; then the side
+// job's workgroups.
 template <int FAMILY, int kSmemP, int kSmemChunk>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
-                                                                   int64_t nseg,
+                                                                   int64_t nseg, int gy,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
-  const int64_t c = blockIdx.x;
-  if (c >= nseg - 1) {   // workgroups past the chunks: the side job (mi_side), row 0 only
-    if (blockIdx.y == 0) beta_side_block(G.side, c - (nseg - 1));
+  const int64_t chunks = nseg - 1;
+  const int64_t padded = (chunks + 7) / 8 * 8;
+  const int64_t b = blockIdx.x;
+  if (b >= padded * gy) {   // workgroups past the chunks: the side job (mi_side)
+    beta_side_block(G.side, b - padded * gy);
     return;
   }
+  const int64_t c = (b / (8 * gy)) * 8 + b % 8;
+  const int64_t kblock = (b / 8) % gy;
+  if (c >= chunks) return;   // padding
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
   const int64_t i0 = c * kSmemChunk;
@@ -593,7 +602,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
   const int64_t K = G.K;
-  const int64_t kbase = (int64_t)blockIdx.y * (kBcastThreads * kSmemP) + threadIdx.x;
+  const int64_t kbase = kblock * (kBcastThreads * kSmemP) + threadIdx.x;
   float lg[kSmemP], dl[kSmemP];
 #pragma unroll
   for (int p = 0; p < kSmemP; ++p) {
@@ -1135,13 +1144,22 @@ size_t finalize_offset(const mi_group* g, const Plan& p) {
 template <int FAM>
 void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 block(mi::kBcastThreads);
+  // p.grid = (chunks + side blocks, particle blocks): the kernel takes them as one XCD-aware
+  // dimension (see k_site_bcast_smem)
+  const int64_t chunks = p.nseg - 1;
+  const int64_t side = (int64_t)p.grid.x - chunks;
+  const int gy = (int)p.grid.y;
+  const dim3 grid((unsigned)(ceil_div(chunks, 8) * 8 * gy + side));
+#define MI_SMEM(P, CH) \
+  hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, flags)
   switch (smem_variant()) {
-    case 1: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 4096>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
-    case 2: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 8192>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
-    case 3: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 8192>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
-    case 4: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 8, 2048>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
-    default: hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096>), p.grid, block, bcast_lds(), s, G, part, p.nseg, flags); break;
+    case 1: MI_SMEM(8, 4096); break;
+    case 2: MI_SMEM(4, 8192); break;
+    case 3: MI_SMEM(8, 8192); break;
+    case 4: MI_SMEM(8, 2048); break;
+    default: MI_SMEM(4, 4096); break;
   }
+#undef MI_SMEM
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
