@@ -210,6 +210,12 @@ typedef struct mi_reduce {
   int64_t K;
   int32_t num_sites;
   int32_t num_slots;
+  /* bit v: value v's segment block [nseg * K] holds a rank-one sum instead: u[0 .. nseg) at its
+   * start, then f[0 .. K) and e[0 .. K); the value is f[k] * sum_seg u[seg] + e[k] (a per-particle
+   * constant times a particle-independent sum, e.g. a Bernoulli site's slot gradient over shared
+   * data: w dl_k * sum_i x_i - w dl_k N sigmoid(l_k)) */
+  int32_t rank1;
+  int32_t pad0;
   double scale[MI_MAX_SITES];
   double slot_scale;
   float* total;          /* [K] */

@@ -133,6 +133,7 @@ class Reduce(ctypes.Structure):
     _fields_ = [
         ("part", c_vp), ("nseg", c_i64), ("K", c_i64),
         ("num_sites", ctypes.c_int32), ("num_slots", ctypes.c_int32),
+        ("rank1", ctypes.c_int32), ("pad0", ctypes.c_int32),
         ("scale", ctypes.c_double * MAX_SITES), ("slot_scale", ctypes.c_double),
         ("total", c_vp), ("site_lp", c_vp), ("slot_grad", c_vp),
     ]

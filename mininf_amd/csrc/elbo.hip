@@ -419,23 +419,30 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
   double* lds = &red[0][0];   // [kRedG][kRedK] doubles
   double t = 0.0;
   for (int v = v0; v < v1; ++v) {
-    const float* __restrict__ p = J.part + (int64_t)v * J.nseg * K + kc;
+    // rank-one values (mi_reduce.rank1): the particle-independent u[seg], then f[k] u + e[k]
+    const bool r1 = (J.rank1 >> v) & 1;
+    const float* __restrict__ p = J.part + (int64_t)v * J.nseg * K + (r1 ? 0 : kc);
+    const int64_t stride = r1 ? 1 : K;
     double acc = 0.0;
     int64_t g = gl;
     for (; g + 7 * kRedG < J.nseg; g += 8 * kRedG) {
       float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * K];
+      for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * stride];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += (double)x[j];
     }
-    for (; g < J.nseg; g += kRedG) acc += (double)p[g * K];
+    for (; g < J.nseg; g += kRedG) acc += (double)p[g * stride];
     __syncthreads();
     lds[gl * kRedK + kl] = acc;
     __syncthreads();
     if (gl == 0 && k < K) {
       double s = 0.0;
       for (int j = 0; j < kRedG; ++j) s += lds[j * kRedK + kl];
+      if (r1) {
+        const float* __restrict__ q = J.part + (int64_t)v * J.nseg * K + J.nseg;
+        s = (double)q[k] * s + (double)q[K + k];
+      }
       if (v < J.num_sites) {
         s *= pick(J.scale, v);
         if (J.site_lp != nullptr) J.site_lp[(int64_t)v * K + k] = s;

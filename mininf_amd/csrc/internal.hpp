@@ -13,6 +13,7 @@
 // With long segment lists (> 512) and a `scratch` of mi_finalize_scratch_bytes, the reduction
 // runs in two launches (segment chunks in parallel, then the chunk sums); otherwise in one.
 size_t mi_finalize_scratch_bytes(int64_t nseg, int64_t K, int nv);
+// rank1: bit v marks value v as stored in mi_reduce's rank-one layout (one-launch path only).
 int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
                        const double* scale, double slot_scale, float* total, double* site_lp,
-                       float* slot_grad, double* scratch, hipStream_t stream);
+                       float* slot_grad, double* scratch, hipStream_t stream, int rank1 = 0);

@@ -578,10 +578,14 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // every particle block of chunk c runs on the same XCD (workgroups go to the 8 XCDs round-robin:
 // block b -> XCD b % 8 = c % 8) and the chunk is fetched into that XCD's L2 once; then the side
 // job's workgroups.
+// rank1: the slot value is written in the rank-one layout of mi_reduce.rank1 (the chunk sums u[c]
+// from the particle-block-0 workgroups, f[k] = w dl_k and e[k] = -N w sigmoid(l_k) dl_k from the
+// chunk-0 workgroups) instead of one partial per (chunk, particle): half the partial slab.
 template <int FAMILY, int kSmemP, int kSmemChunk>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
+                                                                   int rank1,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
   const int64_t chunks = nseg - 1;
@@ -695,12 +699,14 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
                          ? G.operands[o_a].slot : -1;
   const float w = (float)st.scale;
   const int64_t extra = nseg - 1;
+  float* slot_part = part + (int64_t)(1 + slot_a) * nseg * K;   // (slot_a >= 0)
+  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0) slot_part[c] = s_a;   // u[c]
 #pragma unroll
   for (int p = 0; p < kSmemP; ++p) {
     const int64_t k = kbase + p * kBcastThreads;
     if (k >= K) continue;
     part[c * K + k] = (float)acc[p];
-    if (slot_a >= 0) part[((int64_t)(1 + slot_a) * nseg + c) * K + k] = w * (s_a * dl[p]);
+    if (slot_a >= 0 && !rank1) slot_part[c * K + k] = w * (s_a * dl[p]);
     if (c == 0) {
       const float l = lg[p];
       const float t = expf(-fabsf(l));
@@ -708,10 +714,18 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       const double sig = (double)(l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t));
       const double n = (double)G.N;
       part[extra * K + k] = (float)(-n * softplus);
-      if (slot_a >= 0)
-        part[((int64_t)(1 + slot_a) * nseg + extra) * K + k] = w * (float)(-n * sig * (double)dl[p]);
+      if (slot_a >= 0) {
+        const float e = w * (float)(-n * sig * (double)dl[p]);
+        if (rank1) {
+          slot_part[nseg + k] = w * dl[p];       // f[k]
+          slot_part[nseg + K + k] = e;           // e[k]
+        } else {
+          slot_part[extra * K + k] = e;
+        }
+      }
     }
   }
+  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0 && c == 0) slot_part[extra] = 0.0f;
   publish_flags(flags, fl);
 }
 
@@ -721,6 +735,8 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
 struct FinalizeArgs {
   int32_t num_sites;
   int32_t num_slots;
+  int32_t rank1;      // bit v: value v in the rank-one layout (mi_reduce.rank1)
+  int32_t pad0;
   double scale[MI_MAX_SITES];  // num_sites <= MI_MAX_SITES
   double slot_scale;  // the group's grad_scale: slot gradients are speculative like dense ones
 };
@@ -784,16 +800,19 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const T* __restrict_
   const int v_begin = split ? (int)blockIdx.y : 0;
   const int v_end = split ? v_begin + 1 : nv;
   for (int v = v_begin; v < v_end; ++v) {
-    const T* p = part + (int64_t)v * nseg * K + kc;
+    const bool r1 = (A.rank1 >> v) & 1;
+    // rank one: the particle-independent u[seg] (stride 1) instead of the per-particle column
+    const T* p = part + (int64_t)v * nseg * K + (r1 ? 0 : kc);
+    const int64_t stride = r1 ? 1 : K;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     int64_t g = gl;
     for (; g + 3 * kFinG < nseg; g += 4 * kFinG) {
-      a0 += (double)p[g * K];
-      a1 += (double)p[(g + kFinG) * K];
-      a2 += (double)p[(g + 2 * kFinG) * K];
-      a3 += (double)p[(g + 3 * kFinG) * K];
+      a0 += (double)p[g * stride];
+      a1 += (double)p[(g + kFinG) * stride];
+      a2 += (double)p[(g + 2 * kFinG) * stride];
+      a3 += (double)p[(g + 3 * kFinG) * stride];
     }
-    for (; g < nseg; g += kFinG) a0 += (double)p[g * K];
+    for (; g < nseg; g += kFinG) a0 += (double)p[g * stride];
     __syncthreads();
     red[gl][kl] = (a0 + a1) + (a2 + a3);
     __syncthreads();
@@ -801,6 +820,10 @@ __global__ __launch_bounds__(kFinK * kFinG) void k_finalize(const T* __restrict_
       double acc = 0.0;
 #pragma unroll
       for (int j = 0; j < kFinG; ++j) acc += red[j][kl];
+      if (r1) {
+        const T* q = part + (int64_t)v * nseg * K + nseg;
+        acc = (double)q[kc] * acc + (double)q[K + kc];
+      }
       if (v < A.num_sites) {
         acc *= A.scale[v];
         if (site_lp != nullptr) site_lp[(int64_t)v * K + k] = acc;
@@ -1141,6 +1164,13 @@ size_t finalize_offset(const mi_group* g, const Plan& p) {
   return (prep_offset(g, p) + middle + 255) / 256 * 256;
 }
 
+// The slot value of a k_site_bcast_smem launch in the rank-one layout (mi_reduce.rank1): one
+// slot, and a segment list short enough for the one-launch finalize / the fused reduction.
+bool smem_rank1(const mi_group* g, const Plan& p) {
+  return g->num_slots == 1 && g->compute_grads && p.nseg >= 3 && p.nseg <= MI_REDUCE_MAX_SEG &&
+         env_int("MININF_AMD_BCAST_RANK1", 1) != 0;
+}
+
 template <int FAM>
 void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 block(mi::kBcastThreads);
@@ -1150,8 +1180,9 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   const int64_t side = (int64_t)p.grid.x - chunks;
   const int gy = (int)p.grid.y;
   const dim3 grid((unsigned)(ceil_div(chunks, 8) * 8 * gy + side));
+  const int rank1 = smem_rank1(&G, p) ? 1 : 0;
 #define MI_SMEM(P, CH) \
-  hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, flags)
+  hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, rank1, flags)
   switch (smem_variant()) {
     case 1: MI_SMEM(8, 4096); break;
     case 2: MI_SMEM(4, 8192); break;
@@ -1178,17 +1209,18 @@ size_t mi_finalize_scratch_bytes(int64_t nseg, int64_t K, int nv) {
 
 int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
                        const double* scale, double slot_scale, float* total, double* site_lp,
-                       float* slot_grad, double* scratch, hipStream_t stream) {
+                       float* slot_grad, double* scratch, hipStream_t stream, int rank1) {
   if (num_sites > MI_MAX_SITES) return MI_EINVAL;
   mi::FinalizeArgs A{};
   A.num_sites = num_sites;
   A.num_slots = num_slots;
+  A.rank1 = rank1;
   A.slot_scale = slot_scale;
   for (int i = 0; i < num_sites; ++i) A.scale[i] = scale[i];
   const int nv = num_sites + num_slots;
   const unsigned gx = (unsigned)ceil_div(K, mi::kFinK);
   const unsigned gy = num_sites == 1 ? (unsigned)nv : 1u;
-  if (scratch != nullptr && mi_finalize_scratch_bytes(nseg, K, nv) != 0) {
+  if (scratch != nullptr && mi_finalize_scratch_bytes(nseg, K, nv) != 0 && rank1 == 0) {
     // long segment lists: chunks of segments in parallel, then the chunk sums
     const int64_t nchunk = ceil_div(nseg, mi::kFinChunk);
     hipLaunchKernelGGL(mi::k_finalize_chunks, dim3(gx, (unsigned)nv, (unsigned)nchunk),
@@ -1375,12 +1407,15 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   }
   double scales[MI_MAX_SITES];
   for (int i = 0; i < reduced_lp; ++i) scales[i] = prescaled ? 1.0 : G.sites[i].scale;
+  // values in the rank-one layout: the slot of a k_site_bcast_smem launch (after the site value)
+  const int rank1_mask = (smem && smem_rank1(group, p)) ? (1 << reduced_lp) : 0;
   if (reduce != nullptr && p.nseg <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
     reduce->part = part;
     reduce->nseg = p.nseg;
     reduce->K = G.K;
     reduce->num_sites = reduced_lp;
     reduce->num_slots = G.num_slots;
+    reduce->rank1 = rank1_mask;
     for (int i = 0; i < reduced_lp; ++i) reduce->scale[i] = scales[i];
     reduce->slot_scale = (double)G.grad_scale;
     reduce->total = total;
@@ -1391,7 +1426,8 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) +
                                               finalize_offset(group, p));
   return mi_launch_finalize(part, p.nseg, G.K, reduced_lp, G.num_slots, scales,
-                            (double)G.grad_scale, total, site_lp, slot_grad, scratch, s);
+                            (double)G.grad_scale, total, site_lp, slot_grad, scratch, s,
+                            rank1_mask);
 }
 
 int mi_reduce_launch(const mi_reduce* r, void* stream) {
@@ -1402,7 +1438,7 @@ int mi_reduce_launch(const mi_reduce* r, void* stream) {
   // nseg <= MI_REDUCE_MAX_SEG: the one-launch finalize (no chunk scratch)
   return mi_launch_finalize(r->part, r->nseg, r->K, r->num_sites, r->num_slots, r->scale,
                             r->slot_scale, r->total, r->site_lp, r->slot_grad, nullptr,
-                            static_cast<hipStream_t>(stream));
+                            static_cast<hipStream_t>(stream), r->rank1);
 }
 
 int mi_group_draw_partials(const mi_group* group, size_t* offset_bytes, int64_t* rows) {
