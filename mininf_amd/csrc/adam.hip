@@ -65,19 +65,43 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
   const float step_size = (float)(A.lr / (double)bc1);
   const int64_t i0 = (int64_t)b * chunk;
   const int64_t i1 = min(T.numel, i0 + chunk);
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += kAdamThreads) {
-    float param = T.param[i];
-    float grad = T.grad[i];
+  auto update = [&](float& param, float grad, float& m, float& v) {
     if (A.maximize) grad = -grad;
-    if (A.weight_decay != 0.0) grad = (float)((double)grad + (double)param * A.weight_decay);
-    const float m = (float)(A.beta1 * (double)T.exp_avg[i] + (1.0 - A.beta1) * (double)grad);
-    const float v = (float)(A.beta2 * (double)T.exp_avg_sq[i] +
-                            (1.0 - A.beta2) * (double)grad * (double)grad);
+    // the contractions spelled out: fma(beta, moment, (1 - beta) * grad [* grad]), the form
+    // torch's kernel compiles to (the compiler may pick another when left to itself)
+    if (A.weight_decay != 0.0) grad = (float)fma((double)param, A.weight_decay, (double)grad);
+    m = (float)fma(A.beta1, (double)m, (1.0 - A.beta1) * (double)grad);
+    v = (float)fma(A.beta2, (double)v, ((1.0 - A.beta2) * (double)grad) * (double)grad);
     const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + A.eps);
     param -= step_size * m / denom;
-    T.param[i] = param;
-    T.exp_avg[i] = m;
-    T.exp_avg_sq[i] = v;
+  };
+  const bool vec = ((reinterpret_cast<uintptr_t>(T.param) | reinterpret_cast<uintptr_t>(T.grad) |
+                     reinterpret_cast<uintptr_t>(T.exp_avg) |
+                     reinterpret_cast<uintptr_t>(T.exp_avg_sq)) & 15) == 0;
+  int64_t i = i0 + 4 * (int64_t)threadIdx.x;
+  if (vec) {   // 16-byte loads and stores (chunk is a multiple of 4 * kAdamThreads)
+    for (; i + 3 < i1; i += 4 * kAdamThreads) {
+      float4 p = *reinterpret_cast<const float4*>(T.param + i);
+      const float4 g = *reinterpret_cast<const float4*>(T.grad + i);
+      float4 m = *reinterpret_cast<const float4*>(T.exp_avg + i);
+      float4 v = *reinterpret_cast<const float4*>(T.exp_avg_sq + i);
+      update(p.x, g.x, m.x, v.x);
+      update(p.y, g.y, m.y, v.y);
+      update(p.z, g.z, m.z, v.z);
+      update(p.w, g.w, m.w, v.w);
+      *reinterpret_cast<float4*>(T.param + i) = p;
+      *reinterpret_cast<float4*>(T.exp_avg + i) = m;
+      *reinterpret_cast<float4*>(T.exp_avg_sq + i) = v;
+    }
+  }
+  // the rest (the tail, or unaligned tensors) element by element
+  for (int64_t j = (vec ? i : i0 + threadIdx.x); j < i1; j += vec ? 1 : kAdamThreads) {
+    if (vec && j >= i + 4) break;
+    float p = T.param[j], m = T.exp_avg[j], v = T.exp_avg_sq[j];
+    update(p, T.grad[j], m, v);
+    T.param[j] = p;
+    T.exp_avg[j] = m;
+    T.exp_avg_sq[j] = v;
   }
 
   __syncthreads();   // every thread of the block has read the step
@@ -124,7 +148,7 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
     int64_t chunk = std::max<int64_t>(8 * mi::kAdamThreads,
                                       (T.numel + mi::kAdamGroup * mi::kAdamGroup - 1) /
                                           (mi::kAdamGroup * mi::kAdamGroup));
-    chunk = (chunk + mi::kAdamThreads - 1) / mi::kAdamThreads * mi::kAdamThreads;
+    chunk = (chunk + 4 * mi::kAdamThreads - 1) / (4 * mi::kAdamThreads) * (4 * mi::kAdamThreads);
     P.first[t] = blocks;
     P.chunk[t] = chunk;
     blocks += (int)((T.numel + chunk - 1) / chunk);

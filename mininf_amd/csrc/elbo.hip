@@ -795,13 +795,21 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
     return;
   }
   const int64_t rows = F.draw_kind == MI_DRAW_PARTIALS ? F.partial_rows : e->K;
-  int ti = 1;
-  while (ti < 64 && ti < F.n) ti <<= 1;
-  const int tk = mi::kElboThreads / ti;
-  const int64_t gx = ceil_div(F.n, ti);
   // rows per particle lane: one Beta gradient per thread (long fp64 chains) unless they were
   // precomputed (then 16: a column's sums usually fit one block, no cross-block completion)
   const int64_t per_lane = !forward_absorbed(F) ? 4 : (F.dgrad == nullptr ? 1 : 16);
+  // lanes along the rows: enough for per_lane rows each (few rows, e.g. a fused draw's
+  // per-particle-block partials: one lane, 256 elements per block); the rest along the elements
+  int tk = 1;
+  while (tk < mi::kElboThreads && tk < ceil_div(rows, per_lane)) tk <<= 1;
+  int ti = mi::kElboThreads / tk;
+  int ti_need = 1;
+  while (ti_need < ti && ti_need < F.n) ti_need <<= 1;
+  if (ti_need < ti) {   // fewer elements than lanes: more lanes along the rows
+    ti = ti_need;
+    tk = mi::kElboThreads / ti;
+  }
+  const int64_t gx = ceil_div(F.n, ti);
   int64_t slices = ceil_div(rows, (int64_t)tk * per_lane);
   slices = std::max<int64_t>(1, std::min<int64_t>(slices, ceil_div(2048, gx)));
   if (slices > 1 && counters + gx > kMaxCounters) slices = 1;

@@ -581,7 +581,10 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // rank1: the slot value is written in the rank-one layout of mi_reduce.rank1 (the chunk sums u[c]
 // from the particle-block-0 workgroups, f[k] = w dl_k and e[k] = -N w sigmoid(l_k) dl_k from the
 // chunk-0 workgroups) instead of one partial per (chunk, particle): half the partial slab.
-template <int FAMILY, int kSmemP, int kSmemChunk>
+// SUFF (MININF_AMD_BCAST_SUFFSTAT=1, a measurement of the floor, not the default): the
+// per-(particle, element) FMA loop replaced by its closed form l_k * sum_i x_i -- the same value
+// in exact arithmetic (C2's per-eval arithmetic is reducible).
+template <int FAMILY, int kSmemP, int kSmemChunk, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   // for all of them: one group of lookahead). Even and odd element pairs go to separate
   // accumulators, 2 kSmemP independent chains of 64 terms per block.
   constexpr int kGroup = 32, kBlock = 256;
-  const int nfull = len & ~(kBlock - 1);
+  const int nfull = SUFF ? 0 : len & ~(kBlock - 1);
   int j = 0;
   if (nfull > 0) {
     float xc[kGroup];
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       flush(in);
     }
   }
-  if (j < len) {   // the chunk's tail: element pairs, a zero for an odd last element
+  if (!SUFF && j < len) {   // the chunk's tail: element pairs, a zero for an odd last element
     f32x2 in[2][kSmemP];
 #pragma unroll
     for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
@@ -692,6 +695,10 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
     s_a += v;
   }
   s_a = block_sum(s_a, scratch);
+  if (SUFF) {
+#pragma unroll
+    for (int p = 0; p < kSmemP; ++p) acc[p] = (double)lg[p] * (double)s_a;
+  }
 
   // ---- partials of this chunk, and the particle-constant segment from the chunk-0 blocks -------
   const int o_a = st.operand[0];
@@ -1188,7 +1195,13 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
     case 2: MI_SMEM(4, 8192); break;
     case 3: MI_SMEM(8, 8192); break;
     case 4: MI_SMEM(8, 2048); break;
-    default: MI_SMEM(4, 4096); break;
+    default:
+      if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
+        hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096, true>), grid, block, bcast_lds(),
+                           s, G, part, p.nseg, gy, rank1, flags);
+      else
+        MI_SMEM(4, 4096);
+      break;
   }
 #undef MI_SMEM
 }
