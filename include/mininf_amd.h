@@ -265,7 +265,7 @@ int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
 
 /* ---- guide reparameterised sampling (replaces nn.py:133-145 -> Normal/Beta.rsample) ------------ */
 
-/* Counter-based Philox-4x32-10 normals: eps[k, i] is a function of (seed, step, stream_id,
+/* Counter-based Philox-4x32-7 normals: eps[k, i] is a function of (seed, step, stream_id,
  * particle_offset + k, i) only, so the union of draws is independent of how particles are sharded
  * across GPUs. z[k, i] = loc[i] + eps[k, i] * scale[i] (normal.py:83-86). If `eps` is non-NULL it is
  * used instead of the generator (parity mode: injected host noise, row-major [K, N]).

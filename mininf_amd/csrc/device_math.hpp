@@ -37,7 +37,7 @@ MI_DEV double digamma(double x) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Philox-4x32-10 (Salmon, Moraes, Dror, Shaw: "Parallel random numbers: as easy as 1, 2, 3",
+// Philox-4x32-R (Salmon, Moraes, Dror, Shaw: "Parallel random numbers: as easy as 1, 2, 3",
 // SC'11). Counter-based: the output is a pure function of (counter, key), which is what makes the
 // particle draws independent of the grid shape and of how particles are split across GPUs.
 // ---------------------------------------------------------------------------------------------
@@ -45,9 +45,10 @@ struct U4 {
   uint32_t x, y, z, w;
 };
 
-MI_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+template <int ROUNDS>
+MI_DEV U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int round = 0; round < 10; ++round) {
+  for (int round = 0; round < ROUNDS; ++round) {
     // one 32x32->64 multiply per word (v_mad_u64_u32) instead of separate low / high halves
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
@@ -60,8 +61,20 @@ MI_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// Uniform in the open interval (0, 1) from the top 24 bits (exactly representable in fp32).
-MI_DEV float u01(uint32_t bits) { return ((float)(bits >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+// The 10-round generator of the published known-answer vectors (mi_philox4x32).
+MI_DEV U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) { return philox4x32<10>(c, k0, k1); }
+
+// Rounds of the guide generator. Philox-4x32-7 passes TestU01's BigCrush (Salmon et al., table 2:
+// 7 rounds is the smallest Crush-resistant count; 10 is their default safety margin). The
+// fused-draw site programs spend ~1/4 of their VALU cycles here (v_mad_u64_u32 issues at ~3x an
+// FMA), so the guide uses 7; oracle/philox.c restates the same count.
+constexpr int kGuideRounds = 7;
+
+// Uniform in the open interval (0, 1) from the top 24 bits: ((bits >> 8) + 0.5) * 2^-24 as one FMA
+// (the same single rounding of the same exact value, scaled by a power of two).
+MI_DEV float u01(uint32_t bits) {
+  return fmaf((float)(bits >> 8), 5.9604644775390625e-08f, 2.98023223876953125e-08f);
+}
 
 // Two standard normals from two uniforms (Box-Muller) on the hardware transcendentals:
 // v_log_f32 (log2), v_sqrt_f32 and v_sin_f32 / v_cos_f32, which take their argument in
@@ -81,7 +94,7 @@ MI_DEV U4 guide_bits(uint64_t seed, uint64_t step, uint32_t stream_id, uint32_t 
                      uint64_t particle) {
   U4 c{(uint32_t)quad, (uint32_t)particle, (uint32_t)step ^ (uint32_t)(step >> 32),
        (stream_id << 8) | (sub & 0xFFu)};
-  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return philox4x32<kGuideRounds>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
 // eps for elements 4q .. 4q+3 of particle p.
@@ -107,6 +120,29 @@ MI_DEV double wave_sum(double v) {
   return v;
 }
 
+// Orders a wave's LDS accesses (lanes exchanging values through LDS): a wave's LDS operations
+// execute in issue order, so only the compiler has to be kept from moving them across this point.
+MI_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Row sums of a wave's [T][65] LDS tile (row p: the 64 lanes' values for particle p; the odd
+// stride keeps the column reads on distinct banks). Lane T * q + p adds columns [q T, q T + T) of
+// row p, then the 64 / T partial sums of a row meet in a shuffle tree; lane p < T returns row p.
+template <int T>
+MI_DEV float tile_row_sums(const float* tile, int lane) {
+  const int p = lane & (T - 1), q = lane / T;
+  const float* row = tile + p * 65 + q * T;
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < T; ++j) s += row[j];
+#pragma unroll
+  for (int offset = T; offset < kWave; offset <<= 1) s += __shfl_xor(s, offset, kWave);
+  return s;
+}
+
 // Sum over lanes that differ only in bits >= log2(width) (lanes sharing lane % width).
 MI_DEV float wave_sum_strided(float v, int width) {
   for (int offset = 32; offset >= width; offset >>= 1) v += __shfl_xor(v, offset, kWave);
@@ -130,13 +166,12 @@ MI_DEV float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 // smaller than every sum they enter.
 MI_DEV float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 
-// log1p(t), t in [0, 1]: u = 1 + t rounds, and log(u) * t / (u - 1) cancels the rounding of u
-// (Goldberg's trick); v_log_f32 is log2.
-MI_DEV float log1p_unit(float t) {
-  const float u = 1.0f + t;
-  const float d = u - 1.0f;
-  const float lg = __builtin_amdgcn_logf(u) * 0.69314718055994531f;
-  return d == 0.0f ? t : lg * (t * rcp(d));
+// log1p(t), t in [0, 1], from u = fl(1 + t) and ru = 1 / u (which the Bernoulli caller needs for
+// the sigmoid anyway): log(u) plus the first-order correction (t - (u - 1)) / u for the rounding
+// of u (u - 1 is exact for u in [1, 2]); v_log_f32 is log2. For t below half an ulp of 1, u = 1
+// and the result is t.
+MI_DEV float log1p_unit(float t, float u, float ru) {
+  return fmaf(t - (u - 1.0f), ru, __builtin_amdgcn_logf(u) * 0.69314718055994531f);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -154,7 +189,7 @@ struct Elem {
 MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
   const float inv = rcp(scale);
   const float z = (v - loc) * inv;
-  e.lp = -0.5f * z * z - logf(scale) - kHalfLog2Pi;
+  e.lp = fmaf(-0.5f * z, z, -(logf(scale) + kHalfLog2Pi));
   e.d[0] = z * inv;
   e.d[1] = (z * z - 1.0f) * inv;
   e.d[2] = -z * inv;
@@ -167,11 +202,12 @@ MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
 // The streaming site programs evaluate this per (particle, element), so it is written with the
 // hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp each) instead of libm's
 // correctly-rounded-ish expf/log1pf/division sequences (~100 VALU ops per element on gfx950):
-// log1p(t) for t in [0, 1] uses log(u) * t / (u - 1) with u = 1 + t, exact to a few ulp.
+// log1p(t) for t in [0, 1] is log(u) corrected for the rounding of u = 1 + t (log1p_unit).
 MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
   const float t = fast_exp(-fabsf(l));
-  e.lp = -(fmaxf(l, 0.0f) - l * v + log1p_unit(t));
-  const float r = rcp(1.0f + t);
+  const float u = 1.0f + t;
+  const float r = rcp(u);
+  e.lp = -(fmaxf(l, 0.0f) - l * v + log1p_unit(t, u, r));
   const float sig = l >= 0.0f ? r : t * r;
   e.d[0] = v - sig;
   e.d[1] = 0.0f;

@@ -164,7 +164,7 @@ struct Stream {
     if (used == 4) {
       U4 c{(uint32_t)elem, (uint32_t)particle, (uint32_t)step ^ (uint32_t)(step >> 32),
            (stream_id << 8) | (sub << 6) | (block & 63u)};
-      bits = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      bits = philox4x32<kGuideRounds>(c, (uint32_t)seed, (uint32_t)(seed >> 32));
       ++block;
       used = 0;
     }

@@ -17,6 +17,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -183,6 +184,11 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "  const int lane = threadIdx.x & 63;\n";
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
+  // LDS of the row loops' particle sums: nv tiles of [tile_rows][65] floats per wave
+  const int tile_rows = nv <= 2 ? 16 : 8;
+  if (row)
+    o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
+      << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";
   for (int s = 0; s < g.num_sites; ++s) {
     o << "  unsigned fl" << s << " = 0u;\n";
     o << "  const float scale" << s << " = (float)G.sites[" << s << "].scale;\n";
@@ -268,6 +274,24 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       if (mask_is(s, kDense)) o << in << "bool " << prefix << "m" << s << "[" << Es << "];\n";
   };
 
+  // Per-particle sums over the wave's elements (the row loops): each particle's lane values go to
+  // a [tile_rows][65] LDS tile of the wave, and every tile_rows particles the wave sums the rows
+  // (mi::tile_row_sums: tile_rows columns per lane, then a shuffle tree over the row's lanes) --
+  // about one LDS write, one LDS read and one add per particle and value, where a shuffle
+  // reduction per particle costs six exchanges and six adds.
+  auto emit_particle_sums = [&](const char* in) {
+    for (int v = 0; v < nv; ++v)
+      o << in << "tile[" << v * tile_rows * 65 << " + r * 65 + lane] = " << value_expr(v) << ";\n";
+    o << in << "if (r == " << tile_rows - 1 << " || k + 1 == k_end) {\n";
+    o << in << "  mi::wave_lds_sync();\n";
+    for (int v = 0; v < nv; ++v)
+      o << in << "  { const float t = mi::tile_row_sums<" << tile_rows << ">(tile + "
+        << v * tile_rows * 65 << ", lane);\n" << in << "    if (lane <= r) part[((long)" << v
+        << " * nseg + seg) * K + (k - r) + lane] = t; }\n";
+    o << in << "  mi::wave_lds_sync();\n";
+    o << in << "}\n";
+  };
+
   // One copy of the row loop (see below). Element e of the lane: `ie` in the clamped copy.
   auto emit_row_loop = [&](bool full) {
     const std::string ie = full ? "(base + e * 64 + lane)" : "idx[e]";
@@ -326,9 +350,8 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << in << "if (k_begin < k_end) {\n";
     row_loads("        ", "n", "k_begin");
     o << in << "}\n";
-    for (int v = 0; v < nv; ++v) o << in << "float keep" << v << " = 0.0f;\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
-    o << in << "  const int r = (int)((k - k_begin) & 63);\n";
+    o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     declare_dense("        ", "d");
     for (int op = 0; op < g.num_operands; ++op)
       if (is(op, kDense))
@@ -363,16 +386,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
             << ") gx" << op << "[k * gsk" << op << " + " << ie << " * gsi" << op
             << "] = G.grad_scale * g" << op << "[e];\n";
       }
-    for (int v = 0; v < nv; ++v)
-      o << in2 << "{ const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
-        << " = (lane == r) ? t : keep" << v << "; }\n";
-    o << in2 << "if (r == 63 || k + 1 == k_end) {\n";
-    o << in2 << "  if (lane <= r) {\n";
-    for (int v = 0; v < nv; ++v)
-      o << in2 << "    part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
-    o << in2 << "  }\n";
-    for (int v = 0; v < nv; ++v) o << in2 << "  keep" << v << " = 0.0f;\n";
-    o << in2 << "}\n";
+    emit_particle_sums(in2);
     o << in << "}\n";
   };
 
@@ -412,9 +426,8 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     if (dgrad)
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
         << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
-    for (int v = 0; v < nv; ++v) o << in << "float keep" << v << " = 0.0f;\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
-    o << in << "  const int r = (int)((k - k_begin) & 63);\n";
+    o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
       << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
          "+ qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
@@ -447,16 +460,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << " + base + lane * 4;\n#pragma unroll\n" << in2 << "for (int e = 0; e < " << E
           << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * g" << op << "[e]; }\n";
     }
-    for (int v = 0; v < nv; ++v)
-      o << in2 << "{ const float t = mi::wave_sum(" << value_expr(v) << "); keep" << v
-        << " = (lane == r) ? t : keep" << v << "; }\n";
-    o << in2 << "if (r == 63 || k + 1 == k_end) {\n";
-    o << in2 << "  if (lane <= r) {\n";
-    for (int v = 0; v < nv; ++v)
-      o << in2 << "    part[((long)" << v << " * nseg + seg) * K + (k - r) + lane] = keep" << v << ";\n";
-    o << in2 << "  }\n";
-    for (int v = 0; v < nv; ++v) o << in2 << "  keep" << v << " = 0.0f;\n";
-    o << in2 << "}\n";
+    emit_particle_sums(in2);
     o << in << "}\n";
     if (dgrad)
       o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) if (ok[e]) {\n"
@@ -592,6 +596,14 @@ Compiled compile(const std::string& source) {
   Compiled out;
   std::vector<char> code;
   std::string log;
+  if (const char* dir = std::getenv("MININF_AMD_JIT_DUMP")) {   // diagnostics: keep the source
+    static int serial = 0;
+    const std::string path = std::string(dir) + "/site_program_" + std::to_string(serial++) + ".hip";
+    if (FILE* f = fopen(path.c_str(), "w")) {
+      fwrite(source.data(), 1, source.size(), f);
+      fclose(f);
+    }
+  }
   if (!compile_only(source, &code, &log)) {
     if (std::getenv("MININF_AMD_JIT_VERBOSE") != nullptr)
       fprintf(stderr, "mininf_amd: site program failed to compile:\n%s\n%s\n", log.c_str(),

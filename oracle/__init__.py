@@ -8,7 +8,7 @@ checker for the HIP path:
 * ``logprob``   -- per-family log densities and gradients in numpy float64;
 * ``elbo``      -- K-particle ELBO values and gradients for configs C1-C5 (numpy float64) with
                    injected guide noise;
-* ``philox.c``  -- plain-C Philox-4x32-10 + Box-Muller restatement of the guide generator;
+* ``philox.c``  -- plain-C Philox-4x32 (7 rounds; 10 for the known-answer vectors) + Box-Muller restatement of the guide generator;
 * ``cpu_port``  -- the reference's single-particle torch-CPU semantics, timed as ``cpu_baseline``.
 
 Parity is pinned: every function here is checked against the golden fixtures in ``tests/golden``,

@@ -1,7 +1,7 @@
 /*
  * oracle/philox.c -- TEST INFRASTRUCTURE ONLY.
  *
- * Plain-C restatement of the guide generator of mininf_amd (csrc/common.hpp): Philox-4x32-10
+ * Plain-C restatement of the guide generator of mininf_amd (csrc/device_math.hpp): Philox-4x32-7
  * (Salmon, Moraes, Dror, Shaw, SC'11) and the Box-Muller transform on 24-bit uniforms, with the
  * counter layout documented in include/mininf_amd.h (mi_normal_rsample). Built by oracle/build.py
  * with gcc into oracle/liboracle.so and used by the tests to pin the device generator bit-exactly
@@ -22,9 +22,12 @@ static void round_fn(uint32_t c[4], uint32_t k0, uint32_t k1) {
   c[3] = lo0;
 }
 
-void oracle_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+/* Philox-4x32 with `rounds` rounds (10: the published known-answer vectors; 7: the guide
+ * generator, GUIDE_ROUNDS, device_math.hpp kGuideRounds). */
+void oracle_philox4x32(const uint32_t ctr[4], uint32_t k0, uint32_t k1, int rounds,
+                       uint32_t out[4]) {
   uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < rounds; ++r) {
     round_fn(c, k0, k1);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -34,6 +37,12 @@ void oracle_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint3
   out[2] = c[2];
   out[3] = c[3];
 }
+
+void oracle_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+  oracle_philox4x32(ctr, k0, k1, 10, out);
+}
+
+enum { GUIDE_ROUNDS = 7 };
 
 static float u01(uint32_t bits) { return ((float)(bits >> 8) + 0.5f) * 5.9604644775390625e-08f; }
 
@@ -45,7 +54,7 @@ void oracle_guide_normals(int64_t K, int64_t N, uint64_t seed, uint64_t step, ui
       const uint32_t ctr[4] = {(uint32_t)q, (uint32_t)(particle_offset + k),
                                (uint32_t)step ^ (uint32_t)(step >> 32), stream_id << 8};
       uint32_t b[4];
-      oracle_philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), b);
+      oracle_philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), GUIDE_ROUNDS, b);
       float n[4];
       for (int j = 0; j < 2; ++j) {
         const double r = sqrt(-2.0 * log((double)u01(b[2 * j])));
