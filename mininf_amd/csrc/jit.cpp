@@ -141,8 +141,9 @@ void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, const std::
   if (st.mask != nullptr) obs = "(" + obs + " && " + mask_var(st, s) + ")";
   o << in << "  const bool obs = " << obs << ";\n";
   o << in << "  lp" << s << " += obs ? el.lp : 0.0f;\n";
-  o << in << "  fl" << s << " |= (el.param_bad ? " << MI_FLAG_PARAM
-    << "u : 0u) | ((obs && el.support_bad) ? " << MI_FLAG_SUPPORT << "u : 0u);\n";
+  // lane-mask booleans (scalar ORs of the compare results), turned into flag bits once at the end
+  o << in << "  pb" << s << " |= el.param_bad;\n" << in << "  sb" << s
+    << " |= obs && el.support_bad;\n";
   if (g.compute_grads) {
     bool any = false;
     for (int q = 0; q < 3; ++q) {
@@ -190,7 +191,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
       << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";
   for (int s = 0; s < g.num_sites; ++s) {
-    o << "  unsigned fl" << s << " = 0u;\n";
+    o << "  bool pb" << s << " = false, sb" << s << " = false;\n";
     o << "  const float scale" << s << " = (float)G.sites[" << s << "].scale;\n";
     for (int q = 0; q < 3; ++q)
       if (g.sites[s].operand[q] < 0 && role_used(g.sites[s].family, q))
@@ -540,7 +541,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << "  }\n";
   }
   // dense masks use the names "dm<s>" inside rows; map mask_var's "md<s>[e]" onto them
-  for (int s = 0; s < g.num_sites; ++s) o << "  mi::publish_flags(flags + " << s << ", fl" << s << ");\n";
+  for (int s = 0; s < g.num_sites; ++s)
+    o << "  mi::publish_flags(flags + " << s << ", (pb" << s << " ? " << MI_FLAG_PARAM << "u : 0u) | (sb"
+      << s << " ? " << MI_FLAG_SUPPORT << "u : 0u));\n";
   o << "}\n";
   std::string text = o.str();
   for (int s = 0; s < g.num_sites; ++s) {
