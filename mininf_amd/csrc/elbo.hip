@@ -323,7 +323,7 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
 
 // ---- deferred site finalize reductions (mi_elbo.reduce) ---------------------------------------
 // Block (job a, particle block kb, value v) sums part[v][seg][k] over the job's segments for 64
-// particles: 4 segment groups of 64 lanes, eight loads in flight per lane, partial sums in fp64
+// particles: 4 segment groups of 64 lanes, up to sixteen loads in flight per lane, partial sums in fp64
 // combined in a fixed order -- the arithmetic of sites.hip k_finalize, fused into this launch.
 // Jobs with one site value split their values over blocks (as k_finalize's split mode).
 // Long segment lists use blocks of 32 particles x 8 segment groups (more blocks, fewer serial load
@@ -425,12 +425,22 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
     const int64_t stride = r1 ? 1 : K;
     double acc = 0.0;
     int64_t g = gl;
-    for (; g + 7 * kRedG < J.nseg; g += 8 * kRedG) {
+    // sixteen loads in flight per lane (a C2-sized list, ~250 segments over 8 groups, is two
+    // rounds of memory latency instead of four)
+    for (; g + 15 * kRedG < J.nseg; g += 16 * kRedG) {
+      float x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) x[j] = p[(g + j * kRedG) * stride];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc += (double)x[j];
+    }
+    if (g + 7 * kRedG < J.nseg) {
       float x[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * stride];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += (double)x[j];
+      g += 8 * kRedG;
     }
     for (; g < J.nseg; g += kRedG) acc += (double)p[g * stride];
     __syncthreads();

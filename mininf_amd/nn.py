@@ -213,6 +213,32 @@ class ParameterizedFactorizedDistribution(nn.ModuleDict):
         return FactorizedDistribution({name: module() for name, module in self.items()})
 
 
+_UNIT: Dict[torch.device, torch.Tensor] = {}
+
+
+class _Loss(torch.Tensor):
+    """
+    The loss tensor the fused ELBO returns: an ordinary 0-d tensor (operations on it give plain
+    tensors) whose ``backward()`` seeds autograd with a cached device 1.0 instead of
+    ``torch.ones_like(loss)`` -- otherwise a fill launch in every (captured) training step.
+    """
+    __torch_function__ = torch._C._disabled_torch_function_impl
+
+    def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
+        if gradient is None and self.dim() == 0 and self.is_cuda and not create_graph:
+            gradient = _UNIT.get(self.device)
+            if gradient is None and not torch.cuda.is_current_stream_capturing():
+                gradient = _UNIT[self.device] = torch.ones((), dtype=self.dtype,
+                                                           device=self.device)
+            if gradient is not None and gradient.dtype != self.dtype:
+                gradient = None
+        torch.Tensor.backward(self, gradient, retain_graph, create_graph, inputs)
+
+    def __repr__(self, *, tensor_contents=None):
+        return torch._tensor_str._str(self, tensor_contents=tensor_contents).replace(
+            type(self).__name__ + "(", "tensor(", 1)
+
+
 class EvidenceLowerBoundLoss(nn.Module):
     """
     Negative evidence lower bound, estimated with ``num_particles`` Monte-Carlo particles on the
@@ -346,6 +372,8 @@ class EvidenceLowerBoundLoss(nn.Module):
             if rest:
                 extra = cast(torch.Tensor, sum(f.entropy().sum() for f in rest))
                 loss = loss - (extra / world if world > 1 else extra)
+            if loss.is_cuda and loss.dim() == 0 and type(loss) is torch.Tensor:
+                loss.__class__ = _Loss   # the same tensor object and autograd node
         else:
             joint = engine.log_joint(trace, g0, device)
             entropy = approximation.entropy()
