@@ -588,9 +588,12 @@ template <int FAMILY, int kSmemP, int kSmemChunk, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
-                                                                   int rank1,
+                                                                   int mode,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
+  // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below)
+  const int rank1 = mode & 1;
+  const bool balance = (mode & 2) != 0;
   const int64_t chunks = nseg - 1;
   const int64_t padded = (chunks + 7) / 8 * 8;
   const int64_t b = blockIdx.x;
@@ -652,6 +655,19 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
 #pragma unroll
     for (int e = 0; e < kGroup; ++e) xc[e] = xs[e];
     for (; j < nfull; j += kBlock) {
+      // Progress-balanced priority: a wave drops one priority level per quarter of its chunk, so
+      // the SIMD's arbiter (priority, then age) lets the waves behind it catch up; the waves of a
+      // SIMD then finish together instead of the oldest first, which would leave the last one
+      // issuing alone (at half the VALU rate) through the kernel's tail.
+      if (balance) {
+        const int quarter = (4 * j) / nfull;
+        if (quarter != (4 * (j - kBlock)) / nfull || j == 0) {
+          if (quarter == 0) __builtin_amdgcn_s_setprio(3);
+          else if (quarter == 1) __builtin_amdgcn_s_setprio(2);
+          else if (quarter == 2) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+      }
       f32x2 in[2][kSmemP];
 #pragma unroll
       for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
@@ -1187,7 +1203,7 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   const int64_t side = (int64_t)p.grid.x - chunks;
   const int gy = (int)p.grid.y;
   const dim3 grid((unsigned)(ceil_div(chunks, 8) * 8 * gy + side));
-  const int rank1 = smem_rank1(&G, p) ? 1 : 0;
+  const int rank1 = (smem_rank1(&G, p) ? 1 : 0) | (env_int("MININF_AMD_BCAST_BALANCE", 1) ? 2 : 0);
 #define MI_SMEM(P, CH) \
   hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, rank1, flags)
   switch (smem_variant()) {
