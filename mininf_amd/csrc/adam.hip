@@ -80,18 +80,42 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
                      reinterpret_cast<uintptr_t>(T.exp_avg_sq)) & 15) == 0;
   int64_t i = i0 + 4 * (int64_t)threadIdx.x;
   if (vec) {   // 16-byte loads and stores (chunk is a multiple of 4 * kAdamThreads)
-    for (; i + 3 < i1; i += 4 * kAdamThreads) {
-      float4 p = *reinterpret_cast<const float4*>(T.param + i);
-      const float4 g = *reinterpret_cast<const float4*>(T.grad + i);
-      float4 m = *reinterpret_cast<const float4*>(T.exp_avg + i);
-      float4 v = *reinterpret_cast<const float4*>(T.exp_avg_sq + i);
+    float4* __restrict__ param = reinterpret_cast<float4*>(T.param);
+    const float4* __restrict__ grad = reinterpret_cast<const float4*>(T.grad);
+    float4* __restrict__ exp_avg = reinterpret_cast<float4*>(T.exp_avg);
+    float4* __restrict__ exp_avg_sq = reinterpret_cast<float4*>(T.exp_avg_sq);
+    auto step4 = [&](float4& p, const float4& g, float4& m, float4& v) {
       update(p.x, g.x, m.x, v.x);
       update(p.y, g.y, m.y, v.y);
       update(p.z, g.z, m.z, v.z);
       update(p.w, g.w, m.w, v.w);
-      *reinterpret_cast<float4*>(T.param + i) = p;
-      *reinterpret_cast<float4*>(T.exp_avg + i) = m;
-      *reinterpret_cast<float4*>(T.exp_avg_sq + i) = v;
+    };
+    // two quads per lane per pass: all eight 16-byte loads in flight before the first update
+    constexpr int64_t kStride = 4 * kAdamThreads;
+    for (; i + kStride + 3 < i1; i += 2 * kStride) {
+      const int64_t q0 = i >> 2, q1 = (i + kStride) >> 2;
+      float4 p0 = param[q0], p1 = param[q1];
+      const float4 g0 = grad[q0], g1 = grad[q1];
+      float4 m0 = exp_avg[q0], m1 = exp_avg[q1];
+      float4 v0 = exp_avg_sq[q0], v1 = exp_avg_sq[q1];
+      step4(p0, g0, m0, v0);
+      step4(p1, g1, m1, v1);
+      param[q0] = p0;
+      param[q1] = p1;
+      exp_avg[q0] = m0;
+      exp_avg[q1] = m1;
+      exp_avg_sq[q0] = v0;
+      exp_avg_sq[q1] = v1;
+    }
+    for (; i + 3 < i1; i += kStride) {
+      const int64_t q = i >> 2;
+      float4 p = param[q];
+      const float4 g = grad[q];
+      float4 m = exp_avg[q], v = exp_avg_sq[q];
+      step4(p, g, m, v);
+      param[q] = p;
+      exp_avg[q] = m;
+      exp_avg_sq[q] = v;
     }
   }
   // the rest (the tail, or unaligned tensors) element by element

@@ -120,6 +120,19 @@ MI_DEV double wave_sum(double v) {
   return v;
 }
 
+// Progress-balanced wave priority for loops whose waves share SIMDs for their whole length: one
+// s_setprio level less per quarter of the loop (step `i` of `n`), so the arbiter (priority, then
+// age) lets the waves behind catch up and a SIMD's waves finish together rather than the oldest
+// first -- a wave left issuing alone runs at half the VALU rate.
+MI_DEV void balance_priority(long i, long n) {
+  const long q = (4 * i) / n;
+  if (i != 0 && q == (4 * (i - 1)) / n) return;
+  if (q == 0) __builtin_amdgcn_s_setprio(3);
+  else if (q == 1) __builtin_amdgcn_s_setprio(2);
+  else if (q == 2) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 // Orders a wave's LDS accesses (lanes exchanging values through LDS): a wave's LDS operations
 // execute in issue order, so only the compiler has to be kept from moving them across this point.
 MI_DEV void wave_lds_sync() {

@@ -119,6 +119,7 @@ struct AbsorbPlan {
   int64_t counter[MI_MAX_FACTORS];   // first completion counter of the factor's columns
   int64_t partial[MI_MAX_FACTORS];   // offset (doubles) of its [slices, n, 2] partial sums
   int32_t pre[MI_MAX_FACTORS];       // 1: a Beta factor whose [n, 4] forward sums are in F.saved
+  int32_t epl[MI_MAX_FACTORS];       // elements per lane (4: a backward over a few partial rows)
 };
 
 // Block-dependent selections from the by-value kernel descriptors, written as unrolled
@@ -232,6 +233,42 @@ MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int
   }
 }
 
+// Backward of a draw whose particle sums arrive as a few partial rows (MI_DRAW_PARTIALS): lane
+// elements base + e * ti, e < 4 -- every load of the four elements (partial rows, the parameters
+// for the entropy and exp-transform terms) in flight before the first gradient is stored.
+MI_DEV void partial_lane_elements(const mi_factor& F, int64_t base, int ti, int64_t rows, float u,
+                                  double w) {
+  constexpr int kE = 4;
+  double g[kE][2];
+  bool ok[kE];
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    const int64_t i = base + (int64_t)e * ti;
+    ok[e] = i < F.n;
+    const int64_t ic = ok[e] ? i : 0;
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t r = 0; r < rows; ++r) {
+      s0 += (double)F.partial[0][r * F.n + ic];
+      s1 += (double)F.partial[1][r * F.n + ic];
+    }
+    double d0, d1;
+    entropy_grad(F, ic, d0, d1);
+    g[e][0] = (double)u * s0 + w * d0;
+    g[e][1] = (double)u * s1 + w * d1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (F.transform[j] == MI_TRANSFORM_EXP) g[e][j] *= (double)F.param[j][ic * F.stride[j]];
+  }
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
+    if (!ok[e]) continue;
+    const int64_t i = base + (int64_t)e * ti;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (F.grad[j] != nullptr) F.grad[j][i * F.grad_stride[j]] = (float)g[e][j];
+  }
+}
+
 // One block of absorbed-factor work (block `bid` of the absorbed range). FORWARD: Beta factors,
 // leaving pre[i] = {S0, S1, dH0, dH1}; backward: everything else, writing the gradients.
 template <bool FORWARD>
@@ -263,6 +300,29 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   const int64_t r0 = (int64_t)slice * rows_per_slice;
   const int64_t r1 = min(rows, r0 + rows_per_slice);
   double s0 = 0.0, s1 = 0.0;
+  if (!FORWARD && pick(P.epl, a) == 4) {   // a fused draw's few partial rows: 4 elements per lane
+    partial_lane_elements(F, (int64_t)col * ti * 4 + tx, ti, rows, u, w);
+    return;
+  }
+  if (tk == 1 && slices == 1) {   // a lane per element: no block reduction, and no barrier
+                                  // between its loads
+    if (i < F.n) {
+      draw_sums<FORWARD>(F, i, r0, r1, 1, s0, s1);
+      double d0, d1;
+      entropy_grad(F, i, d0, d1);
+      if (FORWARD) {
+        double* pre = F.saved + 4 * i;
+        pre[0] = s0;
+        pre[1] = s1;
+        pre[2] = d0;
+        pre[3] = d1;
+      } else {
+        write_grad(F, 0, i, (double)u * s0 + w * d0);
+        write_grad(F, 1, i, (double)u * s1 + w * d1);
+      }
+    }
+    return;
+  }
   if (i < F.n) draw_sums<FORWARD>(F, i, r0 + ty, r1, tk, s0, s1);
   red[threadIdx.x][0] = s0;
   red[threadIdx.x][1] = s1;
@@ -797,6 +857,7 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
   P.pre[a] = 0;
   if (!forward && finish) {   // finish only: one element per thread
     P.pre[a] = 1;
+    P.epl[a] = 1;
     P.ti[a] = mi::kElboThreads;
     P.gx[a] = (int)ceil_div(F.n, mi::kElboThreads);
     P.slices[a] = 1;
@@ -825,8 +886,10 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
   if (slices > 1 && counters + gx > kMaxCounters) slices = 1;
   const int64_t rps = ceil_div(rows, slices);
   slices = ceil_div(rows, rps);
+  // a backward over a few partial rows, one lane per element: four elements per lane instead
+  P.epl[a] = (!forward && F.draw_kind == MI_DRAW_PARTIALS && tk == 1 && slices == 1) ? 4 : 1;
   P.ti[a] = ti;
-  P.gx[a] = (int)gx;
+  P.gx[a] = (int)(P.epl[a] == 4 ? ceil_div(F.n, (int64_t)ti * 4) : gx);
   P.slices[a] = (int)slices;
   P.rows_per_slice[a] = rps;
   P.counter[a] = counters;
@@ -835,7 +898,7 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
     counters += gx;
     doubles += slices * F.n * 2;
   }
-  blocks += (int)(gx * slices);
+  blocks += (int)(P.gx[a] * slices);
 }
 
 // particles per reducing block for long segment lists (MININF_AMD_ELBO_KRED: 16, 32 or 64)

@@ -100,7 +100,7 @@ std::string mask_kind_tag(const mi_site& st) {
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
-    << plan.waves_per_eu << "|"
+    << plan.waves_per_eu << (plan.balance ? "b" : "") << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -352,6 +352,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     row_loads("        ", "n", "k_begin");
     o << in << "}\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
+    if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     declare_dense("        ", "d");
     for (int op = 0; op < g.num_operands; ++op)
@@ -428,6 +429,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
         << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
+    if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
       << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "

@@ -13,6 +13,7 @@ struct PlanInfo {
   int kw;          // COL: lanes per element group (power of two <= 64)
   bool combined;   // reduce one weighted log-joint value per particle instead of one per site
   int waves_per_eu;  // occupancy target handed to the compiler (0 = compiler's choice)
+  bool balance;    // ROW: progress-balanced wave priority over the particle loop
   unsigned grid_x;
   unsigned grid_y;
 };

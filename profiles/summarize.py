@@ -4,11 +4,17 @@ files committed here:
 
 * ``<round>_<cfg>_kernel_stats.csv`` -- rocprofv3 ``--kernel-trace --stats`` summary (as written by
   rocprofv3; kernel names shortened), graph-replay steps as benched;
-* ``<round>_pmc.json`` -- per-launch HBM bytes of each config's dominant kernel from the two PMC
-  passes (``--pmc FETCH_SIZE`` and ``--pmc WRITE_SIZE``, separate runs, eager steps), with
-  FETCH_SIZE doubled: on gfx950 it reports half the bytes of a coalesced streaming read
-  (MI355X_MICROARCH.md, HBM section; confirmed on our own kernels, whose algorithmic read bytes
-  are known).
+* ``<round>_pmc.json`` -- per-launch HBM bytes of each config's dominant kernel (and of the step's
+  other large kernels, under ``"others"``) from the two PMC passes (``--pmc FETCH_SIZE`` and
+  ``--pmc WRITE_SIZE``, separate runs, eager steps), with FETCH_SIZE doubled for vector-memory
+  kernels: on gfx950 it reports half the bytes of a coalesced streaming read (MI355X_MICROARCH.md,
+  HBM section; confirmed on our own kernels, whose algorithmic read bytes are known, see
+  DESIGN.md). The C2 site kernel reads its data through the scalar unit (64-byte s_load), which
+  FETCH_SIZE counts in full (4 MB of x -> 4.33 MB raw): no doubling there.
+* ``<round>_valu_pmc.json`` -- issue counters of the VALU-bound kernels (``SQ_INSTS_VALU`` and its
+  per-type split, ``GRBM_GUI_ACTIVE``), with the VALU pipe's busy fraction from measured issue
+  costs (tools/valu_peak.hip: 2 cycles per wave64 instruction, 4 for v_pk_fma_f32, 8 for a
+  transcendental, 6 for v_mad_u64_u32).
 
 Usage: python profiles/summarize.py r01 [gpurun_out]
 """
@@ -26,8 +32,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 DOMINANT = {
     "c2": r"k_site_bcast",
     "c3": r"k_linear",
+    "c4": r"k_linear",
     "c5": r"mi_site_program|k_group_row",
 }
+# raw FETCH_SIZE -> bytes: 2 for vector-memory streaming (the gfx950 correction), 1 for the
+# scalar-load C2 kernel (calibrated against its 4 MB of data)
+FETCH_SCALE = {"c2": 1.0}
+OTHERS = r"k_elbo_forward|k_elbo_backward|k_adam_step|k_minibatch_rows|k_finalize"
 
 
 def short(name: str) -> str:
@@ -62,6 +73,10 @@ def counters(raw: str, kind: str, cfg: str):
     return per
 
 
+def per_launch(values):
+    return sum(values) / len(values) if values else None
+
+
 def pmc(raw: str, round_tag: str) -> None:
     result = {}
     for cfg, pattern in DOMINANT.items():
@@ -74,18 +89,72 @@ def pmc(raw: str, round_tag: str) -> None:
         if not keys:
             continue
         key = max(keys, key=lambda k: k[1])
-        f = fetch[key]
-        wv = write.get(key, [])
-        fetch_b = 2.0 * 1024.0 * sum(f) / len(f)            # KB -> B, x2 gfx950 correction
-        write_b = 1024.0 * sum(wv) / len(wv) if wv else None
-        result[cfg] = {
-            "kernel": key[0], "grid_size": key[1], "launches": len(f),
-            "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
-            "traffic_bytes_per_launch": fetch_b + (write_b or 0.0),
-            "raw_fetch_size_kb": sum(f) / len(f),
-            "raw_write_size_kb": (sum(wv) / len(wv)) if wv else None,
-        }
+        scale = FETCH_SCALE.get(cfg, 2.0)
+
+        def entry(k, fetch_scale):
+            f, wv = per_launch(fetch.get(k, [])), per_launch(write.get(k, []))
+            fetch_b = fetch_scale * 1024.0 * f if f is not None else None
+            write_b = 1024.0 * wv if wv is not None else None
+            return {"kernel": k[0], "grid_size": k[1], "launches": len(fetch.get(k, [])),
+                    "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+                    "traffic_bytes_per_launch": (fetch_b or 0.0) + (write_b or 0.0),
+                    "raw_fetch_size_kb": f, "raw_write_size_kb": wv,
+                    "fetch_scale": fetch_scale}
+        result[cfg] = entry(key, scale)
+        result[cfg]["others"] = [entry(k, 2.0) for k in sorted(fetch)
+                                 if k != key and re.search(OTHERS, k[0])]
     with open(os.path.join(HERE, f"{round_tag}_pmc.json"), "w") as fh:
+        json.dump(result, fh, indent=1)
+
+
+# issue cost in SIMD cycles per wave64 instruction (tools/valu_peak.hip on MI355X)
+COST = {"plain": 2.0, "pk_fma": 4.0, "trans": 8.0, "int64": 6.0}
+SIMDS = 1024
+XCDS = 8
+
+
+def valu(raw: str, round_tag: str) -> None:
+    result = {}
+    for cfg, pattern in DOMINANT.items():
+        per = {}
+        for kind in ("valu", "vtype"):
+            src = os.path.join(raw, f"{kind}_{cfg}", "run_counter_collection.csv")
+            if not os.path.exists(src):
+                continue
+            rows = [r for r in csv.DictReader(open(src)) if re.search(pattern, r["Kernel_Name"])]
+            if not rows:
+                continue
+            grid = max(int(r["Grid_Size"]) for r in rows)
+            acc = collections.defaultdict(list)
+            dur = {}
+            for r in rows:
+                if int(r["Grid_Size"]) != grid:
+                    continue
+                acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+                dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            per.update({n: sum(v) / len(v) for n, v in acc.items()})
+            per["kernel"] = short(rows[0]["Kernel_Name"])
+            per[f"{kind}_us"] = sum(dur.values()) / len(dur) / 1e3
+        if "SQ_INSTS_VALU" not in per or "GRBM_GUI_ACTIVE" not in per:
+            continue
+        cycles = per["GRBM_GUI_ACTIVE"] / XCDS
+        us = per.get("vtype_us", per.get("valu_us"))
+        per["clock_ghz"] = cycles / (us * 1e3)
+        if "SQ_INSTS_VALU_TRANS_F32" in per:
+            trans = per["SQ_INSTS_VALU_TRANS_F32"]
+            int64 = per.get("SQ_INSTS_VALU_INT64", 0.0)
+            fma = per.get("SQ_INSTS_VALU_FMA_F32", 0.0)
+            # the C2 kernel's FMAs are packed (v_pk_fma_f32, 4 cycles); elsewhere scalar
+            pk = fma if cfg == "c2" else 0.0
+            plain = per["SQ_INSTS_VALU"] - trans - int64 - pk
+            busy = (plain * COST["plain"] + pk * COST["pk_fma"] + trans * COST["trans"] +
+                    int64 * COST["int64"])
+            per["valu_issue_cycles"] = busy
+            per["valu_busy"] = busy / (SIMDS * cycles)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in per:
+            per["mfma_busy"] = per["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cycles)
+        result[cfg] = per
+    with open(os.path.join(HERE, f"{round_tag}_valu_pmc.json"), "w") as fh:
         json.dump(result, fh, indent=1)
 
 
@@ -95,6 +164,7 @@ def main() -> None:
     for cfg in ("c2", "c3", "c4", "c5"):
         kernel_stats(raw, round_tag, cfg)
     pmc(raw, round_tag)
+    valu(raw, round_tag)
 
 
 if __name__ == "__main__":
