@@ -783,6 +783,10 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
             lg = _float(logits, site.name)
             lg = lg.reshape((K,) + (1,) * (len(shape) + 1 - (lg.dim() - 1)) + tuple(lg.shape[1:]))
             lg = lg.expand((K,) + tuple(shape) + (C,)).reshape(K, N, C).contiguous()
+            if value.is_floating_point():
+                # non-integer (or NaN) values are outside integer_interval(0, C - 1): -1 makes
+                # the kernel flag them instead of the cast truncating them into the support
+                value = torch.where(value == value.trunc(), value, torch.full_like(value, -1.0))
             val = _collapse(value.to(torch.int64), K, shape).tensor.expand(K, N)
             mask = None if site.mask is None else site.mask.to(device).bool().expand(shape) \
                 .reshape(1, N).expand(K, N)
