@@ -370,7 +370,14 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     elapsed, mode = eager_elapsed * steps / eager_steps, "eager"
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
-        captured = StepGraph(forward_backward, warmup=2)
+        # one replay = `repeat` consecutive steps (N = 1): each graph launch leaves the device
+        # idle ~13 us, which a launch-bound step amortises (mininf_amd.graph.StepGraph)
+        repeat = 1
+        if world == 1:
+            repeat = args.graph_repeat or next(r for r in (4, 2, 1) if steps % r == 0)
+            if steps % repeat:
+                raise SystemExit(f"--graph-repeat {repeat} does not divide --steps {steps}")
+        captured = StepGraph(forward_backward, warmup=2, repeat=repeat)
         update = StepGraph(apply_update, warmup=1) if world > 1 else None
 
         def graph_step():
@@ -381,11 +388,25 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 return bucket.loss()
             return out
 
-        for _ in range(warmup):
+        for _ in range(max(1, warmup // repeat)):
             graph_step()
-        elapsed, loss = timed(graph_step, steps)
+        elapsed, loss = timed(graph_step, steps // repeat)
         captured.check()
-        mode = "hipGraph replay"
+        mode = "hipGraph replay" + (f" ({repeat} steps per replay)" if repeat > 1 else "")
+        floor_ms = None
+        if config == "c2" and world == 1:
+            # C2's per-eval sum over x_i l_k is reducible to l_k sum_i x_i:
+            # the same step with the site kernel's closed form, reported beside the per-eval number
+            os.environ["MININF_AMD_BCAST_SUFFSTAT"] = "1"
+            try:
+                floor_graph = StepGraph(forward_backward, warmup=2, repeat=repeat)
+                for _ in range(max(1, warmup // repeat)):
+                    floor_graph()
+                floor_s, _ = timed(floor_graph, steps // repeat)
+                floor_graph.check()
+                floor_ms = 1e3 * floor_s / steps
+            finally:
+                del os.environ["MININF_AMD_BCAST_SUFFSTAT"]
 
     if args.profile_host and rank == 0:
         import cProfile
@@ -433,6 +454,11 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                         f" + {args.dist_backend} grad all-reduce") if world > 1 else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms,
+                   **({"reducible_floor_ms_per_step": floor_ms,
+                       "reducible_floor_note": "the same step with the site kernel evaluating "
+                       "sum_i x_i l_k as l_k sum_i x_i (MININF_AMD_BCAST_SUFFSTAT=1); value and "
+                       "roofline are the per-eval path"} if args.graph and floor_ms is not None
+                      else {}),
                    "optimizer": ("mininf_amd.optim.Adam (one HIP launch)" if args.optimizer == "mi"
                                  else "torch.optim.Adam(fused=True)")},
         "roofline": roof,
@@ -445,6 +471,9 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--graph-repeat", type=int, default=0,
+                    help="steps captured per graph replay at N = 1 (0: 4, 2 or 1, whichever "
+                         "divides --steps)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2")

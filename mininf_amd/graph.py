@@ -134,9 +134,18 @@ class StepGraph:
             that gradient buffers are allocated inside the graph's memory pool.
         warmup: Eager warm-up iterations on a side stream before capture (compiles the specialised
             site programs, fills caches, initialises library handles).
+        repeat: Consecutive steps captured into the one graph (each replay runs ``repeat`` full
+            steps). Every graph launch costs the device ~13 us of idle time between the last
+            kernel of one replay and the first of the next on MI355X; a launch-bound step (a few
+            dozen microseconds of kernels) amortises it over ``repeat`` steps. The step must keep
+            its per-step state on the device (generator counter, minibatch counter, optimizer
+            step counts), as the engine's own steps do.
     """
-    def __init__(self, step: Callable[[], object], warmup: int = 3) -> None:
+    def __init__(self, step: Callable[[], object], warmup: int = 3, repeat: int = 1) -> None:
+        if repeat < 1:
+            raise ValueError("repeat must be a positive integer")
         self.step = step
+        self.repeat = repeat
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         count = 0
@@ -161,26 +170,42 @@ class StepGraph:
         self._joints: List = []
         with graph_safe(self._joints), _capture_safe_distributions(), \
                 torch.cuda.graph(self.graph):
-            self.output = step()
-            flags = [joint.flag_vector() for joint in self._joints]
-            flags = [f for f in flags if f is not None]
+            for _ in range(repeat):
+                self.output = step()
+            if len(self._joints) % repeat:
+                raise RuntimeError("the captured steps recorded different validations")
+            per_step = len(self._joints) // repeat
+            # one step's validations: what the host checks (every captured step ORs into the
+            # same words)
+            steps = [self._joints[r * per_step:(r + 1) * per_step] for r in range(repeat)]
             mirror = None
-            if len(self._joints) == 1 and flags and self._joints[0].sticky and \
-                    flags[0] is self._joints[0].flags:
-                self._flags_device = flags[0]
+            sticky = [j[0] for j in steps] if per_step == 1 else []
+            if sticky and all(j.sticky and j.flag_vector() is not None and
+                              j.flag_vector() is j.flags and
+                              j.flags.data_ptr() == sticky[0].flags.data_ptr() for j in sticky):
+                self._flags_device = sticky[0].flags
                 self._accumulator = None
-                mirror = self._joints[0].mirror
-            elif flags:
-                vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
-                    else flags[0]
-                if vector.numel() != count:
-                    raise RuntimeError(f"the captured step has {vector.numel()} validation words, "
-                                       f"its warm-up steps {count}")
-                self._accumulator.bitwise_or_(vector)
-                self._flags_device = self._accumulator
+                mirror = sticky[0].mirror
             else:
-                self._flags_device = None
-                self._accumulator = None
+                any_flags = False
+                for joints in steps:
+                    flags = [joint.flag_vector() for joint in joints]
+                    flags = [f for f in flags if f is not None]
+                    if not flags:
+                        continue
+                    any_flags = True
+                    vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
+                        else flags[0]
+                    if vector.numel() != count:
+                        raise RuntimeError(f"the captured step has {vector.numel()} validation "
+                                           f"words, its warm-up steps {count}")
+                    self._accumulator.bitwise_or_(vector)
+                if any_flags:
+                    self._flags_device = self._accumulator
+                else:
+                    self._flags_device = None
+                    self._accumulator = None
+            self._joints = steps[0]
         # The ELBO forward of a sticky step writes its words to pinned host memory itself (the
         # mirror); otherwise the copy is enqueued after each replay (one small asynchronous D2H
         # copy: pinned host memory cannot be allocated while capturing).

@@ -54,6 +54,32 @@ def test_graph_replays_match_eager_steps(device):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
 
 
+def test_multi_step_replays_match_eager_steps(device):
+    """StepGraph(repeat=3): each replay runs three full steps (the bench's launch amortisation);
+    losses of every third step and the parameters match eager steps."""
+    eager_step, eager_module, _ = coin_setup(device)
+    graph_body, graph_module, _ = coin_setup(device)
+    eager_losses = [float(eager_step()) for _ in range(2 + 3 * 3)]
+    captured = StepGraph(graph_body, warmup=2, repeat=3)
+    graph_losses = [float(captured()) for _ in range(3)]
+    captured.check()
+    torch.testing.assert_close(torch.tensor(graph_losses),
+                               torch.tensor(eager_losses[2 + 2::3]), rtol=1e-6, atol=0)
+    for a, b in zip(eager_module.parameters(), graph_module.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
+
+
+def test_multi_step_replay_raises_validation_errors(device):
+    body, _, x = coin_setup(device)
+    captured = StepGraph(body, warmup=2, repeat=2)
+    captured()
+    captured.check()
+    x[3] = 2.0   # outside Bernoulli's support: found by a replay, raised by the next check
+    captured()
+    with pytest.raises(ValueError, match="is not in the support"):
+        captured.check()
+
+
 def test_graph_defers_validation_errors(device):
     body, _, x = coin_setup(device)
     captured = StepGraph(body, warmup=2)
