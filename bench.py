@@ -374,7 +374,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         # idle ~13 us, which a launch-bound step amortises (mininf_amd.graph.StepGraph)
         repeat = 1
         if world == 1:
-            repeat = args.graph_repeat or next(r for r in (4, 2, 1) if steps % r == 0)
+            repeat = args.graph_repeat or next(r for r in (8, 6, 5, 4, 3, 2, 1) if steps % r == 0)
             if steps % repeat:
                 raise SystemExit(f"--graph-repeat {repeat} does not divide --steps {steps}")
         captured = StepGraph(forward_backward, warmup=2, repeat=repeat)
@@ -472,7 +472,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--graph-repeat", type=int, default=0,
-                    help="steps captured per graph replay at N = 1 (0: 4, 2 or 1, whichever "
+                    help="steps captured per graph replay at N = 1 (0: the largest of 8, 6, 5, 4, 3, 2, 1 that "
                          "divides --steps)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
