@@ -14,6 +14,7 @@
 #include "internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 namespace mi {
@@ -169,7 +170,12 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
         T.exp_avg_sq == nullptr || T.step == nullptr || T.numel < 1)
       return MI_EINVAL;
     // at most kAdamGroup^2 blocks per tensor, 8 elements per thread at least
-    int64_t chunk = std::max<int64_t>(8 * mi::kAdamThreads,
+    static const int64_t min_chunk = [] {   // elements per block at least (MININF_AMD_ADAM_CHUNK)
+      const char* v = std::getenv("MININF_AMD_ADAM_CHUNK");
+      const int64_t n = v != nullptr ? std::atoll(v) : 8 * mi::kAdamThreads;
+      return std::max<int64_t>(4 * mi::kAdamThreads, n);
+    }();
+    int64_t chunk = std::max<int64_t>(min_chunk,
                                       (T.numel + mi::kAdamGroup * mi::kAdamGroup - 1) /
                                           (mi::kAdamGroup * mi::kAdamGroup));
     chunk = (chunk + 4 * mi::kAdamThreads - 1) / (4 * mi::kAdamThreads) * (4 * mi::kAdamThreads);

@@ -100,7 +100,7 @@ std::string mask_kind_tag(const mi_site& st) {
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
-    << plan.waves_per_eu << (plan.balance ? "b" : "") << "|"
+    << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -428,6 +428,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     if (dgrad)
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
         << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
+    if (plan.unroll > 1) o << "#pragma unroll " << plan.unroll << "\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";

@@ -14,6 +14,7 @@ struct PlanInfo {
   bool combined;   // reduce one weighted log-joint value per particle instead of one per site
   int waves_per_eu;  // occupancy target handed to the compiler (0 = compiler's choice)
   bool balance;    // ROW: progress-balanced wave priority over the particle loop
+  int unroll;      // fused-draw row loop: particles unrolled per iteration (1 = none)
   unsigned grid_x;
   unsigned grid_y;
 };

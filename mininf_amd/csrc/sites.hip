@@ -1157,6 +1157,7 @@ PlanInfo plan_info(const Plan& p, bool combined) {
   info.elems = p.shape == kRow ? p.elems : std::max(1, env_int("MININF_AMD_COL_UNROLL",
                                                                      kColUnroll));
   info.waves_per_eu = env_int("MININF_AMD_WAVES_PER_EU", 0);
+  info.unroll = std::max(1, env_int("MININF_AMD_DRAW_UNROLL", 1));
   info.balance = info.row && env_int("MININF_AMD_ROW_BALANCE", 0) != 0;   // measured: no gain on C5 (two rounds of waves, not a lone-wave tail)
   info.kw = p.kw;
   info.grid_x = p.grid.x;
