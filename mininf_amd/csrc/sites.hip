@@ -704,11 +704,37 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   }
 
   // ---- chunk sum and support flags (vector loads, L2-resident by now) --------------------------
+  // Each lane takes kSmemChunk / kBcastThreads consecutive elements with all its loads in flight
+  // at once (a strided loop waits for one L2 round trip per element group, at the end of every
+  // wave).
+  constexpr int kPerLane = kSmemChunk / kBcastThreads;
+  static_assert(kPerLane % 4 == 0, "whole float4 groups per lane");
   float s_a = 0.0f;
-  for (int i = threadIdx.x; i < len; i += kBcastThreads) {
-    const float v = xg[i0 + i];
-    fl |= !(v == 0.0f || v == 1.0f) ? MI_FLAG_SUPPORT : 0u;
-    s_a += v;
+  {
+    const int e0 = (int)threadIdx.x * kPerLane;
+    const float* xl = xg + i0 + e0;
+    if (e0 + kPerLane <= len && (reinterpret_cast<uintptr_t>(xl) & 15) == 0) {
+      float v[kPerLane];
+#pragma unroll
+      for (int q = 0; q < kPerLane / 4; ++q) {
+        const float4 t = reinterpret_cast<const float4*>(xl)[q];
+        v[4 * q] = t.x;
+        v[4 * q + 1] = t.y;
+        v[4 * q + 2] = t.z;
+        v[4 * q + 3] = t.w;
+      }
+#pragma unroll
+      for (int e = 0; e < kPerLane; ++e) {
+        fl |= !(v[e] == 0.0f || v[e] == 1.0f) ? MI_FLAG_SUPPORT : 0u;
+        s_a += v[e];
+      }
+    } else {
+      for (int e = e0; e < len && e < e0 + kPerLane; ++e) {
+        const float v = xg[i0 + e];
+        fl |= !(v == 0.0f || v == 1.0f) ? MI_FLAG_SUPPORT : 0u;
+        s_a += v;
+      }
+    }
   }
   s_a = block_sum(s_a, scratch);
   if (SUFF) {
