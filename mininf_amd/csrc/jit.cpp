@@ -428,6 +428,10 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     if (dgrad)
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
         << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kParticle))
+        o << in << "float pn" << op << " = k_begin < k_end ? x" << op << "[k_begin * sk" << op
+          << "] : 0.0f;\n";
     if (plan.unroll > 1) o << "#pragma unroll " << plan.unroll << "\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
@@ -443,7 +447,15 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << "  { const float* __restrict__ r = x" << op << " + k * sk" << op
           << " + base + lane * 4;\n#pragma unroll\n" << in << "  for (int e = 0; e < " << E
           << "; ++e) d" << op << "[e] = r[(e >> 2) * 256 + (e & 3)]; }\n";
-    particle_loads("      ", "k");
+    // per-particle operands: next row's values loaded one iteration ahead (a scalar load waited
+    // on right away would stall the wave for its L2 round trip every row)
+    for (int op = 0; op < g.num_operands; ++op)
+      if (is(op, kParticle))
+        o << in << "  const float p" << op << " = pn" << op << ";\n" << in << "  if (k + 1 < k_end) pn"
+          << op << " = x" << op << "[(k + 1) * sk" << op << "];\n";
+    for (int st = 0; st < g.num_sites; ++st)
+      if (mask_is(st, kParticle))
+        o << in << "  const bool mp" << st << " = mk" << st << "[k * msk" << st << "] != 0;\n";
     zero_accumulators("      ");
     const char* in2 = "      ";
     for (int op = 0; op < g.num_operands; ++op)
