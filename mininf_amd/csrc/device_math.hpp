@@ -200,12 +200,17 @@ struct Elem {
 // Normal(loc, scale): -(v-loc)^2 / (2 scale^2) - log(scale) - log(sqrt(2 pi))
 // torch/distributions/normal.py:88-103; support real (constraints.py: `value == value`).
 MI_DEV void eval_normal(float loc, float scale, float v, Elem& e) {
+  // in terms of diff = v - loc: -diff^2 / (2 sigma^2) - log sigma - log sqrt(2 pi), and
+  // d/dloc = diff / sigma^2 -- with a constant scale, (-0.5 / sigma^2) and 1 / sigma^2 are loop
+  // invariants and an element costs four instructions
   const float inv = rcp(scale);
-  const float z = (v - loc) * inv;
-  e.lp = fmaf(-0.5f * z, z, -(logf(scale) + kHalfLog2Pi));
-  e.d[0] = z * inv;
-  e.d[1] = (z * z - 1.0f) * inv;
-  e.d[2] = -z * inv;
+  const float inv2 = inv * inv;
+  const float diff = v - loc;
+  e.lp = fmaf((-0.5f * inv2) * diff, diff, -(logf(scale) + kHalfLog2Pi));
+  const float g = diff * inv2;
+  e.d[0] = g;
+  e.d[1] = fmaf(diff, g, -1.0f) * inv;   // (z^2 - 1) / sigma, z = diff / sigma
+  e.d[2] = -g;
   e.param_bad = !(scale > 0.0f) || (loc != loc);
   e.support_bad = (v != v);
 }
