@@ -925,7 +925,11 @@ Layout make_layout(const mi_elbo* e) {
     const mi_reduce& J = e->reduce[r];
     L.red.first[r] = nred;
     L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
-    L.red.kred[r] = (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred() : mi::kRedKWide;
+    // long lists over few particles (a fused draw's block rows: ~1000 segments, K = 128): 16
+    // particles x 16 segment groups per block, for more blocks and fewer serial loads per lane
+    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? 16
+                    : (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred()
+                                                                     : mi::kRedKWide;
     nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
   }
   L.red.first[L.red.num] = nred;

@@ -100,7 +100,8 @@ std::string mask_kind_tag(const mi_site& st) {
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
-    << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll << "|"
+    << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll
+    << (plan.block_rows ? "B" : "") << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -280,16 +281,36 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   // (mi::tile_row_sums: tile_rows columns per lane, then a shuffle tree over the row's lanes) --
   // about one LDS write, one LDS read and one add per particle and value, where a shuffle
   // reduction per particle costs six exchanges and six adds.
-  auto emit_particle_sums = [&](const char* in) {
+  // block_rows: the block's four waves combine their row sums in LDS (fixed wave order) and write
+  // one partial row per block (gridDim.x rows) -- a quarter of the partials, short enough for the
+  // ELBO forward's fused reduction; every wave then runs the loop (see emit_draw_loop).
+  auto emit_particle_sums = [&](const char* in, bool block_rows) {
     for (int v = 0; v < nv; ++v)
       o << in << "tile[" << v * tile_rows * 65 << " + r * 65 + lane] = " << value_expr(v) << ";\n";
     o << in << "if (r == " << tile_rows - 1 << " || k + 1 == k_end) {\n";
     o << in << "  mi::wave_lds_sync();\n";
-    for (int v = 0; v < nv; ++v)
-      o << in << "  { const float t = mi::tile_row_sums<" << tile_rows << ">(tile + "
-        << v * tile_rows * 65 << ", lane);\n" << in << "    if (lane <= r) part[((long)" << v
-        << " * nseg + seg) * K + (k - r) + lane] = t; }\n";
-    o << in << "  mi::wave_lds_sync();\n";
+    if (!block_rows) {
+      for (int v = 0; v < nv; ++v)
+        o << in << "  { const float t = mi::tile_row_sums<" << tile_rows << ">(tile + "
+          << v * tile_rows * 65 << ", lane);\n" << in << "    if (lane <= r) part[((long)" << v
+          << " * nseg + seg) * K + (k - r) + lane] = t; }\n";
+      o << in << "  mi::wave_lds_sync();\n";
+    } else {
+      for (int v = 0; v < nv; ++v)
+        o << in << "  { const float t = mi::tile_row_sums<" << tile_rows << ">(tile + "
+          << v * tile_rows * 65 << ", lane);\n" << in << "    if (lane < " << tile_rows
+          << ") bsum[(" << v << " * 4 + (threadIdx.x >> 6)) * " << tile_rows << " + lane] = t; }\n";
+      o << in << "  __syncthreads();\n";
+      o << in << "  if (threadIdx.x < " << tile_rows << " && (int)threadIdx.x <= r) {\n";
+      for (int v = 0; v < nv; ++v)
+        o << in << "    part[((long)" << v << " * gridDim.x + blockIdx.x) * K + (k - r) + threadIdx.x] = "
+          << "((bsum[(" << v << " * 4) * " << tile_rows << " + threadIdx.x] + bsum[(" << v
+          << " * 4 + 1) * " << tile_rows << " + threadIdx.x]) + bsum[(" << v << " * 4 + 2) * "
+          << tile_rows << " + threadIdx.x]) + bsum[(" << v << " * 4 + 3) * " << tile_rows
+          << " + threadIdx.x];\n";
+      o << in << "  }\n";
+      o << in << "  __syncthreads();\n";
+    }
     o << in << "}\n";
   };
 
@@ -388,7 +409,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
             << ") gx" << op << "[k * gsk" << op << " + " << ie << " * gsi" << op
             << "] = G.grad_scale * g" << op << "[e];\n";
       }
-    emit_particle_sums(in2);
+    emit_particle_sums(in2, false);
     o << in << "}\n";
   };
 
@@ -404,11 +425,12 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     auto elem = [&](const char* e) {
       return std::string("((") + e + " >> 2) * 256 + lane * 4 + (" + e + " & 3))";
     };
-    o << in << "const long nominal = seg * " << 64 * E << "L;\n";
+    o << in << "const long nominal = " << (plan.block_rows ? "seg_c" : "seg") << " * " << 64 * E
+      << "L;\n";
     o << in << "const long shift = max(0L, nominal + " << 64 * E << "L - N);\n";
     o << in << "const long base = nominal - shift;\n";
     o << in << "bool ok[" << E << "];\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
-      << "; ++e) ok[e] = " << elem("e") << " >= shift;\n";
+      << "; ++e) ok[e] = " << (plan.block_rows ? "live && " : "") << elem("e") << " >= shift;\n";
     for (int op = 0; op < g.num_operands; ++op)
       if (is(op, kShared))
         o << in << "float s" << op << "[" << E << "];\n" << in << "{ const float* __restrict__ r = x"
@@ -476,7 +498,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << " + base + lane * 4;\n#pragma unroll\n" << in2 << "for (int e = 0; e < " << E
           << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * g" << op << "[e]; }\n";
     }
-    emit_particle_sums(in2);
+    emit_particle_sums(in2, plan.block_rows);
     o << in << "}\n";
     if (dgrad)
       o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) if (ok[e]) {\n"
@@ -492,7 +514,16 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
          "*G.draw.step_device : 0ull);\n";
     o << "  const unsigned dstream = G.draw.stream_id;\n";
     o << "  const long dpoff = G.draw.particle_offset;\n";
-    o << "  if (seg < nseg) {\n";
+    if (plan.block_rows) {
+      // every wave runs the loop (block barriers at the flushes): a wave past the last segment
+      // re-reads the last one with all of its elements masked off
+      o << "  __shared__ float bsum[" << nv * 4 * tile_rows << "];\n";
+      o << "  const bool live = seg < nseg;\n";
+      o << "  {\n";
+      o << "    const long seg_c = live ? seg : nseg - 1;\n";
+    } else {
+      o << "  if (seg < nseg) {\n";
+    }
     o << "    const long k_begin = (long)blockIdx.y * arg;\n";
     o << "    const long k_end = min(K, k_begin + arg);\n";
     emit_draw_loop();

@@ -15,6 +15,7 @@ struct PlanInfo {
   int waves_per_eu;  // occupancy target handed to the compiler (0 = compiler's choice)
   bool balance;    // ROW: progress-balanced wave priority over the particle loop
   int unroll;      // fused-draw row loop: particles unrolled per iteration (1 = none)
+  bool block_rows; // fused-draw row loop: one partial row per block (gridDim.x rows), not per wave
   unsigned grid_x;
   unsigned grid_y;
 };

@@ -1112,6 +1112,7 @@ unsigned bcast_lds() {
 
 struct Plan {
   Shape shape;
+  bool draw = false;       // a fused guide draw (mi_draw)
   int elems;               // ROW: elements per lane per row
   int64_t nseg;
   int64_t rows_per_block;  // ROW
@@ -1148,6 +1149,7 @@ Plan make_plan(const mi_group* g) {
   const bool short_rows = g->N < 256 && g->draw.operand == 0;
   if ((row || row_fallback) && !short_rows) {
     p.shape = kRow;
+    p.draw = g->draw.operand != 0;
     // fused draws: one Philox quad per lane and row keeps the register footprint at 4 waves/SIMD
     p.elems = g->draw.operand != 0 ? (env_int("MININF_AMD_DRAW_ELEMS", 4) == 8 ? 8 : 4)
                                    : row_elems();
@@ -1184,6 +1186,9 @@ PlanInfo plan_info(const Plan& p, bool combined) {
                                                                      kColUnroll));
   info.waves_per_eu = env_int("MININF_AMD_WAVES_PER_EU", 0);
   info.unroll = std::max(1, env_int("MININF_AMD_DRAW_UNROLL", 1));
+  // fused draws: the block's four waves combine their particle sums (a quarter of the partial rows:
+  // C5's 3907 segments become 977 rows, within the ELBO forward's fused reduction)
+  info.block_rows = info.row && p.draw && env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0;
   info.balance = info.row && env_int("MININF_AMD_ROW_BALANCE", 0) != 0;   // measured: no gain on C5 (two rounds of waves, not a lone-wave tail)
   info.kw = p.kw;
   info.grid_x = p.grid.x;
@@ -1360,6 +1365,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   const bool combined = site_lp == nullptr;
   int reduced_lp = G.num_sites;
   bool prescaled = false;  // partials already carry the site scales
+  int64_t prows = p.nseg;   // partial rows written (fused-draw programs: one per block)
   float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
   if (group->draw.operand != 0 && (p.shape != kRow || !draw_supported(group))) return MI_EUNSUPPORTED;
   if (group->side.out != nullptr && !(p.shape == kBcast && bcast_smem(group))) return MI_EUNSUPPORTED;
@@ -1430,6 +1436,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
       if (rc == 0) {
         prescaled = combined;
         reduced_lp = combined ? 1 : G.num_sites;
+        if (info.block_rows) prows = (int64_t)p.grid.x;
         break;
       }
       if (G.draw.operand != 0) return MI_EUNSUPPORTED;  // fused draws need the specialised kernel
@@ -1466,9 +1473,9 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   for (int i = 0; i < reduced_lp; ++i) scales[i] = prescaled ? 1.0 : G.sites[i].scale;
   // values in the rank-one layout: the slot of a k_site_bcast_smem launch (after the site value)
   const int rank1_mask = (smem && smem_rank1(group, p)) ? (1 << reduced_lp) : 0;
-  if (reduce != nullptr && p.nseg <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
+  if (reduce != nullptr && prows <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
     reduce->part = part;
-    reduce->nseg = p.nseg;
+    reduce->nseg = prows;
     reduce->K = G.K;
     reduce->num_sites = reduced_lp;
     reduce->num_slots = G.num_slots;
@@ -1482,7 +1489,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   }
   double* scratch = reinterpret_cast<double*>(static_cast<char*>(workspace) +
                                               finalize_offset(group, p));
-  return mi_launch_finalize(part, p.nseg, G.K, reduced_lp, G.num_slots, scales,
+  return mi_launch_finalize(part, prows, G.K, reduced_lp, G.num_slots, scales,
                             (double)G.grad_scale, total, site_lp, slot_grad, scratch, s,
                             rank1_mask);
 }
