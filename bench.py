@@ -474,8 +474,8 @@ def main():
     ap.add_argument("--graph-repeat", type=int, default=0,
                     help="steps captured per graph replay at N = 1 (0: the largest of 8, 6, 5, 4, 3, 2, 1 that "
                          "divides --steps)")
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--eager", dest="graph", action="store_false",

@@ -109,7 +109,11 @@ class ParameterizedDistribution(nn.Module):
                 sources[name] = (unconstrained, "identity")
             else:
                 forward = _forward_transform(transform)
-                arguments[name] = forward(unconstrained)
+                if isinstance(forward, distributions.ExpTransform) and unconstrained.is_cuda and \
+                        unconstrained.dtype == torch.float32:
+                    arguments[name] = _ExpFn.apply(unconstrained)   # one mi_transform_params
+                else:
+                    arguments[name] = forward(unconstrained)
                 if isinstance(forward, distributions.ExpTransform):
                     sources[name] = (unconstrained, "exp")
         distribution = self.distribution_cls(**arguments, **self.distribution_constants)
@@ -146,6 +150,31 @@ class ParameterizedDistribution(nn.Module):
         beta._mininf_amd_sources = {  # type: ignore[attr-defined]
             "concentration1": (u1, "exp"), "concentration0": (u0, "exp")}
         return beta
+
+
+class _ExpFn(torch.autograd.Function):
+    """``exp(u)`` of a positive-constrained guide parameter (``transform_to(positive)``,
+    nn.py:91-96) as one ``mi_transform_params`` launch."""
+    @staticmethod
+    def forward(ctx, u: torch.Tensor):  # type: ignore[override]
+        out = torch.empty(u.shape, dtype=torch.float32, device=u.device)
+        if u.numel() > 0:
+            flat = u.reshape(-1)
+            P = _native.Params()
+            P.m, P.n = 1, flat.numel()
+            P.u[0] = flat.data_ptr()
+            P.stride[0] = flat.stride(0) if flat.numel() > 1 else 0
+            P.transform[0] = _native.TRANSFORM_EXP
+            _native.check(_native.lib().mi_transform_params(ctypes.byref(P), out.data_ptr(),
+                                                            _native.stream_handle(u.device)),
+                          "mi_transform_params")
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad: torch.Tensor):  # type: ignore[override]
+        (out,) = ctx.saved_tensors
+        return grad * out   # d exp(u) / du = exp(u)
 
 
 class _ExpStackFn(torch.autograd.Function):
