@@ -683,29 +683,41 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
 #pragma unroll
     for (int q = 0; q < kMaxTails; ++q) {
       if (q >= R.tails) break;
-      double sum[2];
-#pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        double acc = 0.0;
-        for (int b = threadIdx.x; b < nshare; b += kElboThreads)
-          acc += __hip_atomic_load(&work[R.tail_part + ((int64_t)q * nshare + b) * 2 + c2],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // both sums through one fixed-order tree (red[][0] and red[][1]); the three trigammas of the
+      // entropy derivatives on lanes 0-2 meanwhile
+      double acc0 = 0.0, acc1 = 0.0;
+      for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
+        const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
+        acc0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const float a = *R.tail_c1[q], b = *R.tail_c0[q];
+      const float tsum = a + b;
+      const float tg = threadIdx.x == 0 ? trigammaf(tsum)
+                       : threadIdx.x == 1 ? trigammaf(a)
+                       : threadIdx.x == 2 ? trigammaf(b) : 0.0f;
+      __syncthreads();
+      red[threadIdx.x][0] = acc0;
+      red[threadIdx.x][1] = acc1;
+      __shared__ float tgs[3];
+      if (threadIdx.x < 3) tgs[threadIdx.x] = tg;
+      __syncthreads();
+      for (int half = kElboThreads >> 1; half > 0; half >>= 1) {
+        if ((int)threadIdx.x < half) {
+          red[threadIdx.x][0] += red[threadIdx.x + half][0];
+          red[threadIdx.x][1] += red[threadIdx.x + half][1];
+        }
         __syncthreads();
-        rsum[threadIdx.x] = acc;
-        __syncthreads();
-        lds_tree(rsum, kElboThreads);
-        sum[c2] = rsum[0];
       }
       if (threadIdx.x == 0) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
-        const float a = *R.tail_c1[q], b = *R.tail_c0[q];
-        const float tsum = a + b;
-        const float tt = (tsum - 2.0f) * trigammaf(tsum);
+        const float tt = (tsum - 2.0f) * tgs[0];
         double* pre = R.tail_saved[q];
-        pre[0] = sum[0];
-        pre[1] = sum[1];
-        pre[2] = (double)(tt - (a - 1.0f) * trigammaf(a));
-        pre[3] = (double)(tt - (b - 1.0f) * trigammaf(b));
+        pre[0] = red[0][0];
+        pre[1] = red[0][1];
+        pre[2] = (double)(tt - (a - 1.0f) * tgs[1]);
+        pre[3] = (double)(tt - (b - 1.0f) * tgs[2]);
       }
+      __syncthreads();
     }
   }
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=

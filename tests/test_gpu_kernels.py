@@ -832,3 +832,42 @@ def test_categorical_model_against_oracle(device, float_values):
         bad = torch.masked.as_masked_tensor(frac, torch.as_tensor(mask, device=device))
         with pytest.raises(ValueError, match="is not in the support"):
             mi.nn.EvidenceLowerBoundLoss(num_particles=K)(mi.condition(model, y=bad), approx())
+
+
+def test_elbo_loss_tensor_and_guide_exp(device):
+    """
+    The fused ELBO's loss is a plain-looking 0-d tensor whose backward() seeds autograd with a
+    cached device 1.0 (no fill launch): same gradients as an explicit ones seed, repr as a tensor,
+    and operations on it give ordinary tensors. A positive guide parameter's exp runs in
+    mi_transform_params: values equal torch.exp's, and its autograd backward is exp(u).
+    """
+    from torch.distributions import Bernoulli, Beta
+    torch.manual_seed(0)
+    x = (torch.rand(3000) < 0.6).float().to(device)
+
+    def model():
+        theta = mi.sample("theta", Beta(2, 2))
+        mi.sample("x", Bernoulli(theta), sample_shape=[3000])
+
+    grads = []
+    for explicit in (False, True):
+        guide_mod = mi.nn.ParameterizedDistribution(Beta, concentration0=2.0,
+                                                    concentration1=3.0).to(device)
+        loss = mi.nn.EvidenceLowerBoundLoss(num_particles=64, seed=3)(
+            mi.condition(model, x=x), {"theta": guide_mod()})
+        assert repr(loss).startswith("tensor(") and type(loss + 1) is torch.Tensor
+        if explicit:
+            torch.autograd.backward(loss, torch.ones((), device=device))
+        else:
+            loss.backward()
+        grads.append([p.grad.clone() for p in guide_mod.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+    module = mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(1000),
+                                             scale=torch.rand(1000) + 0.5).to(device)
+    scale = module().scale
+    u = module.distribution_parameters["scale"]
+    torch.testing.assert_close(scale, torch.exp(u.detach()), rtol=2e-7, atol=0)
+    scale.sum().backward()
+    torch.testing.assert_close(u.grad, torch.exp(u.detach()), rtol=2e-7, atol=0)
