@@ -418,6 +418,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         torch.cuda.synchronize()
         profiler.disable()
         pstats.Stats(profiler, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+        pstats.Stats(profiler, stream=sys.stderr).sort_stats("cumulative").print_stats(45)
 
     ms = 1e3 * elapsed / steps
     value = w["evals"] * world * steps / elapsed

@@ -149,15 +149,16 @@ class Minibatch(torch.Tensor):
                         lookup(out) is not None:
                     out = out.as_subclass(Minibatch)
                 return out
-            for x in _flatten(args, kwargs):
+            stack = [args, kwargs]
+            while stack:   # the call's tensors (lists, tuples and dicts walked)
+                x = stack.pop()
                 if isinstance(x, Minibatch):
                     ensure_filled(x)
+                elif isinstance(x, (list, tuple)):
+                    stack.extend(x)
+                elif isinstance(x, dict):
+                    stack.extend(x.values())
             return func(*args, **kwargs)
-
-
-def _flatten(args, kwargs):
-    from torch.utils._pytree import tree_flatten
-    return tree_flatten((args, kwargs))[0]
 
 
 class DeviceDataLoader:

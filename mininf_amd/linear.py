@@ -24,6 +24,7 @@ import torch
 from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_map
 
+from . import guide as _guide
 from .guide import lazy_of
 
 _functorch = torch._C._functorch
@@ -52,6 +53,20 @@ class NeedsDraws(Exception):
     in an operation other than a site parameter / value: the loss then re-traces with real draws.
     """
 
+
+
+def _leaves(args, kwargs):
+    """The tensors of a torch function call's arguments (lists, tuples and dicts walked; the
+    pytree machinery costs tens of microseconds per call on this path)."""
+    stack = [args, kwargs]
+    while stack:
+        x = stack.pop()
+        if isinstance(x, torch.Tensor):
+            yield x
+        elif isinstance(x, (list, tuple)):
+            stack.extend(x)
+        elif isinstance(x, dict):
+            stack.extend(x.values())
 
 @dataclasses.dataclass
 class Deferred:
@@ -146,17 +161,16 @@ class DeferredMatmul(TorchFunctionMode):
             X, theta = args
             info = Deferred(X=X, theta=theta, shape=torch.Size([X.shape[0]]))
             return self._placeholder(theta, info.shape, info)
+        if not self.deferred and not _guide._LAZY:
+            return func(*args, **kwargs)   # no placeholder exists: nothing to look for
         touched = []
         lazy = []
-
-        def scan(x):
+        for x in _leaves(args, kwargs):
             info = self.lookup(x)
             if info is not None:
                 touched.append(info)
             elif lazy_of(x) is not None:
                 lazy.append(x)
-            return x
-        tree_map(scan, (args, kwargs))
         if not touched and not lazy:
             return func(*args, **kwargs)
         if func in _METADATA:
