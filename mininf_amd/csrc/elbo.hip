@@ -241,23 +241,41 @@ MI_DEV void partial_lane_elements(const mi_factor& F, int64_t base, int ti, int6
   constexpr int kE = 4;
   double g[kE][2];
   bool ok[kE];
+  int64_t ic[kE];
+  double s0[kE], s1[kE];
+  float pm[kE][2];
 #pragma unroll
   for (int e = 0; e < kE; ++e) {
     const int64_t i = base + (int64_t)e * ti;
     ok[e] = i < F.n;
-    const int64_t ic = ok[e] ? i : 0;
-    double s0 = 0.0, s1 = 0.0;
-    for (int64_t r = 0; r < rows; ++r) {
-      s0 += (double)F.partial[0][r * F.n + ic];
-      s1 += (double)F.partial[1][r * F.n + ic];
+    ic[e] = ok[e] ? i : 0;
+    s0[e] = s1[e] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pm[e][j] = F.param[j] != nullptr ? F.param[j][ic[e] * F.stride[j]] : 1.0f;
+  }
+  // rows outermost: each row's eight loads (four elements, two sums) issue together
+  for (int64_t r = 0; r < rows; ++r) {
+    float a0[kE], a1[kE];
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      a0[e] = F.partial[0][r * F.n + ic[e]];
+      a1[e] = F.partial[1][r * F.n + ic[e]];
     }
+#pragma unroll
+    for (int e = 0; e < kE; ++e) {
+      s0[e] += (double)a0[e];
+      s1[e] += (double)a1[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < kE; ++e) {
     double d0, d1;
-    entropy_grad(F, ic, d0, d1);
-    g[e][0] = (double)u * s0 + w * d0;
-    g[e][1] = (double)u * s1 + w * d1;
+    entropy_grad(F, ic[e], d0, d1);
+    g[e][0] = (double)u * s0[e] + w * d0;
+    g[e][1] = (double)u * s1[e] + w * d1;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      if (F.transform[j] == MI_TRANSFORM_EXP) g[e][j] *= (double)F.param[j][ic * F.stride[j]];
+      if (F.transform[j] == MI_TRANSFORM_EXP) g[e][j] *= (double)pm[e][j];
   }
 #pragma unroll
   for (int e = 0; e < kE; ++e) {
