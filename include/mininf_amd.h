@@ -293,6 +293,16 @@ int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t
                     const uint64_t* step_device, uint32_t stream_id,
                     int64_t particle_offset, const float* x_in, float* x, void* stream);
 
+/* mi_beta_rsample for a guide whose concentrations are exp of unconstrained parameters
+ * (ParameterizedDistribution.forward, nn.py:86-96 -> transform_to(positive), and Beta.__init__'s
+ * stack, beta.py:36-40): every draw computes its concentrations from u1 / u0 (expf, as
+ * mi_transform_params) and the k = 0 draws also write them, interleaved, to conc[N, 2] -- the
+ * transform and the draw in one launch. */
+int mi_beta_rsample_exp(const float* u1, int64_t u1_stride, const float* u0, int64_t u0_stride,
+                        float* conc, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                        const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                        const float* x_in, float* x, void* stream);
+
 /* Implicit reparameterisation gradient of the Beta draws (dirichlet.py:17-20 ->
  * torch._dirichlet_grad, ATen/native/Distributions.h dirichlet_grad_one), reduced over particles:
  *   dc1[i * dc1_stride] = sum_k dx[k,i] * dgrad(x, c1, c1+c0) * (1 - x)

@@ -206,13 +206,23 @@ MI_DEV float sample_gamma(float alpha, Stream& rng) {
   return boost * d;  // not reached in practice (acceptance > 95 % per attempt)
 }
 
+// EXP: c1 / c0 hold the unconstrained parameters; the concentrations are expf of them (as
+// k_transform_params) and the k = 0 threads write them to conc[i, 0..1].
+template <bool EXP>
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
     const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
     int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
-    uint32_t stream_id, int64_t poff, const float* __restrict__ x_in, float* __restrict__ x) {
+    uint32_t stream_id, int64_t poff, const float* __restrict__ x_in, float* __restrict__ x,
+    float* __restrict__ conc) {
   const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   if (t >= K * N) return;
   const int64_t k = t / N, i = t - k * N;
+  const float a = EXP ? expf(c1[i * c1_s]) : c1[i * c1_s];
+  const float b = EXP ? expf(c0[i * c0_s]) : c0[i * c0_s];
+  if (EXP && k == 0) {
+    conc[2 * i] = a;
+    conc[2 * i + 1] = b;
+  }
   if (x_in != nullptr) {
     x[t] = x_in[t];
     return;
@@ -220,10 +230,10 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
   if (step_dev != nullptr) step += *step_dev;
   Stream ra{seed, step, stream_id, 0u, (uint64_t)i, (uint64_t)(poff + k)};
   Stream rb{seed, step, stream_id, 1u, (uint64_t)i, (uint64_t)(poff + k)};
-  const float g1 = sample_gamma(c1[i * c1_s], ra);
-  const float g0 = sample_gamma(c0[i * c0_s], rb);
+  const float g1 = sample_gamma(a, ra);
+  const float g0 = sample_gamma(b, rb);
   const float s = g1 + g0;
-  x[t] = s > 0.0f ? g1 / s : (c1[i * c1_s] >= c0[i * c0_s] ? 1.0f : 0.0f);
+  x[t] = s > 0.0f ? g1 / s : (a >= b ? 1.0f : 0.0f);
 }
 
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
@@ -505,10 +515,24 @@ int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t
                     const float* x_in, float* x, void* stream) {
   if (c1 == nullptr || c0 == nullptr || x == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
     return MI_EINVAL;
-  hipLaunchKernelGGL(mi::k_beta_rsample, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+  hipLaunchKernelGGL(mi::k_beta_rsample<false>, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), c1, c1_stride,
                      c0, c0_stride, K, N, seed, step, step_device, stream_id, particle_offset, x_in,
-                     x);
+                     x, nullptr);
+  return to_code(hipGetLastError());
+}
+
+int mi_beta_rsample_exp(const float* u1, int64_t u1_stride, const float* u0, int64_t u0_stride,
+                        float* conc, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                        const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                        const float* x_in, float* x, void* stream) {
+  if (u1 == nullptr || u0 == nullptr || conc == nullptr || x == nullptr || K < 1 || N < 1 ||
+      stream_id > 0xFFFFFFu)
+    return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_beta_rsample<true>, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), u1, u1_stride,
+                     u0, u0_stride, K, N, seed, step, step_device, stream_id, particle_offset, x_in,
+                     x, conc);
   return to_code(hipGetLastError());
 }
 

@@ -128,6 +128,109 @@ def beta_concentration(distribution: Beta, N: int) -> torch.Tensor:
     return conc if conc.is_contiguous() else conc.contiguous()
 
 
+# ---- deferred exp transforms of Beta guides ---------------------------------------------------
+# ParameterizedDistribution.forward of a Beta guide returns its [.., 2] concentration array
+# before anything reads it; the guide's draw (mi_beta_rsample_exp) then computes exp(u) and
+# writes the array itself, so the transform needs no launch of its own. Any other reader (torch
+# argument validation, .mean, a user's own use) launches the transform first (mi_transform_params).
+
+@dataclasses.dataclass(eq=False)
+class _PendingExp:
+    out: "weakref.ReferenceType"
+    u1: torch.Tensor
+    u0: torch.Tensor
+    params: object          # the mi_params of the transform launch
+    filled: bool = False
+
+
+_PENDING_EXP: Dict[int, _PendingExp] = {}
+
+
+def _storage_of(tensor) -> Optional[int]:
+    if not isinstance(tensor, torch.Tensor):
+        return None
+    try:
+        return tensor.untyped_storage().data_ptr()
+    except (RuntimeError, NotImplementedError):
+        return None
+
+
+def pending_exp(tensor) -> Optional[_PendingExp]:
+    """The pending transform a concentration array (or a view of it) waits for, or None."""
+    if not _PENDING_EXP:
+        return None
+    rec = _PENDING_EXP.get(_storage_of(tensor))
+    if rec is None or rec.filled or rec.out() is None:
+        return None
+    return rec
+
+
+def fill_exp(tensor) -> None:
+    """Launch a pending transform (mi_transform_params) before its array is read."""
+    rec = pending_exp(tensor)
+    if rec is None:
+        return
+    out = rec.out()
+    nat.check(nat.lib().mi_transform_params(ctypes.byref(rec.params), out.data_ptr(),
+                                            nat.stream_handle(out.device)), "mi_transform_params")
+    rec.filled = True
+
+
+def _forget_exp(ptr: int, rec: _PendingExp) -> None:
+    if _PENDING_EXP.get(ptr) is rec:
+        del _PENDING_EXP[ptr]
+
+
+def defer_exp(out: torch.Tensor, u1: torch.Tensor, u0: torch.Tensor, params) -> torch.Tensor:
+    """Register `out` (a PendingConcentration) as the pending exp-stack of (u1, u0). The record
+    lives as long as `out` does; views of it keep `out` alive."""
+    import weakref
+    ptr = _storage_of(out)
+    rec = _PendingExp(weakref.ref(out), u1, u0, params)
+    _PENDING_EXP[ptr] = rec
+    weakref.finalize(out, _forget_exp, ptr, rec)
+    return out
+
+
+_PENDING_METADATA = {
+    torch.Tensor.size, torch.Tensor.dim, torch.Tensor.ndimension, torch.Tensor.numel,
+    torch.Tensor.__len__, torch.Tensor.is_floating_point, torch.Tensor.stride,
+    torch.Tensor.element_size, torch.Tensor.data_ptr, torch.Tensor.untyped_storage,
+    torch.Tensor.storage_offset, torch.Tensor.is_contiguous, torch.Tensor.shape.__get__,
+    torch.Tensor.dtype.__get__, torch.Tensor.device.__get__, torch.Tensor.ndim.__get__,
+    torch.Tensor.requires_grad.__get__, torch.Tensor.is_cuda.__get__, torch.Tensor.layout.__get__,
+    torch.Tensor.grad_fn.__get__, torch.Tensor.is_leaf.__get__, torch.Tensor.__hash__,
+    torch.Tensor._version.__get__, torch.Tensor.reshape, torch.Tensor.view,
+}
+
+
+class PendingConcentration(torch.Tensor):
+    """A Beta guide's concentration array whose exp transform has not run yet (see above): shape
+    queries, reshapes and pointer reads pass through; anything else launches the transform first."""
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        copies = func is torch.Tensor.reshape and args and isinstance(args[0], torch.Tensor) and \
+            not args[0].is_contiguous()   # a reshape that copies reads the values
+        if func not in _PENDING_METADATA or copies:
+            stack = [args, kwargs]
+            while stack:
+                x = stack.pop()
+                if isinstance(x, PendingConcentration):
+                    fill_exp(x)
+                elif isinstance(x, (list, tuple)):
+                    stack.extend(x)
+                elif isinstance(x, dict):
+                    stack.extend(x.values())
+        with torch._C.DisableTorchFunctionSubclass():
+            out = func(*args, **kwargs)
+        if func in (torch.Tensor.reshape, torch.Tensor.view) and isinstance(out, torch.Tensor) \
+                and pending_exp(out) is not None:
+            out = out.as_subclass(PendingConcentration)
+            out._pending_root = args[0]   # keeps the pending record's tensor alive
+        return out
+
+
 class _BetaRsampleFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg: DrawConfig, conc: torch.Tensor):  # type: ignore[override]
@@ -136,10 +239,20 @@ class _BetaRsampleFn(torch.autograd.Function):
         x = torch.empty((K, N), dtype=torch.float32, device=conc.device)
         seed, step = _philox_key(cfg)
         base = conc.data_ptr()
-        nat.check(nat.lib().mi_beta_rsample(
-            base, 2, base + 4, 2, K, N, seed, step, nat.ptr(cfg.step_device), cfg.stream_id,
-            cfg.particle_offset, nat.ptr(cfg.noise), x.data_ptr(), nat.stream_handle(conc.device)),
-            "mi_beta_rsample")
+        pending = pending_exp(conc)
+        if pending is not None:   # the guide's exp transform and the draw in one launch
+            u1, u0 = pending.u1.reshape(-1), pending.u0.reshape(-1)
+            nat.check(nat.lib().mi_beta_rsample_exp(
+                u1.data_ptr(), u1.stride(0) if u1.numel() > 1 else 0, u0.data_ptr(),
+                u0.stride(0) if u0.numel() > 1 else 0, base, K, N, seed, step,
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
+                x.data_ptr(), nat.stream_handle(conc.device)), "mi_beta_rsample_exp")
+            pending.filled = True
+        else:
+            nat.check(nat.lib().mi_beta_rsample(
+                base, 2, base + 4, 2, K, N, seed, step, nat.ptr(cfg.step_device), cfg.stream_id,
+                cfg.particle_offset, nat.ptr(cfg.noise), x.data_ptr(),
+                nat.stream_handle(conc.device)), "mi_beta_rsample")
         ctx.save_for_backward(x, conc)
         ctx.K, ctx.N = K, N
         return x

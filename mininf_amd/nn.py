@@ -15,6 +15,7 @@ estimates. The returned loss is a 0-d float32 tensor with ``grad_fn``.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Callable, cast, Dict, Optional, Set, Type
 
 import torch
@@ -152,6 +153,10 @@ class ParameterizedDistribution(nn.Module):
         return beta
 
 
+def _defer_beta_exp() -> bool:
+    return os.environ.get("MININF_AMD_DEFER_BETA_EXP", "1") != "0"
+
+
 class _ExpFn(torch.autograd.Function):
     """``exp(u)`` of a positive-constrained guide parameter (``transform_to(positive)``,
     nn.py:91-96) as one ``mi_transform_params`` launch."""
@@ -189,10 +194,14 @@ class _ExpStackFn(torch.autograd.Function):
             P.u[j] = flat.data_ptr()
             P.stride[j] = flat.stride(0) if u.numel() > 1 else 0
             P.transform[j] = _native.TRANSFORM_EXP
+        ctx.save_for_backward(out)
+        if _defer_beta_exp():
+            # the guide's draw computes and writes the array (mi_beta_rsample_exp); any earlier
+            # reader launches the transform itself (guide.PendingConcentration)
+            return guide.defer_exp(out.as_subclass(guide.PendingConcentration), u1, u0, P)
         _native.check(_native.lib().mi_transform_params(ctypes.byref(P), out.data_ptr(),
                                                         _native.stream_handle(u1.device)),
                       "mi_transform_params")
-        ctx.save_for_backward(out)
         return out
 
     @staticmethod

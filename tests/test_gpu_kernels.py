@@ -871,3 +871,45 @@ def test_elbo_loss_tensor_and_guide_exp(device):
     torch.testing.assert_close(scale, torch.exp(u.detach()), rtol=2e-7, atol=0)
     scale.sum().backward()
     torch.testing.assert_close(u.grad, torch.exp(u.detach()), rtol=2e-7, atol=0)
+
+
+def test_beta_guide_transform_fused_into_draw(device, monkeypatch):
+    """
+    A Beta guide's exp transform runs inside its draw (mi_beta_rsample_exp) unless something reads
+    the concentrations first: the ELBO, gradients and the written concentrations equal the
+    separate-launch path bit for bit, and a reader without a draw (no_grad, .mean) sees the values.
+    """
+    from torch.distributions import Bernoulli, Beta
+    x = (torch.rand(2000, generator=torch.Generator().manual_seed(2)) < 0.3).float().to(device)
+
+    def model():
+        theta = mi.sample("theta", Beta(2, 2))
+        mi.sample("x", Bernoulli(theta), sample_shape=[2000])
+
+    # torch's own argument validation reads the concentrations (and so runs the transform); the
+    # captured steps run without it, as here
+    monkeypatch.setattr(torch.distributions.Distribution, "_validate_args", False)
+    results = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("MININF_AMD_DEFER_BETA_EXP", defer)
+        module = mi.nn.ParameterizedDistribution(Beta, concentration0=2.5,
+                                                 concentration1=1.5).to(device)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=128, seed=5, validate=False)
+        guide_dist = module()
+        pending = guide.pending_exp(guide_dist._dirichlet.concentration) is not None
+        assert pending == (defer == "1")
+        loss = loss_fn(mi.condition(model, x=x), {"theta": guide_dist})
+        loss.backward()
+        assert guide.pending_exp(guide_dist._dirichlet.concentration) is None
+        results.append((float(loss), [p.grad.clone() for p in module.parameters()],
+                        guide_dist._dirichlet.concentration.detach().clone()))
+    (l0, g0, c0), (l1, g1, c1) = results
+    assert l0 == l1
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert torch.equal(c0, c1)
+    monkeypatch.setenv("MININF_AMD_DEFER_BETA_EXP", "1")
+    module = mi.nn.ParameterizedDistribution(Beta, concentration0=2.5,
+                                             concentration1=1.5).to(device)
+    with torch.no_grad():
+        d = module()
+    torch.testing.assert_close(d.mean.cpu(), torch.tensor(1.5 / 4.0), rtol=1e-6, atol=0)
