@@ -442,14 +442,18 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       val[16 * PT] = (float)lpd;
     }
   }
+  // a constant sigma: one division for all rows (sixteen fp64 divisions are a long serial tail of
+  // a short launch)
+  const double w_const = (FAMILY == MI_NORMAL && grads && !per_particle_sigma)
+                             ? (double)wscale / ((double)L.scale_constant * (double)L.scale_constant)
+                             : (double)wscale;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t kk = k0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    double w = (double)wscale;
-    if (FAMILY == MI_NORMAL && grads && kk < K) {
-      const double sigma =
-          per_particle_sigma ? (double)L.scale[kk * L.scale_stride_k] : (double)L.scale_constant;
-      w /= sigma * sigma;
+    double w = w_const;
+    if (FAMILY == MI_NORMAL && grads && per_particle_sigma && kk < K) {
+      const double sigma = (double)L.scale[kk * L.scale_stride_k];
+      w = (double)wscale / (sigma * sigma);
     }
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
