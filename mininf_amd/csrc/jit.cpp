@@ -454,6 +454,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       if (is(op, kParticle))
         o << in << "float pn" << op << " = k_begin < k_end ? x" << op << "[k_begin * sk" << op
           << "] : 0.0f;\n";
+    // Two copies of the particle loop: a segment that is neither ragged nor past the end has
+    // every element valid, and its unmasked sites need no per-element select.
+    auto emit_k_loop = [&](const std::string& valid) {
     if (plan.unroll > 1) o << "#pragma unroll " << plan.unroll << "\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
@@ -486,7 +489,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     const std::string inner = std::string(in2) + "  ";
     for (int op = 0; op < g.num_operands; ++op)
       if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
-    for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, "ok[e]", inner.c_str());
+    for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, valid, inner.c_str());
     o << in2 << "}\n";
     for (int op = 0; op < g.num_operands; ++op) {
       if (!dense_grad(op)) continue;
@@ -499,6 +502,12 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * g" << op << "[e]; }\n";
     }
     emit_particle_sums(in2, plan.block_rows);
+    o << in << "}\n";
+    };
+    o << in << "if (" << (plan.block_rows ? "live && " : "") << "shift == 0) {\n";
+    emit_k_loop("true");
+    o << in << "} else {\n";
+    emit_k_loop("ok[e]");
     o << in << "}\n";
     if (dgrad)
       o << in << "#pragma unroll\n" << in << "for (int e = 0; e < " << E << "; ++e) if (ok[e]) {\n"
