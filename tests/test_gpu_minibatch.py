@@ -127,6 +127,38 @@ def test_captured_loop_draws_a_batch_per_replay(device):
     assert len(set(eager_losses)) == len(eager_losses)   # a new batch (and draw) every step
 
 
+def test_multi_step_replay_with_minibatches_and_hip_adam(device):
+    """StepGraph(repeat=4) over the minibatch loop with mininf_amd.optim.Adam: four batches,
+    draws and Adam steps per replay, the same losses and parameters as eager steps."""
+    model, X, y = regression(device, n=8192)
+
+    def setup():
+        loader = DeviceDataLoader(X, y, batch_size=1024, shuffle=True, drop_last=True, seed=4)
+        module = guide_module(device)
+        optimizer = mi.optim.Adam(module.parameters(), lr=0.01)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=32, seed=6)
+
+        def step():
+            optimizer.zero_grad(set_to_none=True)
+            Xb, yb = loader.next()
+            loss = loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": module()})
+            loss.backward()
+            optimizer.step()
+            return loss.detach()
+        return step, module
+
+    eager, eager_module = setup()
+    eager_losses = [float(eager()) for _ in range(2 + 4 * 3)]
+    body, graph_module = setup()
+    captured = StepGraph(body, warmup=2, repeat=4)
+    graph_losses = [float(captured()) for _ in range(3)]
+    captured.check()
+    torch.testing.assert_close(torch.tensor(graph_losses),
+                               torch.tensor(eager_losses[2 + 3::4]), rtol=1e-6, atol=0)
+    for a, b in zip(eager_module.parameters(), graph_module.parameters()):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-6, atol=0)
+
+
 def test_invalid_values_raise_reference_message(device):
     model, X, y = regression(device)
     y = y.clone()
