@@ -276,6 +276,15 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
                       const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
                       const float* eps, float* z, void* stream);
 
+/* mi_normal_rsample for a guide whose scale is exp of an unconstrained parameter u
+ * (ParameterizedDistribution.forward, nn.py:86-96 -> transform_to(positive)): the draws use
+ * expf(u[i * u_stride]) (as mi_transform_params) and the first particle block writes it to
+ * scale_out[i * u_stride] -- the transform and the draw in one launch. */
+int mi_normal_rsample_exp(const float* loc, int64_t loc_stride, const float* u, int64_t u_stride,
+                          float* scale_out, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                          const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                          const float* eps, float* z, void* stream);
+
 /* Backward of mi_normal_rsample: dloc[i] = sum_k dz[k,i], dscale[i] = sum_k dz[k,i] * eps[k,i]
  * with eps regenerated from the counter (or read from `eps`). */
 int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);

@@ -208,6 +208,9 @@ _SIGNATURES = {
     "mi_beta_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
                                        ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                        c_vp]),
+    "mi_normal_rsample_exp": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                             ctypes.c_uint64, ctypes.c_uint64, c_vp,
+                                             ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp]),
     "mi_beta_rsample_exp": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp, ctypes.c_uint32,
                                            c_i64, c_vp, c_vp, c_vp]),

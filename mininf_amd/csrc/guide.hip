@@ -20,11 +20,14 @@ constexpr int kGuideThreads = 256;
 // -------------------------------------------------------------------------------------------------
 // Normal
 // -------------------------------------------------------------------------------------------------
+// EXP: `scale` holds the unconstrained parameter; the scale is expf of it (as
+// k_transform_params) and the first row block writes it to scale_out (same strides).
+template <bool EXP>
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
     const float* __restrict__ loc, int64_t loc_s, const float* __restrict__ scale, int64_t scale_s,
     int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
     uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in, float* __restrict__ z,
-    int64_t rows_per_block) {
+    int64_t rows_per_block, float* __restrict__ scale_out) {
   if (step_dev != nullptr) step += *step_dev;
   const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   const int64_t i0 = quad * 4;
@@ -36,7 +39,8 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
   for (int j = 0; j < 4; ++j) {
     const int64_t i = min(i0 + j, N - 1);
     m[j] = loc[i * loc_s];
-    sd[j] = scale[i * scale_s];
+    sd[j] = EXP ? expf(scale[i * scale_s]) : scale[i * scale_s];
+    if (EXP && blockIdx.y == 0 && i0 + j < N) scale_out[(i0 + j) * scale_s] = sd[j];
   }
   const bool full = (i0 + 4 <= N) && ((N & 3) == 0);
   for (int64_t k = k0; k < k1; ++k) {
@@ -464,10 +468,27 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
   const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
   const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(K, ceil_div(2048, gx)));
   const int64_t rows = ceil_div(K, gy);
-  hipLaunchKernelGGL(mi::k_normal_rsample, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
+  hipLaunchKernelGGL(mi::k_normal_rsample<false>, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
                      scale, scale_stride, K, N, seed, step, step_device, stream_id, particle_offset,
-                     eps, z, rows);
+                     eps, z, rows, nullptr);
+  return to_code(hipGetLastError());
+}
+
+int mi_normal_rsample_exp(const float* loc, int64_t loc_stride, const float* u, int64_t u_stride,
+                          float* scale_out, int64_t K, int64_t N, uint64_t seed, uint64_t step,
+                          const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
+                          const float* eps, float* z, void* stream) {
+  if (loc == nullptr || u == nullptr || scale_out == nullptr || z == nullptr || K < 1 || N < 1 ||
+      stream_id > 0xFFFFFFu)
+    return MI_EINVAL;
+  const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
+  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(K, ceil_div(2048, gx)));
+  const int64_t rows = ceil_div(K, gy);
+  hipLaunchKernelGGL(mi::k_normal_rsample<true>, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
+                     dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
+                     u, u_stride, K, N, seed, step, step_device, stream_id, particle_offset, eps, z,
+                     rows, scale_out);
   return to_code(hipGetLastError());
 }
 

@@ -282,6 +282,7 @@ class _GroupLauncher:
                 dw.operand = index + 1
                 dw.stream_id = d.cfg.stream_id
                 dw.loc, dw.loc_stride = d.loc.data_ptr(), d.loc_s
+                guide.fill_exp(d.scale)   # a deferred exp transform runs before the kernel reads it
                 dw.scale, dw.scale_stride = d.scale.data_ptr(), d.scale_s
                 dw.seed, dw.step = guide._philox_key(d.cfg)
                 dw.step_device = nat.ptr(d.cfg.step_device)

@@ -78,11 +78,27 @@ class _NormalRsampleFn(torch.autograd.Function):
         z = torch.empty((K, N), dtype=torch.float32, device=loc.device)
         seed, step = _philox_key(cfg)
         eps = cfg.noise
-        nat.check(nat.lib().mi_normal_rsample(
-            loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step,
-            nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
-            z.data_ptr(), nat.stream_handle(loc.device)),
-            "mi_normal_rsample")
+        pending = pending_exp(scale)
+        out = pending.out() if pending is not None else None
+        if pending is not None and pending.u0 is None and out is not None and \
+                pending.u1.is_contiguous() and out.is_contiguous() and \
+                tuple(pending.u1.shape) == tuple(out.shape):
+            # the guide's exp transform and the draw in one launch: u has the layout of the
+            # (contiguous) transform output, so the scale view's element i is u's at the same
+            # offset and stride
+            u_ptr = pending.u1.data_ptr() + (scale.data_ptr() - out.data_ptr())
+            nat.check(nat.lib().mi_normal_rsample_exp(
+                loc.data_ptr(), loc_s, u_ptr, scale_s, scale.data_ptr(), K, N, seed, step,
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
+                z.data_ptr(), nat.stream_handle(loc.device)), "mi_normal_rsample_exp")
+            pending.filled = True
+        else:
+            fill_exp(scale)
+            nat.check(nat.lib().mi_normal_rsample(
+                loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step,
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
+                z.data_ptr(), nat.stream_handle(loc.device)),
+                "mi_normal_rsample")
         ctx.cfg = cfg
         ctx.N = N
         ctx.save_for_backward(scale)
@@ -138,7 +154,7 @@ def beta_concentration(distribution: Beta, N: int) -> torch.Tensor:
 class _PendingExp:
     out: "weakref.ReferenceType"
     u1: torch.Tensor
-    u0: torch.Tensor
+    u0: Optional[torch.Tensor]   # None: a single positive parameter (a Normal guide's scale)
     params: object          # the mi_params of the transform launch
     filled: bool = False
 
@@ -181,7 +197,8 @@ def _forget_exp(ptr: int, rec: _PendingExp) -> None:
         del _PENDING_EXP[ptr]
 
 
-def defer_exp(out: torch.Tensor, u1: torch.Tensor, u0: torch.Tensor, params) -> torch.Tensor:
+def defer_exp(out: torch.Tensor, u1: torch.Tensor, u0: Optional[torch.Tensor],
+              params) -> torch.Tensor:
     """Register `out` (a PendingConcentration) as the pending exp-stack of (u1, u0). The record
     lives as long as `out` does; views of it keep `out` alive."""
     import weakref
@@ -204,15 +221,22 @@ _PENDING_METADATA = {
 }
 
 
+# views (no value read): the results stay pending
+_PENDING_VIEWS = {torch.Tensor.reshape, torch.Tensor.view, torch.Tensor.expand,
+                  torch.Tensor.expand_as, torch.broadcast_to, torch.Tensor.broadcast_to,
+                  torch.broadcast_tensors, torch.functional.broadcast_tensors}
+
+
 class PendingConcentration(torch.Tensor):
-    """A Beta guide's concentration array whose exp transform has not run yet (see above): shape
-    queries, reshapes and pointer reads pass through; anything else launches the transform first."""
+    """A guide parameter array whose exp transform has not run yet (a Beta guide's concentrations,
+    a Normal guide's scale; see above): shape queries, views and pointer reads pass through;
+    anything else launches the transform first."""
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
         copies = func is torch.Tensor.reshape and args and isinstance(args[0], torch.Tensor) and \
             not args[0].is_contiguous()   # a reshape that copies reads the values
-        if func not in _PENDING_METADATA or copies:
+        if (func not in _PENDING_METADATA and func not in _PENDING_VIEWS) or copies:
             stack = [args, kwargs]
             while stack:
                 x = stack.pop()
@@ -224,11 +248,30 @@ class PendingConcentration(torch.Tensor):
                     stack.extend(x.values())
         with torch._C.DisableTorchFunctionSubclass():
             out = func(*args, **kwargs)
-        if func in (torch.Tensor.reshape, torch.Tensor.view) and isinstance(out, torch.Tensor) \
-                and pending_exp(out) is not None:
-            out = out.as_subclass(PendingConcentration)
-            out._pending_root = args[0]   # keeps the pending record's tensor alive
+        if func in _PENDING_VIEWS:
+            roots = [x for x in _flat_args(args) if isinstance(x, PendingConcentration)]
+
+            def rewrap(t):
+                if isinstance(t, torch.Tensor) and pending_exp(t) is not None:
+                    t = t.as_subclass(PendingConcentration)
+                    t._pending_root = roots   # keeps the pending records' tensors alive
+                return t
+            if isinstance(out, (tuple, list)):
+                out = type(out)(rewrap(t) for t in out)
+            else:
+                out = rewrap(out)
         return out
+
+
+def _flat_args(args):
+    stack, flat = [args], []
+    while stack:
+        x = stack.pop()
+        if isinstance(x, (list, tuple)):
+            stack.extend(x)
+        else:
+            flat.append(x)
+    return flat
 
 
 class _BetaRsampleFn(torch.autograd.Function):

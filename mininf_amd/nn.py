@@ -153,8 +153,9 @@ class ParameterizedDistribution(nn.Module):
         return beta
 
 
-def _defer_beta_exp() -> bool:
-    return os.environ.get("MININF_AMD_DEFER_BETA_EXP", "1") != "0"
+def _defer_exp() -> bool:
+    """Whether guide exp transforms are left to the draws that read them (MININF_AMD_DEFER_EXP)."""
+    return os.environ.get("MININF_AMD_DEFER_EXP", "1") != "0"
 
 
 class _ExpFn(torch.autograd.Function):
@@ -163,6 +164,7 @@ class _ExpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u: torch.Tensor):  # type: ignore[override]
         out = torch.empty(u.shape, dtype=torch.float32, device=u.device)
+        ctx.save_for_backward(out)
         if u.numel() > 0:
             flat = u.reshape(-1)
             P = _native.Params()
@@ -170,10 +172,13 @@ class _ExpFn(torch.autograd.Function):
             P.u[0] = flat.data_ptr()
             P.stride[0] = flat.stride(0) if flat.numel() > 1 else 0
             P.transform[0] = _native.TRANSFORM_EXP
+            if _defer_exp() and u.is_contiguous():
+                # the guide's draw computes and writes the scale (mi_normal_rsample_exp); any
+                # earlier reader launches the transform itself (guide.PendingConcentration)
+                return guide.defer_exp(out.as_subclass(guide.PendingConcentration), u, None, P)
             _native.check(_native.lib().mi_transform_params(ctypes.byref(P), out.data_ptr(),
                                                             _native.stream_handle(u.device)),
                           "mi_transform_params")
-        ctx.save_for_backward(out)
         return out
 
     @staticmethod
@@ -195,7 +200,7 @@ class _ExpStackFn(torch.autograd.Function):
             P.stride[j] = flat.stride(0) if u.numel() > 1 else 0
             P.transform[j] = _native.TRANSFORM_EXP
         ctx.save_for_backward(out)
-        if _defer_beta_exp():
+        if _defer_exp():
             # the guide's draw computes and writes the array (mi_beta_rsample_exp); any earlier
             # reader launches the transform itself (guide.PendingConcentration)
             return guide.defer_exp(out.as_subclass(guide.PendingConcentration), u1, u0, P)

@@ -891,7 +891,7 @@ def test_beta_guide_transform_fused_into_draw(device, monkeypatch):
     monkeypatch.setattr(torch.distributions.Distribution, "_validate_args", False)
     results = []
     for defer in ("0", "1"):
-        monkeypatch.setenv("MININF_AMD_DEFER_BETA_EXP", defer)
+        monkeypatch.setenv("MININF_AMD_DEFER_EXP", defer)
         module = mi.nn.ParameterizedDistribution(Beta, concentration0=2.5,
                                                  concentration1=1.5).to(device)
         loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=128, seed=5, validate=False)
@@ -907,7 +907,7 @@ def test_beta_guide_transform_fused_into_draw(device, monkeypatch):
     assert l0 == l1
     assert all(torch.equal(a, b) for a, b in zip(g0, g1))
     assert torch.equal(c0, c1)
-    monkeypatch.setenv("MININF_AMD_DEFER_BETA_EXP", "1")
+    monkeypatch.setenv("MININF_AMD_DEFER_EXP", "1")
     module = mi.nn.ParameterizedDistribution(Beta, concentration0=2.5,
                                              concentration1=1.5).to(device)
     with torch.no_grad():
@@ -942,3 +942,37 @@ def test_bcast_reducible_floor_matches_per_eval(device, monkeypatch):
     assert abs(l0 - l1) <= 1e-5 * abs(l0)
     for a, b in zip(g0, g1):
         assert (a - b).abs().max() <= 1e-5 * a.abs().max()
+
+
+def test_normal_guide_transform_fused_into_draw(device, monkeypatch):
+    """A Normal guide's scale = exp(u) is computed and written by its draw
+    (mi_normal_rsample_exp): the ELBO, gradients and scale equal the separate-launch path bit for
+    bit, for a vector factor (a small materialised draw) and a scalar one (a broadcast scale)."""
+    gen = torch.Generator().manual_seed(4)
+    X = torch.randn(3000, 8, generator=gen).to(device)
+    y = (X @ torch.randn(8, generator=gen).to(device)) + 0.3
+
+    def model():
+        mu = mi.sample("mu", Normal(0.0, 1.0))
+        theta = mi.sample("theta", Normal(mu, 1.0), sample_shape=[8])
+        mi.sample("y", Normal(X @ theta, 1.0))
+
+    monkeypatch.setattr(torch.distributions.Distribution, "_validate_args", False)
+    results = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("MININF_AMD_DEFER_EXP", defer)
+        guide_mod = mi.nn.ParameterizedFactorizedDistribution(
+            mu=mi.nn.ParameterizedDistribution(Normal, loc=0.1, scale=0.7),
+            theta=mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(8),
+                                                  scale=torch.full((8,), 0.5))).to(device)
+        approx = guide_mod()
+        assert (guide.pending_exp(approx["theta"].scale) is not None) == (defer == "1")
+        loss = mi.nn.EvidenceLowerBoundLoss(num_particles=64, seed=2, validate=False)(
+            mi.condition(model, y=y), approx)
+        loss.backward()
+        results.append((float(loss), [p.grad.clone() for p in guide_mod.parameters()],
+                        approx["theta"].scale.detach().clone(), approx["mu"].scale.detach().clone()))
+    (l0, g0, s0, m0), (l1, g1, s1, m1) = results
+    assert l0 == l1
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
