@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 6
+#define MI_ABI_VERSION 7
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -120,6 +120,11 @@ typedef struct mi_draw {
   int64_t particle_offset;
   float* dloc;              /* [N] outputs (compute_grads) */
   float* dscale;
+  /* scale_exp non-NULL: the scale is expf(scale_exp[i * scale_stride]) (a guide's
+   * transform_to(positive), nn.py:86-96, as mi_transform_params) and the first particle block
+   * writes it to `scale` -- the transform inside the draw's kernel */
+  const float* scale_exp;
+  int64_t pad0;
 } mi_draw;
 
 /* Independent work carried by extra workgroups of a group's launch (see mi_group_side_supported):

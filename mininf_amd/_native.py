@@ -37,7 +37,7 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 6   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 7   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -68,6 +68,7 @@ class Draw(ctypes.Structure):
         ("loc", c_vp), ("loc_stride", c_i64), ("scale", c_vp), ("scale_stride", c_i64),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
         ("particle_offset", c_i64), ("dloc", c_vp), ("dscale", c_vp),
+        ("scale_exp", c_vp), ("pad0", c_i64),
     ]
 
 

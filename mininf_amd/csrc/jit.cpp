@@ -117,7 +117,8 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
   }
   s << "|" << g.num_slots << "|" << g.compute_grads
     << (plan.row && g.N < 64L * plan.elems ? "|small" : "") << "|draw" << g.draw.operand
-    << (g.draw.loc_stride == 0 ? "b" : "") << (g.draw.scale_stride == 0 ? "b" : "");
+    << (g.draw.loc_stride == 0 ? "b" : "") << (g.draw.scale_stride == 0 ? "b" : "")
+    << (g.draw.scale_exp != nullptr ? "x" : "");
   return Signature{s.str()};
 }
 
@@ -444,8 +445,12 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << "; ++e) m" << st << "[e] = r[(e >> 2) * 256 + (e & 3)] != 0; }\n";
     o << in << "float dwl[" << E << "], dws[" << E << "];\n#pragma unroll\n" << in
       << "for (int e = 0; e < " << E << "; ++e) { const long i = base + " << elem("e")
-      << "; dwl[e] = G.draw.loc[i * G.draw.loc_stride]; dws[e] = G.draw.scale[i * "
-         "G.draw.scale_stride]; }\n";
+      << "; dwl[e] = G.draw.loc[i * G.draw.loc_stride]; ";
+    if (g.draw.scale_exp != nullptr)   // the guide's exp transform here; block row 0 writes it
+      o << "dws[e] = expf(G.draw.scale_exp[i * G.draw.scale_stride]); if (blockIdx.y == 0 && ok[e]) "
+           "const_cast<float*>(G.draw.scale)[i * G.draw.scale_stride] = dws[e]; }\n";
+    else
+      o << "dws[e] = G.draw.scale[i * G.draw.scale_stride]; }\n";
     const bool dgrad = g.compute_grads != 0;
     if (dgrad)
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in

@@ -170,6 +170,7 @@ class _GroupLauncher:
         # the fused draw's dloc / dscale partials stay in the workspace for the ELBO backward
         # (MI_GROUP_DRAW_PARTIALS); set by the ELBO plan when it absorbs the draw
         self.draw_partials = False
+        self.exp_pending = None
         self.workspace: Optional[torch.Tensor] = None   # of the last run
         # Beta implicit-gradient factors carried as extra workgroups of this launch (mi_side):
         # (draws x [K, N], concentration [N, 2]) set by the ELBO plan; side_out is the [K, N, 2]
@@ -253,10 +254,12 @@ class _GroupLauncher:
                 return False
         return True
 
-    def describe(self, compute_grads: bool):
+    def describe(self, compute_grads: bool, fuse_exp: bool = False):
         """
         The ctypes ``mi_group`` descriptor of this group plus freshly allocated dense gradient
-        buffers (one per DENSE operand, None otherwise).
+        buffers (one per DENSE operand, None otherwise). ``fuse_exp``: a fused draw whose guide
+        scale still waits for its exp transform reads the unconstrained parameter instead
+        (``mi_draw.scale_exp``); otherwise the transform is launched first.
         """
         device = self.device
         K, N = self.K, self.N
@@ -282,8 +285,14 @@ class _GroupLauncher:
                 dw.operand = index + 1
                 dw.stream_id = d.cfg.stream_id
                 dw.loc, dw.loc_stride = d.loc.data_ptr(), d.loc_s
-                guide.fill_exp(d.scale)   # a deferred exp transform runs before the kernel reads it
                 dw.scale, dw.scale_stride = d.scale.data_ptr(), d.scale_s
+                source = guide.exp_source(d.scale) if fuse_exp else None
+                if source is not None:
+                    # the guide's deferred exp transform runs inside the site program, which
+                    # writes the scale for the autograd of the transform (run() marks it filled)
+                    self.exp_pending, dw.scale_exp = source
+                else:
+                    guide.fill_exp(d.scale)   # a deferred transform runs before the kernel reads it
                 dw.seed, dw.step = guide._philox_key(d.cfg)
                 dw.step_device = nat.ptr(d.cfg.step_device)
                 dw.particle_offset = d.cfg.particle_offset
@@ -360,7 +369,8 @@ class _GroupLauncher:
         """
         device = self.device
         K, N = self.K, self.N
-        group, grads = self.describe(compute_grads)
+        self.exp_pending = None
+        group, grads = self.describe(compute_grads, fuse_exp=True)
         size = ctypes.c_size_t()
         lib = nat.lib()
         nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
@@ -402,6 +412,9 @@ class _GroupLauncher:
             None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
             nat.stream_handle(device), ctypes.byref(reduce) if defer else None),
             "mi_group_forward_deferred")
+        if self.exp_pending is not None:
+            self.exp_pending.filled = True
+            self.exp_pending = None
         self.reduce = reduce if defer and reduce.part else None
         self.workspace = workspace
         self.partials = None

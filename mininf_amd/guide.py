@@ -78,15 +78,10 @@ class _NormalRsampleFn(torch.autograd.Function):
         z = torch.empty((K, N), dtype=torch.float32, device=loc.device)
         seed, step = _philox_key(cfg)
         eps = cfg.noise
-        pending = pending_exp(scale)
-        out = pending.out() if pending is not None else None
-        if pending is not None and pending.u0 is None and out is not None and \
-                pending.u1.is_contiguous() and out.is_contiguous() and \
-                tuple(pending.u1.shape) == tuple(out.shape):
-            # the guide's exp transform and the draw in one launch: u has the layout of the
-            # (contiguous) transform output, so the scale view's element i is u's at the same
-            # offset and stride
-            u_ptr = pending.u1.data_ptr() + (scale.data_ptr() - out.data_ptr())
+        source = exp_source(scale)
+        if source is not None:
+            # the guide's exp transform and the draw in one launch
+            pending, u_ptr = source
             nat.check(nat.lib().mi_normal_rsample_exp(
                 loc.data_ptr(), loc_s, u_ptr, scale_s, scale.data_ptr(), K, N, seed, step,
                 nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
@@ -179,6 +174,22 @@ def pending_exp(tensor) -> Optional[_PendingExp]:
     if rec is None or rec.filled or rec.out() is None:
         return None
     return rec
+
+
+def exp_source(scale) -> Optional[Tuple[_PendingExp, int]]:
+    """
+    For a Normal guide scale still waiting for its exp transform: the record and the address of
+    the unconstrained parameter element that becomes ``scale``'s first element, so a kernel can
+    read exp(u) at ``scale``'s own offset and strides and write it (mi_normal_rsample_exp,
+    mi_draw.scale_exp). None when nothing is pending or the layouts differ.
+    """
+    rec = pending_exp(scale)
+    out = rec.out() if rec is not None else None
+    if out is None or rec.u0 is not None or not rec.u1.is_contiguous() or \
+            not out.is_contiguous() or tuple(rec.u1.shape) != tuple(out.shape):
+        return None
+    # u has the layout of the (contiguous) transform output: same offset, same strides
+    return rec, rec.u1.data_ptr() + (scale.data_ptr() - out.data_ptr())
 
 
 def fill_exp(tensor) -> None:
