@@ -426,8 +426,6 @@ constexpr int kGroupCounterStride = 16;   // words between group counters (64 by
 // sum_k g_sk dgrad[k] to its own partial, and the last block adds the partials in a fixed order.
 constexpr int kMaxTails = 2;
 
-constexpr int kValues = 4;   // values of a reduce job read together (reduce_job)
-
 struct ReducePlan {
   int external;                   // 1: the reductions ran as their own launches; add their totals
   int num;
@@ -498,41 +496,12 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
   const int64_t kc = k < K ? k : K - 1;
   double* lds = &red[0][0];   // [kRedG][kRedK] doubles
   double t = 0.0;
-  // Up to four values of a multi-value job are read together (kValues accumulators), so a lane
-  // has four values' loads in flight instead of one value's: a long list (a fused draw's block
-  // rows, ~1000 segments) costs a few rounds of memory latency rather than one per value.
-  const bool together = !J.rank1 && v1 - v0 > 1 && v1 - v0 <= kValues;
-  double accv[kValues] = {};
-  if (together) {
-    const float* __restrict__ p = J.part + kc;
-    const int64_t vs = J.nseg * K;
-    const int nvv = v1 - v0;
-    // rounds of eight segments per value, the last one predicated (no serial remainder loop)
-    for (int64_t g = gl; g < J.nseg; g += 8 * kRedG) {
-      float x[kValues][8];
-#pragma unroll
-      for (int q = 0; q < kValues; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          x[q][j] = q < nvv && g + j * kRedG < J.nseg
-                        ? p[(int64_t)(v0 + q) * vs + (g + j * kRedG) * K] : 0.0f;
-#pragma unroll
-      for (int q = 0; q < kValues; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) accv[q] += (double)x[q][j];
-    }
-  }
   for (int v = v0; v < v1; ++v) {
     // rank-one values (mi_reduce.rank1): the particle-independent u[seg], then f[k] u + e[k]
     const bool r1 = (J.rank1 >> v) & 1;
-    double acc = 0.0;
-    if (together) {
-#pragma unroll
-      for (int q = 0; q < kValues; ++q)
-        if (q == v - v0) acc = accv[q];
-    } else {
     const float* __restrict__ p = J.part + (int64_t)v * J.nseg * K + (r1 ? 0 : kc);
     const int64_t stride = r1 ? 1 : K;
+    double acc = 0.0;
     int64_t g = gl;
     // sixteen loads in flight per lane (a C2-sized list, ~250 segments over 8 groups, is two
     // rounds of memory latency instead of four)
@@ -543,15 +512,15 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc += (double)x[j];
     }
-    // the rest in one predicated round (a serial remainder loop is a memory round trip per load)
-    for (; g < J.nseg; g += 8 * kRedG) {
+    if (g + 7 * kRedG < J.nseg) {
       float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = g + j * kRedG < J.nseg ? p[(g + j * kRedG) * stride] : 0.0f;
+      for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * stride];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += (double)x[j];
+      g += 8 * kRedG;
     }
-    }
+    for (; g < J.nseg; g += kRedG) acc += (double)p[g * stride];
     __syncthreads();
     lds[gl * kRedK + kl] = acc;
     __syncthreads();
@@ -663,16 +632,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
           // 16-byte loads, all issued before the logs
           const int64_t nq = F.n >> 2;
           const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
-          int64_t q = first;
-          for (; q + 3 * stride < nq; q += 4 * stride) {   // four quads in flight
-            float4 v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = sq[q + j * stride];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              hf += (logf(v[j].x) + logf(v[j].y)) + (logf(v[j].z) + logf(v[j].w));
-          }
-          for (; q < nq; q += stride) {
+          for (int64_t q = first; q < nq; q += stride) {
             const float4 v = sq[q];
             hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
           }
@@ -981,24 +941,9 @@ int env_kred() {
   return v;
 }
 
-// particles per reducing block for very long lists (MININF_AMD_ELBO_KRED_LONG: 4, 8 or 16)
-int env_kred_long() {
-  static const int v = [] {
-    const char* e = getenv("MININF_AMD_ELBO_KRED_LONG");
-    const int n = e != nullptr ? atoi(e) : 16;
-    return (n == 4 || n == 8 || n == 16) ? n : 16;
-  }();
-  return v;
-}
-
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
-  static const int lead_max = [] {   // MININF_AMD_ELBO_LEAD: cap on the forward's lead blocks
-    const char* v = getenv("MININF_AMD_ELBO_LEAD");
-    const int n = v != nullptr ? atoi(v) : mi::kElboMaxBlocks;
-    return std::min(std::max(n, 64), mi::kElboMaxBlocks);
-  }();
-  L.fwd.lead_blocks = (int)blocks_for(std::max(e->K, longest_factor(e)), lead_max);
+  L.fwd.lead_blocks = (int)blocks_for(std::max(e->K, longest_factor(e)), mi::kElboMaxBlocks);
   int64_t longest = 1;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind == MI_DRAW_NONE) longest = std::max(longest, e->factors[f].n);
@@ -1012,7 +957,7 @@ Layout make_layout(const mi_elbo* e) {
     L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
     // long lists over few particles (a fused draw's block rows: ~1000 segments, K = 128): 16
     // particles x 16 segment groups per block, for more blocks and fewer serial loads per lane
-    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? env_kred_long()
+    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? 16
                     : (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred()
                                                                      : mi::kRedKWide;
     nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
