@@ -353,7 +353,7 @@ def test_fused_elbo_matches_unfused_composition(device):
     ref.backward()
     assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref))
     for name, p in approx.named_parameters():
-        torch.testing.assert_close(fused[name], p.grad, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(fused[name], p.grad, rtol=1e-5, atol=1e-6)
 
 
 def test_fused_elbo_scales_with_upstream(device):
@@ -462,7 +462,7 @@ def test_linear_site_matches_materialised_product(device, family, p, K, monkeypa
     for name in plain[1]:
         # gradients are sums of terms of both signs: the absolute tolerance follows their scale
         scale = max(1.0, float(plain[1][name].abs().max()))
-        torch.testing.assert_close(fused[1][name], plain[1][name], rtol=1e-4, atol=1e-5 * scale)
+        torch.testing.assert_close(fused[1][name], plain[1][name], rtol=1e-5, atol=1e-5 * scale)
 
 
 def _hierarchical(device, n, use_exp=False):
@@ -511,7 +511,7 @@ def test_fused_guide_draw_matches_materialised(device, n, use_exp, monkeypatch):
     plain = run()
     assert abs(fused[0] - plain[0]) <= 1e-5 * abs(plain[0])
     for name in plain[1]:
-        torch.testing.assert_close(fused[1][name], plain[1][name], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(fused[1][name], plain[1][name], rtol=1e-5, atol=1e-5)
 
 
 def _absorb_cases(device, case):
@@ -584,8 +584,8 @@ def test_absorbed_draws_match_autograd(device, case, monkeypatch):
     plain = run()
     assert abs(absorbed[0] - plain[0]) <= 1e-5 * abs(plain[0])
     for name in plain[1]:
-        torch.testing.assert_close(absorbed[1][name], plain[1][name], rtol=1e-4, atol=1e-5)
-        torch.testing.assert_close(scaled[1][name], -1.5 * plain[1][name], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(absorbed[1][name], plain[1][name], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(scaled[1][name], -1.5 * plain[1][name], rtol=1e-5, atol=1e-5)
 
 
 def test_absorption_plan(device):

@@ -6,7 +6,7 @@ gradients (normal.py:88-103, bernoulli.py:121-125), over ragged row counts, part
 not multiples of 32, feature counts with one and two 32-feature tiles, masks, strided X rows and a
 transposed theta.
 
-Tolerances: totals 1e-5 relative (the north-star ELBO tolerance); gradients 1e-4 relative of the
+Tolerances: totals 1e-5 relative (the north-star ELBO tolerance); gradients 1e-5 relative of the
 sum of |terms|, since they are sums of terms of both signs.
 """
 import ctypes
@@ -129,9 +129,9 @@ def test_linear_kernel_matches_fp64(device, family, case, valu):
     assert flags == 0
     np.testing.assert_allclose(total, want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
     err = np.abs(dslots[:P].T - dtheta)
-    assert (err <= 1e-4 * abs(g0) * bound + 1e-7).all(), err.max()
+    assert (err <= 1e-5 * abs(g0) * bound + 1e-7).all(), err.max()
     if per_particle:
-        assert (np.abs(dslots[P] - dsigma) <= 1e-4 * abs(g0) * sbound + 1e-7).all()
+        assert (np.abs(dslots[P] - dsigma) <= 1e-5 * abs(g0) * sbound + 1e-7).all()
 
 
 def test_linear_kernel_flags(device):
