@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 7
+#define MI_ABI_VERSION 8
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -267,6 +267,19 @@ int mi_categorical_forward(const float* logits, int64_t stride_k, int64_t stride
                            float* dlogits, void* workspace, size_t workspace_bytes, float* total,
                            uint32_t* flags, void* stream);
 int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
+
+/* MultivariateNormal site (replaces MultivariateNormal.log_prob, multivariate_normal.py:255-262,
+ * with _batch_mahalanobis at :80-102; sites such as examples/missing-observations.md:42), float64,
+ * row-major contiguous value[b, n], loc[b, n] and lower-triangular scale_tril[b, n, n] (the
+ * caller factorises the covariance). Per batch item b, with w = L^-1 (value - loc):
+ *   log_prob[b] = -0.5 w.w - sum_i log L_ii - n/2 log(2 pi),
+ * and w[b, :], u[b, :] = L^-T w are written for the gradients:
+ *   d/dvalue = -u, d/dloc = u, d/dL = tril(u w^T) - diag(1 / L_ii).
+ * n <= MI_MVN_MAX_N. */
+#define MI_MVN_MAX_N 1024
+int mi_mvn_tril_forward(const double* value, const double* loc, const double* scale_tril,
+                        int64_t batch, int64_t n, double* log_prob, double* w, double* u,
+                        void* stream);
 
 /* ---- guide reparameterised sampling (replaces nn.py:133-145 -> Normal/Beta.rsample) ------------ */
 

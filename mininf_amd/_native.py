@@ -37,7 +37,7 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 7   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 8   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -197,6 +197,8 @@ _SIGNATURES = {
                                               c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_double,
                                               ctypes.c_float, c_vp, c_vp, ctypes.c_size_t, c_vp,
                                               c_vp, c_vp]),
+    "mi_mvn_tril_forward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                           c_vp]),
     "mi_normal_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
                                          ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                          c_vp]),

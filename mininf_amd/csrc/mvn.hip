@@ -1,0 +1,89 @@
+// MultivariateNormal site density over a batch of lower-triangular factors: the log_prob of
+// torch.distributions.MultivariateNormal (multivariate_normal.py:255-262, _batch_mahalanobis at
+// :80-102) for the reference's Gaussian-process sites (examples/missing-observations.md:42),
+// evaluated per particle after the covariance is factorised (rocSOLVER, float64, by the caller).
+//
+// One wave per batch item b (a particle): with r = value - loc,
+//   w = L^-1 r        (forward substitution, right-looking: column i of L updates the rest of r)
+//   u = L^-T w        (back substitution, row i of L: the gradient direction)
+//   log_prob = -0.5 w.w - sum_i log L_ii - n/2 log(2 pi).
+// The working vectors live in LDS (n <= MI_MVN_MAX_N); lane j owns elements j, j + 64, ...
+// Column reads of L are strided but L2-resident (n^2 doubles per particle); the whole step is
+// latency bound, O(n) dependent rounds per wave. float64 throughout: the example's GP covariance
+// (jitter 1e-3) is too ill-conditioned for a float32 solve, the reason the host path refactorises
+// in float64 too.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace mi {
+
+constexpr int kMvnThreads = 64;
+
+__global__ __launch_bounds__(kMvnThreads) void k_mvn_tril(const double* __restrict__ value,
+                                                          const double* __restrict__ loc,
+                                                          const double* __restrict__ L, int n,
+                                                          double* __restrict__ log_prob,
+                                                          double* __restrict__ w_out,
+                                                          double* __restrict__ u_out) {
+  __shared__ double r[MI_MVN_MAX_N];
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const double* Lb = L + b * (int64_t)n * n;
+  for (int j = lane; j < n; j += kMvnThreads) r[j] = value[b * n + j] - loc[b * n + j];
+  __syncthreads();
+  // forward substitution: r becomes w
+  for (int i = 0; i < n; ++i) {
+    const double wi = r[i] / Lb[(int64_t)i * n + i];
+    __syncthreads();   // every lane has read r[i]
+    for (int j = lane; j < n; j += kMvnThreads) {
+      if (j == i) r[j] = wi;
+      else if (j > i) r[j] = fma(-Lb[(int64_t)j * n + i], wi, r[j]);
+    }
+    __syncthreads();
+  }
+  double quad = 0.0, logdet = 0.0;
+  for (int j = lane; j < n; j += kMvnThreads) {
+    const double wj = r[j];
+    quad = fma(wj, wj, quad);
+    logdet += log(Lb[(int64_t)j * n + j]);
+    w_out[b * n + j] = wj;
+  }
+  for (int off = kMvnThreads / 2; off > 0; off >>= 1) {
+    quad += __shfl_xor(quad, off);
+    logdet += __shfl_xor(logdet, off);
+  }
+  if (lane == 0) log_prob[b] = -0.5 * quad - logdet - 0.5 * n * log(2.0 * M_PI);
+  // back substitution: L^T u = w, r becomes u
+  for (int i = n - 1; i >= 0; --i) {
+    const double ui = r[i] / Lb[(int64_t)i * n + i];
+    __syncthreads();
+    for (int j = lane; j < n; j += kMvnThreads) {
+      if (j == i) r[j] = ui;
+      else if (j < i) r[j] = fma(-Lb[(int64_t)i * n + j], ui, r[j]);
+    }
+    __syncthreads();
+  }
+  for (int j = lane; j < n; j += kMvnThreads) u_out[b * n + j] = r[j];
+}
+
+}  // namespace mi
+
+extern "C" {
+
+int mi_mvn_tril_forward(const double* value, const double* loc, const double* scale_tril,
+                        int64_t batch, int64_t n, double* log_prob, double* w, double* u,
+                        void* stream) {
+  if (batch < 0 || n < 1 || n > MI_MVN_MAX_N || batch > 0x7fffffff)
+    return MI_EINVAL;
+  if (batch == 0) return 0;
+  if (value == nullptr || loc == nullptr || scale_tril == nullptr || log_prob == nullptr ||
+      w == nullptr || u == nullptr)
+    return MI_EINVAL;
+  hipLaunchKernelGGL(mi::k_mvn_tril, dim3((unsigned)batch), dim3(mi::kMvnThreads), 0,
+                     static_cast<hipStream_t>(stream), value, loc, scale_tril, (int)n, log_prob,
+                     w, u);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

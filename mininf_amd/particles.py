@@ -11,9 +11,10 @@ plugin point, ``core.py:128-140``) that, instead of evaluating log densities, re
 family, parameter tensors, value, mask and minibatch scale. The recorded [K, ...] tensors come back
 out of ``vmap`` and are handed to the HIP site kernels (:mod:`mininf_amd.engine`).
 
-Sites whose family has no HIP kernel (Gamma, Poisson, MultivariateNormal, InverseGamma, ...) are
-evaluated with ``torch.distributions`` inside the same ``vmap`` (on the GPU) and contribute one
-per-particle sum; they are outside the north-star families and listed in DESIGN.md.
+Sites recorded as "torch" sites (MultivariateNormal, other families without a site kernel) are
+evaluated inside the same ``vmap`` (on the GPU) and contribute one per-particle sum; a float32
+MultivariateNormal is refactorised in float64 and its density runs on ``mi_mvn_tril_forward``
+(:mod:`mininf_amd.mvn`), anything else through ``torch.distributions``.
 """
 from __future__ import annotations
 
@@ -33,7 +34,7 @@ from torch.distributions.utils import lazy_property
 from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_flatten, tree_map
 
-from . import core, data
+from . import core, data, mvn
 from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
 from .util import _normalize_shape, check_constraint, OptionalSize
 
@@ -388,7 +389,12 @@ class ParticleTracer(TracerMixin):
                 data.device.type != "cpu":
             # dense factorisations of float32 covariances are ill-conditioned in practice (the
             # missing-observations example's GP prior): refactorise in float64 on the device
-            log_prob = _mvn_float64(distribution).log_prob(data.double()).float()
+            # refactorise in float64 on the device; the density itself runs on mi_mvn_tril_forward
+            distribution = _mvn_float64(distribution)
+            if mvn.enabled(distribution):
+                log_prob = mvn.log_prob(distribution, data).float()
+            else:
+                log_prob = distribution.log_prob(data.double()).float()
         else:
             log_prob = distribution.log_prob(data)
         if mask is not None:

@@ -1,0 +1,100 @@
+"""
+MultivariateNormal site density on mi_mvn_tril_forward (csrc/mvn.hip, mininf_amd/mvn.py) against
+torch's float64 MultivariateNormal.log_prob and its autograd (multivariate_normal.py:255-262), at
+1e-10 relative (both float64): values and gradients with respect to value, loc and the covariance
+(through torch's Cholesky), event sizes below, at and above one wave (lane loops), broadcast batch
+shapes, the vmap rule of the particle trace, and the missing-observations example's GP site running
+on the kernel (its ELBO parity against the reference's fixture is tests/test_gpu_examples.py).
+"""
+import numpy as np
+import pytest
+import torch
+from torch.distributions import MultivariateNormal
+
+from mininf_amd import mvn
+
+pytestmark = pytest.mark.gpu
+
+
+def spd(batch, n, device, gen):
+    a = torch.randn(*batch, n, n, generator=gen, dtype=torch.float64).to(device)
+    return a @ a.transpose(-1, -2) / n + 0.5 * torch.eye(n, dtype=torch.float64, device=device)
+
+
+def rel(got, want):
+    return float((got - want).abs().max() / max(float(want.abs().max()), 1e-300))
+
+
+@pytest.mark.parametrize("n,vbatch,cbatch", [(1, (3,), (3,)), (50, (8,), (8,)),
+                                             (64, (2, 5), (5,)), (130, (4,), ()),
+                                             (7, (), (6,))])
+def test_mvn_kernel_matches_torch(device, n, vbatch, cbatch):
+    gen = torch.Generator().manual_seed(n)
+    cov = spd(cbatch, n, device, gen)
+    loc = torch.randn(n, generator=gen, dtype=torch.float64).to(device)
+    value = torch.randn(*vbatch, n, generator=gen, dtype=torch.float64).to(device)
+    out = []
+    for kernel in (True, False):
+        c = cov.clone().requires_grad_()
+        m = loc.clone().requires_grad_()
+        v = value.clone().requires_grad_()
+        d = MultivariateNormal(m, covariance_matrix=c, validate_args=False)
+        assert mvn.enabled(d)
+        lp = mvn.log_prob(d, v) if kernel else d.log_prob(v)
+        (lp * torch.linspace(0.5, 1.5, lp.numel(), dtype=torch.float64,
+                             device=device).reshape(lp.shape)).sum().backward()
+        out.append((lp.detach(), v.grad, m.grad, c.grad))
+    for got, want, name in zip(out[0], out[1], ("log_prob", "dvalue", "dloc", "dcov")):
+        assert got.shape == want.shape, name
+        assert rel(got, want) <= 1e-10, (name, rel(got, want))
+
+
+def test_mvn_kernel_under_vmap(device):
+    """The particle trace's vmap rule: batched covariance and value, shared loc."""
+    gen = torch.Generator().manual_seed(3)
+    K, n = 16, 50
+    cov = spd((K,), n, device, gen)
+    value = torch.randn(K, n, generator=gen, dtype=torch.float64).to(device)
+    loc = torch.zeros(n, dtype=torch.float64, device=device)
+
+    def per_particle(c, v):
+        return mvn.log_prob(MultivariateNormal(loc, covariance_matrix=c, validate_args=False), v)
+
+    got = torch.func.vmap(per_particle)(cov, value)
+    want = MultivariateNormal(loc, covariance_matrix=cov).log_prob(value)
+    assert rel(got, want) <= 1e-10
+
+
+def test_mvn_kernel_rejects_oversized_events(device):
+    from mininf_amd import _native as nat
+    buf = torch.zeros(8, dtype=torch.float64, device=device).data_ptr()
+    assert nat.lib().mi_mvn_tril_forward(buf, buf, buf, 1, mvn.MAX_N + 1, buf, buf, buf,
+                                         None) == -1
+
+
+def test_missing_observations_gp_site_runs_on_kernel(device, monkeypatch):
+    """The example's GP prior (MultivariateNormal over 50 points) goes through mi_mvn_tril_forward
+    once per ELBO evaluation, for all particles at once."""
+    import mininf_amd as mi
+    from torch.distributions import Gamma, Normal
+    from tests import example_models as ex
+    calls = []
+    launch = mvn._launch
+
+    def counted(value, loc, scale_tril):
+        calls.append(tuple(scale_tril.shape))
+        return launch(value, loc, scale_tril)
+    monkeypatch.setattr(mvn, "_launch", counted)
+    n, K = ex.MISSING_N, 8
+    approximation = mi.nn.ParameterizedFactorizedDistribution(
+        z=mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n), scale=torch.ones(n)),
+        sigma=mi.nn.ParameterizedDistribution(Gamma, concentration=2, rate=2),
+        length_scale=mi.nn.ParameterizedDistribution(Gamma, concentration=2, rate=2),
+    ).to(device)
+    y = torch.randn(n, device=device)
+    loss = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=0)(
+        mi.condition(ex.missing_model, {"kappa": torch.tensor(0.1, device=device)}, y=y),
+        approximation())
+    loss.backward()
+    assert np.isfinite(float(loss))
+    assert calls and all(shape[-2:] == (n, n) and shape[0] == K for shape in calls), calls
