@@ -8,36 +8,48 @@
 //   u = L^-T w        (back substitution, row i of L: the gradient direction)
 //   log_prob = -0.5 w.w - sum_i log L_ii - n/2 log(2 pi).
 // The working vectors live in LDS (n <= MI_MVN_MAX_N); lane j owns elements j, j + 64, ...
-// Column reads of L are strided but L2-resident (n^2 doubles per particle); the whole step is
-// latency bound, O(n) dependent rounds per wave. float64 throughout: the example's GP covariance
-// (jitter 1e-3) is too ill-conditioned for a float32 solve, the reason the host path refactorises
-// in float64 too.
+// Factors with n <= kMvnLdsMaxN are staged in LDS by one coalesced pass, so each of the 2n
+// dependent rounds reads LDS instead of making an L2 round trip; larger ones are read from global
+// memory (L2-resident, n^2 doubles per particle). The kernel is latency bound either way.
+// float64 throughout: the example's GP covariance (jitter 1e-3) is too ill-conditioned for a
+// float32 solve, the reason the host path refactorises in float64 too.
 #include "common.hpp"
 #include "internal.hpp"
+
+#include <cstdlib>
 
 namespace mi {
 
 constexpr int kMvnThreads = 64;
+// factors up to this size are staged in LDS (row stride n + 1: column reads hit distinct banks)
+constexpr int kMvnLdsMaxN = 80;   // 51.8 KB + the 8 KB vector: within 64 KB per workgroup
 
+template <bool kLds>
 __global__ __launch_bounds__(kMvnThreads) void k_mvn_tril(const double* __restrict__ value,
                                                           const double* __restrict__ loc,
                                                           const double* __restrict__ L, int n,
                                                           double* __restrict__ log_prob,
                                                           double* __restrict__ w_out,
                                                           double* __restrict__ u_out) {
+  extern __shared__ double lds[];   // kLds: the factor, [n][n + 1]
   __shared__ double r[MI_MVN_MAX_N];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
-  const double* Lb = L + b * (int64_t)n * n;
+  const double* Lg = L + b * (int64_t)n * n;
+  const int ld = kLds ? n + 1 : n;
+  if (kLds) {
+    for (int e = lane; e < n * n; e += kMvnThreads) lds[(e / n) * ld + e % n] = Lg[e];
+  }
+  const double* Lb = kLds ? lds : Lg;
   for (int j = lane; j < n; j += kMvnThreads) r[j] = value[b * n + j] - loc[b * n + j];
   __syncthreads();
   // forward substitution: r becomes w
   for (int i = 0; i < n; ++i) {
-    const double wi = r[i] / Lb[(int64_t)i * n + i];
+    const double wi = r[i] / Lb[i * ld + i];
     __syncthreads();   // every lane has read r[i]
     for (int j = lane; j < n; j += kMvnThreads) {
       if (j == i) r[j] = wi;
-      else if (j > i) r[j] = fma(-Lb[(int64_t)j * n + i], wi, r[j]);
+      else if (j > i) r[j] = fma(-Lb[j * ld + i], wi, r[j]);
     }
     __syncthreads();
   }
@@ -45,7 +57,7 @@ __global__ __launch_bounds__(kMvnThreads) void k_mvn_tril(const double* __restri
   for (int j = lane; j < n; j += kMvnThreads) {
     const double wj = r[j];
     quad = fma(wj, wj, quad);
-    logdet += log(Lb[(int64_t)j * n + j]);
+    logdet += log(Lb[j * ld + j]);
     w_out[b * n + j] = wj;
   }
   for (int off = kMvnThreads / 2; off > 0; off >>= 1) {
@@ -55,11 +67,11 @@ __global__ __launch_bounds__(kMvnThreads) void k_mvn_tril(const double* __restri
   if (lane == 0) log_prob[b] = -0.5 * quad - logdet - 0.5 * n * log(2.0 * M_PI);
   // back substitution: L^T u = w, r becomes u
   for (int i = n - 1; i >= 0; --i) {
-    const double ui = r[i] / Lb[(int64_t)i * n + i];
+    const double ui = r[i] / Lb[i * ld + i];
     __syncthreads();
     for (int j = lane; j < n; j += kMvnThreads) {
       if (j == i) r[j] = ui;
-      else if (j < i) r[j] = fma(-Lb[(int64_t)i * n + j], ui, r[j]);
+      else if (j < i) r[j] = fma(-Lb[i * ld + j], ui, r[j]);
     }
     __syncthreads();
   }
@@ -79,9 +91,20 @@ int mi_mvn_tril_forward(const double* value, const double* loc, const double* sc
   if (value == nullptr || loc == nullptr || scale_tril == nullptr || log_prob == nullptr ||
       w == nullptr || u == nullptr)
     return MI_EINVAL;
-  hipLaunchKernelGGL(mi::k_mvn_tril, dim3((unsigned)batch), dim3(mi::kMvnThreads), 0,
-                     static_cast<hipStream_t>(stream), value, loc, scale_tril, (int)n, log_prob,
-                     w, u);
+  static const bool lds = [] {   // MININF_AMD_MVN_LDS=0: read the factor from global memory
+    const char* v = std::getenv("MININF_AMD_MVN_LDS");
+    return v == nullptr || v[0] != '0';
+  }();
+  if (lds && n <= mi::kMvnLdsMaxN) {
+    const size_t bytes = sizeof(double) * (size_t)n * (size_t)(n + 1);
+    hipLaunchKernelGGL(mi::k_mvn_tril<true>, dim3((unsigned)batch), dim3(mi::kMvnThreads), bytes,
+                       static_cast<hipStream_t>(stream), value, loc, scale_tril, (int)n,
+                       log_prob, w, u);
+  } else {
+    hipLaunchKernelGGL(mi::k_mvn_tril<false>, dim3((unsigned)batch), dim3(mi::kMvnThreads), 0,
+                       static_cast<hipStream_t>(stream), value, loc, scale_tril, (int)n,
+                       log_prob, w, u);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
