@@ -35,6 +35,7 @@ from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_flatten, tree_map
 
 from . import core, data, mvn
+from .distributions import InverseGamma
 from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
 from .util import _normalize_shape, check_constraint, OptionalSize
 
@@ -230,8 +231,14 @@ def _is_inverse_gamma(distribution: Distribution) -> bool:
     t = distribution.transforms[0]
     if type(t) is not PowerTransform or is_batched(t.exponent):
         return False
+    if isinstance(distribution, InverseGamma):   # PowerTransform(-1) by construction
+        return True
     exponent = t.exponent
-    return bool((exponent == -1).all()) if isinstance(exponent, torch.Tensor) else exponent == -1
+    if not isinstance(exponent, torch.Tensor):
+        return exponent == -1
+    if exponent.device.type != "cpu" and torch.cuda.is_current_stream_capturing():
+        return False   # unreadable while capturing: the generic torch site path (same density)
+    return bool((exponent == -1).all())
 
 
 class ParticleTracer(TracerMixin):

@@ -98,3 +98,4 @@ def test_missing_observations_gp_site_runs_on_kernel(device, monkeypatch):
     loss.backward()
     assert np.isfinite(float(loss))
     assert calls and all(shape[-2:] == (n, n) and shape[0] == K for shape in calls), calls
+
