@@ -295,6 +295,9 @@ def check_launch(args, world, rank):
 def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budget):
     """Measure one workload (all ranks); rank 0 gets the bench line's dict."""
     w = workload(config, device, world, rank)
+    if args.particles_per_gpu:
+        w["evals"] = w["evals"] // w["k_local"] * args.particles_per_gpu
+        w["k_local"] = args.particles_per_gpu
     module = w["module"]
     if args.optimizer == "torch":
         optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
@@ -306,17 +309,20 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     timer = EventTimer()
     engine.KERNEL_TIMER = timer
 
-    # N > 1: the step is split around the one all-reduce of the gradients -- zero_grad, forward,
-    # backward and packing the gradients into a flat bucket (captured), the RCCL all-reduce of the
-    # bucket, then Adam on gradients bound to the reduced bucket (captured separately).
-    # The bucket also carries the rank's loss share, so the one all-reduce yields the global ELBO.
-    bucket = GradientBucket(module.parameters(), group, with_loss=True) if world > 1 else None
+    # N > 1: the rank's gradients and its loss share are packed into ONE flat bucket
+    # (distributed.GradientBucket), all-reduced once, and Adam runs on gradients bound to the
+    # reduced bucket. Over RCCL the whole step -- collective included -- is one captured graph
+    # (several steps per replay, like N = 1); gloo cannot be captured, so there the step is split
+    # around the host-issued all-reduce (two graphs).
+    sharded = group is not None
+    bucket = GradientBucket(module.parameters(), group, with_loss=True) if sharded else None
+    collective_in_graph = sharded and args.dist_backend == "nccl"
 
     def forward_backward():
         optimizer.zero_grad(set_to_none=True)
         loss = loss_fn(w["conditioned"](), w["guide"]())
         loss.backward()
-        if world == 1:
+        if not sharded:
             optimizer.step()
         else:
             bucket.pack(loss)
@@ -326,10 +332,13 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         bucket.bind()
         optimizer.step()
 
-    def finish_step():
-        if world > 1:
-            bucket.all_reduce()
-            apply_update()
+    def full_step():
+        loss = forward_backward()
+        if not sharded:
+            return loss
+        bucket.all_reduce()
+        apply_update()
+        return bucket.loss()   # the global loss (sum of the ranks' shares)
 
     def barrier():
         if world > 1:
@@ -352,11 +361,8 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         return seconds, out
 
     def eager_step():
-        loss = forward_backward()
-        finish_step()
-        if world > 1:
-            return bucket.loss()   # the global loss (sum of the ranks' shares)
-        return loss.detach()   # keep no autograd graph alive across steps (graph capture needs it)
+        # detached: keep no autograd graph alive across steps (graph capture needs it)
+        return full_step().detach()
 
     # Eager steps: every kernel launched from Python (the kernel timing comes from these).
     for _ in range(warmup):
@@ -373,28 +379,37 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         # one replay = `repeat` consecutive steps (N = 1): each graph launch leaves the device
         # idle ~13 us, which a launch-bound step amortises (mininf_amd.graph.StepGraph)
         repeat = 1
-        if world == 1:
+        if not sharded or collective_in_graph:
             repeat = args.graph_repeat or next(r for r in (8, 6, 5, 4, 3, 2, 1) if steps % r == 0)
             if steps % repeat:
                 raise SystemExit(f"--graph-repeat {repeat} does not divide --steps {steps}")
-        captured = StepGraph(forward_backward, warmup=2, repeat=repeat)
-        update = StepGraph(apply_update, warmup=1) if world > 1 else None
+        if not sharded or collective_in_graph:
+            # RCCL's watchdog thread polls events during the capture: thread-local capture mode
+            graph_step = StepGraph(full_step, warmup=2, repeat=repeat,
+                                   capture_error_mode="thread_local" if sharded else "global")
+            captured = graph_step
+        else:
+            # warm-up with whole steps (all-reduce and update included), so the training state
+            # advances as in the captured N = 1 / RCCL steps; the update graph needs none
+            captured = StepGraph(forward_backward, warmup=2, warmup_step=full_step)
+            update = StepGraph(apply_update, warmup=0)
 
-        def graph_step():
-            out = captured()
-            if world > 1:
+            def graph_step():
+                captured()
                 bucket.all_reduce()
                 update()
                 return bucket.loss()
-            return out
 
         for _ in range(max(1, warmup // repeat)):
             graph_step()
         elapsed, loss = timed(graph_step, steps // repeat)
         captured.check()
         mode = "hipGraph replay" + (f" ({repeat} steps per replay)" if repeat > 1 else "")
+        if sharded:
+            mode += (" with the RCCL all-reduce captured in the graph" if collective_in_graph
+                     else f" split around the host-issued {args.dist_backend} all-reduce")
         floor_ms = None
-        if config == "c2" and world == 1:
+        if config == "c2" and not sharded:
             # C2's per-eval sum over x_i l_k is reducible to l_k sum_i x_i:
             # the same step with the site kernel's closed form, reported beside the per-eval number
             os.environ["MININF_AMD_BCAST_SUFFSTAT"] = "1"
@@ -452,7 +467,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                    "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
                    "parallelism": f"particle-sharded x{world}" + (
                        (" + RCCL grad all-reduce" if args.dist_backend == "nccl" else
-                        f" + {args.dist_backend} grad all-reduce") if world > 1 else ""),
+                        f" + {args.dist_backend} grad all-reduce") if sharded else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms,
                    **({"reducible_floor_ms_per_step": floor_ms,
@@ -490,6 +505,11 @@ def main():
     ap.add_argument("--optimizer", choices=("mi", "torch"), default="mi",
                     help="Adam implementation: mininf_amd.optim.Adam (one HIP launch, default) or "
                          "torch.optim.Adam(fused=True, capturable=True)")
+    ap.add_argument("--particles-per-gpu", type=int, default=0,
+                    help="override the config's particles per GPU (0: the config's own)")
+    ap.add_argument("--process-group", action="store_true",
+                    help="run the sharded step (process group, gradient bucket, all-reduce) even "
+                         "at N = 1: measures the N > 1 step's own overhead on one GPU")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile 20 extra steps and print the hottest host functions to stderr")
     ap.add_argument("--check-launch", action="store_true",
@@ -511,17 +531,24 @@ def main():
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     group = None
-    if world > 1:
+    if world > 1 or args.process_group:
         import torch.distributed as dist
+        init = {}
+        if "MASTER_ADDR" not in os.environ:   # --process-group without a launcher: one rank
+            import socket
+            with socket.socket() as sock:
+                sock.bind(("127.0.0.1", 0))
+                port = sock.getsockname()[1]
+            init = dict(init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, **init)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, **init)
         group = dist.group.WORLD
 
     out = run_config(args.config, args, world, rank, device, group, args.steps, args.warmup,
                      0.0 if args.no_cpu_baseline else 12.0)
-    if world == 1 and args.config == "c2" and not args.no_other_configs:
+    if world == 1 and group is None and args.config == "c2" and not args.no_other_configs:
         # the other single-GPU configurations of BASELINE.json, measured in the same run
         # (shorter: 10 graph-replayed steps each; CPU baseline only for C3)
         out["other_configs"] = {}
@@ -533,7 +560,7 @@ def main():
                 if key in sub}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if group is not None:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 8
+#define MI_ABI_VERSION 9
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -351,6 +351,14 @@ int mi_beta_rsample_backward(const float* dx, int64_t dx_stride_k, int64_t dx_st
  * mi_factor.dgrad. */
 int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const float* c0,
                   int64_t c0_stride, int64_t K, int64_t N, double* out, void* stream);
+
+/* Recovery after a failed hipGraph capture of a training step (mininf_amd.graph.StepGraph): if
+ * `stream` is still capturing, end the capture and destroy the partial graph; then clear the
+ * thread's last HIP error. *was_capturing (optional) reports whether a capture had to be ended.
+ * The host-side counterpart of the reference's exception semantics: an error raised inside a step
+ * (mininf/core.py:142-189, nn.py:212-228) leaves the process usable. Not asynchronous: it acts on
+ * the stream's capture state, not on its work. */
+int mi_capture_abandon(void* stream, int* was_capturing);
 
 /* Start of one ELBO step (EvidenceLowerBoundLoss.forward) in one launch: *snapshot = *counter (the
  * generator step this call's draws and their backward use), *counter += 1, and

@@ -37,7 +37,7 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 8   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 9   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 
 c_i64 = ctypes.c_int64
@@ -218,6 +218,7 @@ _SIGNATURES = {
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp, ctypes.c_uint32,
                                            c_i64, c_vp, c_vp, c_vp]),
     "mi_beta_dgrad": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "mi_capture_abandon": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int)]),
     "mi_step_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mi_group_side_supported": (ctypes.c_int, [ctypes.POINTER(Group),
                                                ctypes.POINTER(ctypes.c_int)]),

@@ -28,7 +28,8 @@ from .util import _format_dict_compact, _normalize_shape, check_constraint, \
 
 
 S = TypeVar("S", bound="SingletonContextMixin")
-LOGGER = logging.getLogger(__name__)
+# the reference's logger name (mininf/core.py:16), so existing logging configuration applies
+LOGGER = logging.getLogger("mininf.core")
 
 
 class SingletonContextMixin:

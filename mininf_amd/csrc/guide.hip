@@ -661,6 +661,25 @@ int mi_beta_dgrad(const float* x, const float* c1, int64_t c1_stride, const floa
   return to_code(hipGetLastError());
 }
 
+int mi_capture_abandon(void* stream, int* was_capturing) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  hipError_t err = hipStreamIsCapturing(s, &status);
+  int capturing = err == hipSuccess && status != hipStreamCaptureStatusNone;
+  if (was_capturing != nullptr) *was_capturing = capturing;
+  if (capturing) {
+    hipGraph_t graph = nullptr;
+    err = hipStreamEndCapture(s, &graph);   // ends an invalidated capture too (graph stays NULL)
+    if (graph != nullptr) (void)hipGraphDestroy(graph);
+  }
+  (void)hipGetLastError();
+  hipStreamCaptureStatus after = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &after) == hipSuccess && after != hipStreamCaptureStatusNone)
+    return to_code(err == hipSuccess ? hipErrorStreamCaptureInvalidated : err);
+  (void)hipGetLastError();
+  return 0;
+}
+
 int mi_step_begin(uint64_t* counter, uint64_t* snapshot, uint32_t* flags, int64_t nflags,
                   void* stream) {
   if (counter == nullptr || snapshot == nullptr || nflags < 0 || (nflags > 0 && flags == nullptr))

@@ -145,9 +145,13 @@ class Minibatch(torch.Tensor):
                 return func(*args, **kwargs)
             if func in _VIEWS:
                 out = func(*args, **kwargs)
-                if isinstance(out, torch.Tensor) and not isinstance(out, Minibatch) and \
-                        lookup(out) is not None:
-                    out = out.as_subclass(Minibatch)
+                hit = lookup(out) if isinstance(out, torch.Tensor) else None
+                if hit is not None:
+                    if not isinstance(out, Minibatch):
+                        out = out.as_subclass(Minibatch)
+                    # the view shares the batch's buffer: it keeps the batch (its rows and its
+                    # lookup entry) alive on its own, also after the yielded tensor is dropped
+                    out._mininf_batch = hit[0]
                 return out
             stack = [args, kwargs]
             while stack:   # the call's tensors (lists, tuples and dicts walked)

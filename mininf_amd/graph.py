@@ -29,6 +29,7 @@ optimizer must be created with ``capturable=True`` when its step is part of the 
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import sys
 import threading
 from numbers import Number
@@ -124,6 +125,54 @@ def graph_safe(collector: list):
         Distribution.set_default_validate_args(previous)
 
 
+def _detached(out):
+    if isinstance(out, torch.Tensor):
+        return out.detach()
+    if isinstance(out, (tuple, list)):
+        return type(out)(_detached(o) for o in out)
+    if isinstance(out, dict):
+        return {k: _detached(v) for k, v in out.items()}
+    return out
+
+
+class CaptureError(RuntimeError):
+    """A training step could not be captured into a hipGraph (see :class:`StepGraph`)."""
+
+
+def _abandon_capture(cuda_graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Stream") -> None:
+    """
+    End a capture that failed part-way: torch's ``capture_end`` (which also hands the graph's
+    memory pool back to the caching allocator) when the capture is still valid, then
+    ``mi_capture_abandon`` for a capture torch could not end (an invalidated one), so the stream
+    is no longer capturing; finally wait for the work queued before the capture.
+    """
+    from . import _native as nat
+    try:
+        cuda_graph.capture_end()
+    except Exception:   # invalidated: torch raised before ending the capture
+        pass
+    was = ctypes.c_int(0)
+    nat.check(nat.lib().mi_capture_abandon(stream.cuda_stream, ctypes.byref(was)),
+              "mi_capture_abandon")
+    torch.cuda.synchronize()
+
+
+def _failing_op(error: BaseException) -> str:
+    """``file:line (function)`` of the innermost frame of ``error`` outside torch and this package:
+    the model code whose operation failed."""
+    import os
+    import traceback
+    skip = (os.path.dirname(torch.__file__), os.path.dirname(os.path.abspath(__file__)))
+    frames = [f for f in traceback.extract_tb(error.__traceback__)
+              if not f.filename.startswith(skip)]
+    if not frames:
+        frames = traceback.extract_tb(error.__traceback__)
+    if not frames:
+        return "at an unknown operation"
+    f = frames[-1]
+    return f"at {f.filename}:{f.lineno} ({f.name}: {(f.line or '').strip()})"
+
+
 class StepGraph:
     """
     Capture ``step()`` (any callable running one training step on the current device) and replay
@@ -140,72 +189,75 @@ class StepGraph:
             dozen microseconds of kernels) amortises it over ``repeat`` steps. The step must keep
             its per-step state on the device (generator counter, minibatch counter, optimizer
             step counts), as the engine's own steps do.
+        warmup_step: What the warm-up iterations run (default: ``step``) -- e.g. a whole training
+            step when ``step`` is the part of it before a host-issued collective, so the warm-up
+            advances the training state exactly as the replays will. ``warmup=0`` skips the
+            warm-up (the caller has run the step on this process already).
+        capture_error_mode: ``torch.cuda.CUDAGraph.capture_begin``'s mode. ``"thread_local"`` when
+            the step holds a collective (RCCL): the process group's watchdog thread polls events
+            while the capture runs, which the default ``"global"`` mode refuses.
+
+    Raises:
+        CaptureError: the step ran an operation a capturing stream does not permit (for example
+            a synchronous host-to-device copy). The capture is abandoned, its partial graph freed
+            and the stream left usable; the error names the model line that failed.
     """
-    def __init__(self, step: Callable[[], object], warmup: int = 3, repeat: int = 1) -> None:
+    def __init__(self, step: Callable[[], object], warmup: int = 3, repeat: int = 1,
+                 capture_error_mode: str = "global",
+                 warmup_step: Optional[Callable[[], object]] = None) -> None:
         if repeat < 1:
             raise ValueError("repeat must be a positive integer")
         self.step = step
         self.repeat = repeat
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        count = 0
+        if warmup < 0:
+            raise ValueError("warmup must be non-negative")
+        count = None
         with torch.cuda.stream(side):
-            for _ in range(max(1, warmup)):
+            for _ in range(warmup):
                 collector: List = []
                 with graph_safe(collector), _capture_safe_distributions():
-                    step()
+                    (warmup_step or step)()
                 for joint in collector:
                     joint.raise_on_violation()
                 count = sum(joint.flag_count() for joint in collector)
+                # the joints hold the step's loss: drop them, or the warm-up's autograd graph
+                # (its AccumulateGrad nodes on this side stream) stays alive into the capture
+                del collector
         torch.cuda.current_stream().wait_stream(side)
         # Validation results must survive replays the host does not inspect: the step's words are
         # OR-ed into this accumulator by the graph itself (allocated and zeroed outside the capture)
         # unless the step's only flags already are never-zeroed words (EvidenceLowerBoundLoss in
         # graph mode), which then serve as the accumulator without an extra node.
-        self._accumulator = torch.zeros(max(1, count), dtype=torch.int64,
+        self._accumulator = torch.zeros(max(1, count or 0), dtype=torch.int64,
                                         device=torch.cuda.current_device())
         torch.cuda.synchronize()
 
         self.graph = torch.cuda.CUDAGraph()
         self._joints: List = []
-        with graph_safe(self._joints), _capture_safe_distributions(), \
-                torch.cuda.graph(self.graph):
-            for _ in range(repeat):
-                self.output = step()
-            if len(self._joints) % repeat:
-                raise RuntimeError("the captured steps recorded different validations")
-            per_step = len(self._joints) // repeat
-            # one step's validations: what the host checks (every captured step ORs into the
-            # same words)
-            steps = [self._joints[r * per_step:(r + 1) * per_step] for r in range(repeat)]
-            mirror = None
-            sticky = [j[0] for j in steps] if per_step == 1 else []
-            if sticky and all(j.sticky and j.flag_vector() is not None and
-                              j.flag_vector() is j.flags and
-                              j.flags.data_ptr() == sticky[0].flags.data_ptr() for j in sticky):
-                self._flags_device = sticky[0].flags
-                self._accumulator = None
-                mirror = sticky[0].mirror
-            else:
-                any_flags = False
-                for joints in steps:
-                    flags = [joint.flag_vector() for joint in joints]
-                    flags = [f for f in flags if f is not None]
-                    if not flags:
-                        continue
-                    any_flags = True
-                    vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
-                        else flags[0]
-                    if vector.numel() != count:
-                        raise RuntimeError(f"the captured step has {vector.numel()} validation "
-                                           f"words, its warm-up steps {count}")
-                    self._accumulator.bitwise_or_(vector)
-                if any_flags:
-                    self._flags_device = self._accumulator
-                else:
-                    self._flags_device = None
-                    self._accumulator = None
-            self._joints = steps[0]
+        self._flags_device: Optional[torch.Tensor] = None
+        mirror = None
+        capture_stream = torch.cuda.Stream()
+        capture_stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(capture_stream):
+            self.graph.capture_begin(capture_error_mode=capture_error_mode)
+            try:
+                with graph_safe(self._joints), _capture_safe_distributions():
+                    for _ in range(repeat):
+                        # detached: holding the captured step's autograd graph would keep its
+                        # AccumulateGrad nodes (and their capture stream) alive past the capture
+                        self.output = _detached(step())
+                    mirror = self._record_validation(count)
+            except BaseException as error:
+                self._joints = []
+                _abandon_capture(self.graph, capture_stream)
+                self.graph = None
+                raise CaptureError("the step cannot be captured into a hipGraph, "
+                                   f"{_failing_op(error)}: {type(error).__name__}: {error}") \
+                    from error
+            self.graph.capture_end()
+        torch.cuda.current_stream().wait_stream(capture_stream)
         # The ELBO forward of a sticky step writes its words to pinned host memory itself (the
         # mirror); otherwise the copy is enqueued after each replay (one small asynchronous D2H
         # copy: pinned host memory cannot be allocated while capturing).
@@ -219,6 +271,54 @@ class StepGraph:
                                            pin_memory=True)
         self._done = torch.cuda.Event()
         self._pending = False
+
+    def _record_validation(self, count: int) -> Optional[torch.Tensor]:
+        """
+        Inside the capture: route the captured steps' validation words into words no replay zeroes
+        (``self._flags_device``); returns the pinned mirror the ELBO forward writes, if any.
+        """
+        repeat = self.repeat
+        if len(self._joints) % repeat:
+            raise RuntimeError("the captured steps recorded different validations")
+        per_step = len(self._joints) // repeat
+        # one step's validations: what the host checks (every captured step ORs into the same
+        # words)
+        steps = [self._joints[r * per_step:(r + 1) * per_step] for r in range(repeat)]
+        mirror = None
+        sticky = [j[0] for j in steps] if per_step == 1 else []
+        if sticky and all(j.sticky and j.flag_vector() is not None and
+                          j.flag_vector() is j.flags and
+                          j.flags.data_ptr() == sticky[0].flags.data_ptr() for j in sticky):
+            self._flags_device = sticky[0].flags
+            self._accumulator = None
+            mirror = sticky[0].mirror
+        else:
+            any_flags = False
+            for joints in steps:
+                flags = [joint.flag_vector() for joint in joints]
+                flags = [f for f in flags if f is not None]
+                if not flags:
+                    continue
+                any_flags = True
+                vector = torch.cat([f.to(torch.int64) for f in flags]) if len(flags) > 1 \
+                    else flags[0]
+                if count is None:   # the accumulator must exist (zeroed) before the capture
+                    raise RuntimeError("a step with non-sticky validation words needs at least "
+                                       "one warm-up iteration")
+                if vector.numel() != count:
+                    raise RuntimeError(f"the captured step has {vector.numel()} validation "
+                                       f"words, its warm-up steps {count}")
+                self._accumulator.bitwise_or_(vector)
+            if any_flags:
+                self._flags_device = self._accumulator
+            else:
+                self._flags_device = None
+                self._accumulator = None
+        self._joints = steps[0]
+        for joint in self._joints:
+            if hasattr(joint, "total"):
+                joint.total = None   # only the validation words are read after the capture
+        return mirror
 
     def __call__(self):
         self._check(block=False)

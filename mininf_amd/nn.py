@@ -200,9 +200,11 @@ class _ExpStackFn(torch.autograd.Function):
             P.stride[j] = flat.stride(0) if u.numel() > 1 else 0
             P.transform[j] = _native.TRANSFORM_EXP
         ctx.save_for_backward(out)
-        if _defer_exp():
+        if _defer_exp() and u1.is_contiguous() and u0.is_contiguous():
             # the guide's draw computes and writes the array (mi_beta_rsample_exp); any earlier
-            # reader launches the transform itself (guide.PendingConcentration)
+            # reader launches the transform itself (guide.PendingConcentration). Only for
+            # contiguous parameters: P then points into their own storage, not into a reshape
+            # copy that is freed when this call returns
             return guide.defer_exp(out.as_subclass(guide.PendingConcentration), u1, u0, P)
         _native.check(_native.lib().mi_transform_params(ctypes.byref(P), out.data_ptr(),
                                                         _native.stream_handle(u1.device)),

@@ -39,8 +39,11 @@ class Adam(torch.optim.Optimizer):
             raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
         if not 0.0 <= weight_decay:
             raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        # capturable=True: Optimizer.load_state_dict then moves a loaded `step` (torch.optim.Adam's
+        # default keeps it as a host tensor) to the parameter's device as float32
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
-                                      maximize=maximize, amsgrad=False))
+                                      maximize=maximize, amsgrad=False, capturable=True,
+                                      foreach=None, fused=None, differentiable=False))
         self._counters: Dict[torch.device, torch.Tensor] = {}
 
     def _counter_words(self, device: torch.device) -> torch.Tensor:
@@ -76,6 +79,21 @@ class Adam(torch.optim.Optimizer):
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p,
                                                            memory_format=torch.preserve_format)
+                # the kernel reads and writes every state tensor on the device: a state assigned
+                # or loaded from elsewhere (a host `step`, a checkpoint mapped to the CPU) is moved
+                # here first, never handed over as a host pointer
+                step = state["step"]
+                if not isinstance(step, torch.Tensor):
+                    state["step"] = step = torch.tensor(float(step), dtype=torch.float32,
+                                                        device=p.device)
+                if step.device != p.device or step.dtype != torch.float32 or step.dim() != 0:
+                    state["step"] = step.to(device=p.device, dtype=torch.float32).reshape(())
+                for key in ("exp_avg", "exp_avg_sq"):
+                    moment = state[key]
+                    if moment.device != p.device or moment.dtype != torch.float32 or \
+                            moment.shape != p.shape or not moment.is_contiguous():
+                        state[key] = moment.to(device=p.device, dtype=torch.float32) \
+                            .reshape(p.shape).contiguous()
                 batch.append((p, state))
             for start in range(0, len(batch), nat.ADAM_MAX_TENSORS):
                 chunk = batch[start:start + nat.ADAM_MAX_TENSORS]

@@ -22,6 +22,7 @@ import collections
 import contextlib
 import copy
 import dataclasses
+import hashlib
 import os
 import weakref
 from typing import Any, Callable, Dict, List, Optional, Tuple, cast
@@ -34,7 +35,7 @@ from torch.distributions.utils import lazy_property
 from torch.overrides import TorchFunctionMode
 from torch.utils._pytree import tree_flatten, tree_map
 
-from . import core, data, mvn
+from . import core, data, mvn, predictive
 from .distributions import InverseGamma
 from .core import batch, no_log_prob, State, TracerMixin, Value, validate_shape
 from .util import _normalize_shape, check_constraint, OptionalSize
@@ -138,6 +139,8 @@ def memo_commit(entry: Tuple) -> None:
         _VALIDATED[key] = (ref, version)
 
 
+# host tensors up to this size are also keyed by their contents (device_copy)
+_CONTENT_KEY_BYTES = 1 << 20
 _HOST_COPIES: "collections.OrderedDict[Tuple, Tuple[torch.Tensor, torch.Tensor]]" = \
     collections.OrderedDict()
 
@@ -150,7 +153,28 @@ def device_copy(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     """
     key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t._version, str(device))
     hit = _HOST_COPIES.get(key)
+    if hit is None and t.numel() * t.element_size() <= _CONTENT_KEY_BYTES:
+        # A small host intermediate the model computes afresh on every call (the GP example's
+        # `x[:, None] - x`, examples/missing-observations.md:40) is a new tensor each time: key it
+        # by its contents, so a captured step finds the copy its warm-up made instead of a
+        # host-to-device copy, which a capturing stream refuses.
+        data = t.detach().contiguous()
+        content = ("content", tuple(t.shape), t.dtype, str(device),
+                   hashlib.blake2b(data.numpy().tobytes() if data.dtype != torch.bfloat16 else
+                                   data.view(torch.int16).numpy().tobytes(),
+                                   digest_size=16).digest())
+        hit = _HOST_COPIES.get(content)
+        if hit is not None:
+            _HOST_COPIES.move_to_end(content)
+            return hit[1]
+        key = content
+        t = data
     if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(
+                f"a host tensor of shape {tuple(t.shape)} meets device particles for the first "
+                "time inside a captured step; its host-to-device copy cannot be captured. Build it "
+                "on the device, or run the step once before capturing it.")
         hit = (t, t.to(device))
         _HOST_COPIES[key] = hit
         while len(_HOST_COPIES) > 64:
@@ -368,35 +392,44 @@ class ParticleTracer(TracerMixin):
         self.sites.append(record)
         return value
 
+    def _check_parameters(self, name: str, distribution: Distribution) -> None:
+        """
+        Device checks of the distribution's ``arg_constraints`` (what ``Distribution.__init__``
+        validates on the host in the reference, torch distribution.py:68-80), raised after the
+        vmap with torch's message.
+        """
+        for param, constraint in distribution.arg_constraints.items():
+            # as Distribution.__init__'s validation: parameters the distribution was not
+            # constructed with (lazy properties, e.g. MultivariateNormal.precision_matrix)
+            # are not checked
+            if param not in distribution.__dict__ and (
+                    not hasattr(type(distribution), param) or
+                    isinstance(getattr(type(distribution), param), lazy_property)):
+                continue
+            try:
+                tensor = getattr(distribution, param)
+            except Exception:  # lazily defined, unused parametrisations
+                continue
+            if isinstance(tensor, torch.Tensor):
+                ok = check_constraint(constraint, tensor).all()
+                self.checks.append(CheckRecord(name, self._emit(ok), (
+                    f"Expected parameter {param} of distribution "
+                    f"{type(distribution).__name__} for site '{name}' to satisfy the "
+                    f"constraint {constraint}, but found invalid values"), order=self.order))
+
     def _record_torch_site(self, name: str, distribution: Distribution, value: Any,
                            data: torch.Tensor, mask: Optional[torch.Tensor], scale: float) -> None:
         if isinstance(data, torch.Tensor) and data.device.type != "cpu":
             distribution = _on_device(distribution, data.device)
         if self._validate_parameters:
             self._check_support(name, value, distribution, cast(Constraint, distribution.support))
-            for param, constraint in distribution.arg_constraints.items():
-                # as Distribution.__init__'s validation: parameters the distribution was not
-                # constructed with (lazy properties, e.g. MultivariateNormal.precision_matrix)
-                # are not checked
-                if param not in distribution.__dict__ and (
-                        not hasattr(type(distribution), param) or
-                        isinstance(getattr(type(distribution), param), lazy_property)):
-                    continue
-                try:
-                    tensor = getattr(distribution, param)
-                except Exception:  # lazily defined, unused parametrisations
-                    continue
-                if isinstance(tensor, torch.Tensor):
-                    ok = check_constraint(constraint, tensor).all()
-                    self.checks.append(CheckRecord(name, self._emit(ok), (
-                        f"Expected parameter {param} of distribution "
-                        f"{type(distribution).__name__} for site '{name}' to satisfy the "
-                        f"constraint {constraint}, but found invalid values"), order=self.order))
+            self._check_parameters(name, distribution)
         if type(distribution) is MultivariateNormal and data.dtype == torch.float32 and \
                 data.device.type != "cpu":
             # dense factorisations of float32 covariances are ill-conditioned in practice (the
-            # missing-observations example's GP prior): refactorise in float64 on the device
-            # refactorise in float64 on the device; the density itself runs on mi_mvn_tril_forward
+            # missing-observations example's GP prior): refactorise in float64 on the device;
+            # the density itself runs on mi_mvn_tril_forward. This departs from the reference's
+            # float32 density on purpose (DESIGN.md section 6, "MultivariateNormal precision").
             distribution = _mvn_float64(distribution)
             if mvn.enabled(distribution):
                 log_prob = mvn.log_prob(distribution, data).float()
@@ -563,16 +596,31 @@ class BroadcastTracer(ParticleTracer):
     (``vmap(randomness="different")``: independent per sample) and recorded; shapes are checked as
     the reference does; support checks become device outputs raised after the vmap.
     """
+    def __init__(self, *args, **kwargs) -> None:
+        super().__init__(*args, **kwargs)
+        self.index: Optional[torch.Tensor] = None   # the sample number (batched under vmap)
+        self.seed = 0
+        self.draws = 0
+
     def sample(self, state: State, name: str, distribution: Distribution,
                sample_shape: OptionalSize = None) -> torch.Tensor:
         sample_shape = _normalize_shape(sample_shape)
         value = state.get(name)
         if value is None:
-            value = distribution.sample(sample_shape)
+            if self.index is not None and predictive.supported(distribution):
+                # the HIP samplers, keyed by (seed, this draw's index, sample, element)
+                value = predictive.draw(distribution, sample_shape, self.index, self.seed,
+                                        self.draws)
+            else:
+                value = distribution.sample(sample_shape)
+            self.draws += 1
             state[name] = value
         if self._validate_parameters:
             value = self._coerce(value, name)
             validate_shape(value, name, distribution, sample_shape)
+            # the reference constructs every distribution with validation on, so an invalid
+            # parameter raises there (torch distribution.py:68-80) before the draw is used
+            self._check_parameters(name, distribution)
             self._check_support(name, value, distribution,
                                 cast(Constraint, distribution.support))
         return value
@@ -586,18 +634,25 @@ def broadcast_particles(model: Callable, states: Dict[str, torch.Tensor]) -> Sta
     result lives on the samples' device. Returns a :class:`State` of [S, ...] tensors (Python
     numbers as [S] tensors, as the reference's transpose_states makes them).
     """
-    core._assert_same_batch_size(cast(State, states))
     names = list(states)
     device = next((v.device for v in states.values() if isinstance(v, torch.Tensor)),
                   torch.device("cpu"))
 
     lift = device if device.type != "cpu" else None
 
+    S = core._assert_same_batch_size(cast(State, states))
+    index = torch.arange(S, device=device)
+    # one seed per call from torch's generator: reproducible under torch.manual_seed
+    seed = int(torch.randint(0, 2 ** 62, ()).item())
+
     def run(compat: bool):
         tracer = BroadcastTracer()
+        tracer.seed = seed
         keys: List[str] = []
 
-        def per_sample(*values):
+        def per_sample(sample_index, *values):
+            tracer.index = sample_index if lift is not None else None
+            tracer.draws = 0
             inner = State(dict(zip(names, values)))
             with tracer, inner, contextlib.ExitStack() as stack:
                 if compat:
@@ -613,9 +668,10 @@ def broadcast_particles(model: Callable, states: Dict[str, torch.Tensor]) -> Sta
         Distribution.set_default_validate_args(False)
         try:
             outputs = torch.func.vmap(per_sample, randomness="different")(
-                *[states[name] for name in names])
+                index, *[states[name] for name in names])
         finally:
             Distribution.set_default_validate_args(previous)
+            tracer.index = None
         return tracer, keys, outputs
 
     try:

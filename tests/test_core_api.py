@@ -321,6 +321,8 @@ def test_batch_oversize_warns_and_errors(caplog):
             mi.sample("x", dist, (14, 9))
     torch.testing.assert_close(lp.total, dist.log_prob(x).sum() * 14 / 15)
     assert "exceeds expected batch shape" in caplog.messages[0]
+    # the reference's logger name (mininf/core.py:16)
+    assert caplog.records[0].name == "mininf.core"
     with mi.State(x=x), pytest.raises(ValueError, match="has more dimensions"), \
             core.LogProbTracer(), mi.batch([7, 9, 2]):
         mi.sample("x", dist, (14, 9))

@@ -54,6 +54,32 @@ def test_graph_replays_match_eager_steps(device):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
 
 
+def test_failed_capture_leaves_the_process_usable(device):
+    """A step that runs an operation a capturing stream refuses (a synchronous copy from pageable
+    host memory) raises CaptureError naming the model line; the capture is abandoned, so the
+    same process then captures and replays a good step (a failed capture used to
+    poison every later test)."""
+    from mininf_amd.graph import CaptureError
+    step, _, _ = coin_setup(device, n=1000, K=16)
+    host = torch.arange(4, dtype=torch.float32)
+    calls = []
+
+    def bad_step():
+        loss = step()
+        if torch.cuda.is_current_stream_capturing():
+            calls.append(1)
+            host.to(device)   # pageable host-to-device copy: not capturable
+        return loss
+
+    with pytest.raises(CaptureError, match="host.to.device"):
+        StepGraph(bad_step, warmup=1)
+    assert calls == [1]
+    assert not torch.cuda.is_current_stream_capturing()
+    # the process is usable: plain work, then a fresh capture and replays that match eager steps
+    assert float((torch.ones(8, device=device) * 2).sum()) == 16.0
+    test_graph_replays_match_eager_steps(device)
+
+
 def test_multi_step_replays_match_eager_steps(device):
     """StepGraph(repeat=3): each replay runs three full steps (the bench's launch amortisation);
     losses of every third step and the parameters match eager steps."""

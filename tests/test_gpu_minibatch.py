@@ -174,3 +174,20 @@ def test_invalid_values_raise_reference_message(device):
     Xb, yb = next(iter(loader))
     with pytest.raises(ValueError, match="is not in the support"):
         loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": guide_module(device)()})
+
+
+def test_view_outlives_the_yielded_tensor(device):
+    """A view of a minibatch keeps its batch alive on its own: reading it after the yielded tensor
+    is gone still gathers the batch's rows."""
+    import gc
+    n, batch = 1000, 64
+    X = torch.arange(n * 2, dtype=torch.float32, device=device).reshape(n, 2)
+    loader = DeviceDataLoader(X, batch_size=batch, shuffle=True, drop_last=True, seed=9)
+    (xb,) = loader.next()
+    rows = xb._mininf_batch.rows.cpu()
+    view = xb.reshape(-1, 1)
+    assert isinstance(view, Minibatch)
+    del xb
+    gc.collect()
+    got = view.clone().as_subclass(torch.Tensor).reshape(batch, 2).cpu()
+    assert torch.equal(got, X.cpu()[rows.long()])

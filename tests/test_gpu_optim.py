@@ -65,3 +65,42 @@ def test_captured_steps_advance(device):
     for a, b in zip(params, ref):
         assert torch.equal(a.detach(), b.detach())
     assert float(opt.state[params[1]]["step"]) == 5.0
+
+
+@pytest.mark.parametrize("source", ["default", "fused_cpu_mapped"])
+def test_loads_a_torch_adam_state_dict(device, source):
+    """A torch.optim.Adam state_dict (its default keeps `step` as a host tensor; a checkpoint
+    mapped to the CPU moves every state tensor there) loads into this Adam, whose later updates
+    stay bit-identical to torch's fused Adam continuing from the same state."""
+    shapes = [(), (3,), (1000,), (300_000,)]
+    ours, ref, start = make(device, shapes), make(device, shapes), make(device, shapes)
+    gen = torch.Generator().manual_seed(2)
+    grads = [[torch.randn(s, generator=gen).to(device) for s in shapes] for _ in range(6)]
+    opt_start = torch.optim.Adam(start, lr=0.01, fused=source != "default")
+    for g in grads[:3]:
+        for p, gi in zip(start, g):
+            p.grad = gi.clone()
+        opt_start.step()
+    saved = opt_start.state_dict()
+    if source == "fused_cpu_mapped":
+        saved = {"state": {k: {n: t.cpu() for n, t in v.items()} for k, v in saved["state"].items()},
+                 "param_groups": saved["param_groups"]}
+    with torch.no_grad():
+        for a, b, s in zip(ours, ref, start):
+            a.copy_(s)
+            b.copy_(s)
+    opt, opt_ref = Adam(ours, lr=0.01), torch.optim.Adam(ref, lr=0.01, fused=True)
+    opt.load_state_dict(saved)
+    # the reference continues as fused Adam (its groups' `fused` comes from the loaded dict)
+    opt_ref.load_state_dict({"state": saved["state"],
+                             "param_groups": [dict(g, fused=True) for g in saved["param_groups"]]})
+    for g in grads[3:]:
+        for a, b, gi in zip(ours, ref, g):
+            a.grad, b.grad = gi.clone(), gi.clone()
+        opt.step()
+        opt_ref.step()
+    for a, b in zip(ours, ref):
+        assert torch.equal(a, b)
+        sa = opt.state[a]
+        assert sa["step"].device == a.device and sa["step"].dtype == torch.float32
+        assert float(sa["step"]) == 6.0
