@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 import mininf_amd  # noqa: E402
 import mininf_amd.optim  # noqa: E402
-from mininf_amd import engine  # noqa: E402
+from mininf_amd import engine, rccl  # noqa: E402
 from mininf_amd.distributed import GradientBucket  # noqa: E402
 from mininf_amd.graph import StepGraph  # noqa: E402
 from torch.distributions import Bernoulli, Beta, Normal  # noqa: E402
@@ -315,8 +315,12 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     # (several steps per replay, like N = 1); gloo cannot be captured, so there the step is split
     # around the host-issued all-reduce (two graphs).
     sharded = group is not None
-    bucket = GradientBucket(module.parameters(), group, with_loss=True) if sharded else None
     collective_in_graph = sharded and args.dist_backend == "nccl"
+    # over RCCL the all-reduce runs on a communicator of our own (mininf_amd.rccl: RCCL called
+    # directly, no process-group watchdog polling events of the captured collective)
+    comm = rccl.Communicator(group, device) if collective_in_graph else None
+    bucket = GradientBucket(module.parameters(), group, with_loss=True,
+                            communicator=comm) if sharded else None
 
     def forward_backward():
         optimizer.zero_grad(set_to_none=True)

@@ -124,7 +124,11 @@ typedef struct mi_draw {
    * transform_to(positive), nn.py:86-96, as mi_transform_params) and the first particle block
    * writes it to `scale` -- the transform inside the draw's kernel */
   const float* scale_exp;
-  int64_t pad0;
+  /* Global index of element 0 of this draw (a multiple of 4; 0 unless the guide factor is sharded
+   * over ranks along its elements, mininf_amd.distributed.DataShard): element i uses the
+   * counter block of global element element_offset + i, so the ranks' slices draw exactly what
+   * one process drawing all elements would. */
+  int64_t element_offset;
 } mi_draw;
 
 /* Independent work carried by extra workgroups of a group's launch (see mi_group_side_supported):
@@ -284,15 +288,16 @@ int mi_mvn_tril_forward(const double* value, const double* loc, const double* sc
 /* ---- guide reparameterised sampling (replaces nn.py:133-145 -> Normal/Beta.rsample) ------------ */
 
 /* Counter-based Philox-4x32-7 normals: eps[k, i] is a function of (seed, step, stream_id,
- * particle_offset + k, i) only, so the union of draws is independent of how particles are sharded
- * across GPUs. z[k, i] = loc[i] + eps[k, i] * scale[i] (normal.py:83-86). If `eps` is non-NULL it is
+ * particle_offset + k, element_offset + i) only, so the union of draws is independent of how
+ * particles (particle_offset) or elements (element_offset, a multiple of 4) are sharded across
+ * GPUs. z[k, i] = loc[i] + eps[k, i] * scale[i] (normal.py:83-86). If `eps` is non-NULL it is
  * used instead of the generator (parity mode: injected host noise, row-major [K, N]).
  * The effective step is `step + *step_device` when `step_device` (a device uint64) is non-NULL, so
  * a captured HIP graph advances the generator by incrementing that word on the device. */
 int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
                       int64_t K, int64_t N, uint64_t seed, uint64_t step,
                       const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
-                      const float* eps, float* z, void* stream);
+                      int64_t element_offset, const float* eps, float* z, void* stream);
 
 /* mi_normal_rsample for a guide whose scale is exp of an unconstrained parameter u
  * (ParameterizedDistribution.forward, nn.py:86-96 -> transform_to(positive)): the draws use
@@ -301,14 +306,15 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
 int mi_normal_rsample_exp(const float* loc, int64_t loc_stride, const float* u, int64_t u_stride,
                           float* scale_out, int64_t K, int64_t N, uint64_t seed, uint64_t step,
                           const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
-                          const float* eps, float* z, void* stream);
+                          int64_t element_offset, const float* eps, float* z, void* stream);
 
 /* Backward of mi_normal_rsample: dloc[i] = sum_k dz[k,i], dscale[i] = sum_k dz[k,i] * eps[k,i]
  * with eps regenerated from the counter (or read from `eps`). */
 int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
 int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
                                int64_t K, int64_t N, uint64_t seed, uint64_t step,
-                               const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset, const float* eps,
+                               const uint64_t* step_device, uint32_t stream_id,
+                               int64_t particle_offset, int64_t element_offset, const float* eps,
                                void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
                                void* stream);
 
@@ -587,9 +593,14 @@ typedef struct mi_factor {
                                    and mi_elbo_backward of the same evaluation reads (required).
                                    Owned by the caller per evaluation, so evaluations sharing a
                                    workspace may interleave (loss1 + loss2, then backward). */
+  int64_t element_offset;       /* Normal, regenerated eps: the draw's mi_draw.element_offset */
+  double weight;                /* this factor's entropy enters as entropy_scale * weight * H_f:
+                                   1 for a factor every rank holds whole or owns a slice of, 1/W
+                                   for one replicated on W data-sharded ranks; > 0 (a zeroed
+                                   descriptor is rejected) */
 } mi_factor;
 
-/* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f sum_i H_f(i)
+/* loss = g0 * sum_t sum_k terms[t][k] - entropy_scale * sum_f weight_f * sum_i H_f(i)
  * terms: per-particle log joints [K] (site-group totals, categorical totals, torch-evaluated sites);
  * g0 = -1/K_total (fp32); entropy_scale = 1/world when particles are sharded over ranks.
  * buffers: the speculative gradients of the site groups (computed for upstream g0), rescaled by

@@ -68,7 +68,7 @@ class Draw(ctypes.Structure):
         ("loc", c_vp), ("loc_stride", c_i64), ("scale", c_vp), ("scale_stride", c_i64),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
         ("particle_offset", c_i64), ("dloc", c_vp), ("dscale", c_vp),
-        ("scale_exp", c_vp), ("pad0", c_i64),
+        ("scale_exp", c_vp), ("element_offset", c_i64),
     ]
 
 
@@ -117,7 +117,7 @@ class Factor(ctypes.Structure):
         ("source", Source * MAX_SOURCES), ("draws", c_vp), ("eps", c_vp),
         ("seed", ctypes.c_uint64), ("step", ctypes.c_uint64), ("step_device", c_vp),
         ("particle_offset", c_i64), ("partial", c_vp * 2), ("partial_rows", c_i64),
-        ("dgrad", c_vp), ("saved", c_vp),
+        ("dgrad", c_vp), ("saved", c_vp), ("element_offset", c_i64), ("weight", ctypes.c_double),
     ]
 
 
@@ -200,20 +200,20 @@ _SIGNATURES = {
     "mi_mvn_tril_forward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                            c_vp]),
     "mi_normal_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
-                                         ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
-                                         c_vp]),
+                                         ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_i64, c_vp,
+                                         c_vp, c_vp]),
     "mi_normal_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
     "mi_normal_rsample_backward": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64,
                                                   ctypes.c_uint64, ctypes.c_uint64, c_vp,
-                                                  ctypes.c_uint32, c_i64, c_vp, c_vp,
+                                                  ctypes.c_uint32, c_i64, c_i64, c_vp, c_vp,
                                                   ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "mi_beta_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,
                                        ctypes.c_uint64, c_vp, ctypes.c_uint32, c_i64, c_vp, c_vp,
                                        c_vp]),
     "mi_normal_rsample_exp": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
                                              ctypes.c_uint64, ctypes.c_uint64, c_vp,
-                                             ctypes.c_uint32, c_i64, c_vp, c_vp, c_vp]),
+                                             ctypes.c_uint32, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mi_beta_rsample_exp": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
                                            ctypes.c_uint64, ctypes.c_uint64, c_vp, ctypes.c_uint32,
                                            c_i64, c_vp, c_vp, c_vp]),

@@ -13,6 +13,7 @@
 //
 // Reductions are deterministic: fixed grids, fp64 per-block partial sums, and the last block to
 // finish (device-scope counter, reset by that block) adds the partials in a fixed order.
+#include <cmath>
 #include "beta_grad.hpp"
 
 #include <algorithm>
@@ -223,7 +224,7 @@ MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int
         e = F.eps[k * n + i];
       } else {
         float q[4];
-        guide_normals(F.seed, step, F.stream_id, (uint64_t)(i >> 2),
+        guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
                       (uint64_t)(F.particle_offset + k), q);
         e = q[i & 3];
       }
@@ -298,7 +299,7 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   for (int q = 1; q < MI_MAX_FACTORS; ++q)
     if (q < P.num && bid >= P.first[q]) a = q;
   const mi_factor F = factor_at(E, pick(P.index, a));
-  const double w = -(double)u * E.entropy_scale;
+  const double w = -(double)u * E.entropy_scale * F.weight;
   const int local = bid - pick(P.first, a);
   const int gx = pick(P.gx, a), ti = pick(P.ti, a), slices = pick(P.slices, a);
   const int64_t rows_per_slice = pick(P.rows_per_slice, a);
@@ -639,10 +640,13 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
           head = nq << 2;
         }
         for (int64_t i = head + first; i < F.n; i += stride) hf += logf(sc[i * ss]);
-        h += (double)hf;
-        if (first == 0) h += 1.4189385332046727 * (double)F.n;
+        double hn = (double)hf;
+        if (first == 0) hn += 1.4189385332046727 * (double)F.n;
+        h += F.weight * hn;
       } else {
-        for (int64_t i = first; i < F.n; i += stride) h += factor_entropy(F, i);
+        double hb = 0.0;
+        for (int64_t i = first; i < F.n; i += stride) hb += factor_entropy(F, i);
+        h += F.weight * hb;
       }
     }
     share = (double)E.g0 * lp - E.entropy_scale * h;
@@ -775,8 +779,8 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_backward(const mi_elbo E,
     for (int64_t i = first; i < F.n; i += stride) {
       double d0, d1;
       entropy_grad(F, i, d0, d1);
-      write_grad(F, 0, i, w * d0);
-      write_grad(F, 1, i, w * d1);
+      write_grad(F, 0, i, w * F.weight * d0);
+      write_grad(F, 1, i, w * F.weight * d1);
     }
   }
   if (u == 1.0f) return;  // the site groups' gradients were computed for exactly this upstream
@@ -794,6 +798,9 @@ namespace {
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 bool valid_factor(const mi_factor& F) {
+  if (!(F.weight > 0.0) || !std::isfinite(F.weight) || F.element_offset < 0 ||
+      (F.element_offset & 3) != 0)
+    return false;
   if (F.n < 1 || (F.family != MI_NORMAL && F.family != MI_BETA && F.family != MI_GAMMA) ||
       F.param[1] == nullptr || ((F.family == MI_BETA || F.family == MI_GAMMA) && F.param[0] == nullptr) ||
       (F.family == MI_GAMMA && F.draw_kind != MI_DRAW_NONE))

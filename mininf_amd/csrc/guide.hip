@@ -26,8 +26,8 @@ template <bool EXP>
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
     const float* __restrict__ loc, int64_t loc_s, const float* __restrict__ scale, int64_t scale_s,
     int64_t K, int64_t N, uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev,
-    uint32_t stream_id, int64_t poff, const float* __restrict__ eps_in, float* __restrict__ z,
-    int64_t rows_per_block, float* __restrict__ scale_out) {
+    uint32_t stream_id, int64_t poff, int64_t qoff, const float* __restrict__ eps_in,
+    float* __restrict__ z, int64_t rows_per_block, float* __restrict__ scale_out) {
   if (step_dev != nullptr) step += *step_dev;
   const int64_t quad = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
   const int64_t i0 = quad * 4;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
 #pragma unroll
       for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
     } else {
-      guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+      guide_normals(seed, step, stream_id, (uint64_t)(qoff + quad), (uint64_t)(poff + k), e);
     }
     float out[4];
 #pragma unroll
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample(
 __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
     const float* __restrict__ dz, int64_t dz_sk, int64_t dz_si, int64_t K, int64_t N,
     uint64_t seed, uint64_t step, const uint64_t* __restrict__ step_dev, uint32_t stream_id,
-    int64_t poff, const float* __restrict__ eps_in, float* __restrict__ out_loc,
+    int64_t poff, int64_t qoff, const float* __restrict__ eps_in, float* __restrict__ out_loc,
     float* __restrict__ out_scale, int64_t out_stride, int64_t rows_per_block, int ti) {
   if (step_dev != nullptr) step += *step_dev;
   __shared__ float red[kGuideThreads][8];
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kGuideThreads) void k_normal_rsample_bwd(
 #pragma unroll
         for (int j = 0; j < 4; ++j) e[j] = (i0 + j < N) ? eps_in[k * N + i0 + j] : 0.0f;
       } else {
-        guide_normals(seed, step, stream_id, (uint64_t)quad, (uint64_t)(poff + k), e);
+        guide_normals(seed, step, stream_id, (uint64_t)(qoff + quad), (uint64_t)(poff + k), e);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -462,8 +462,9 @@ extern "C" {
 int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, int64_t scale_stride,
                       int64_t K, int64_t N, uint64_t seed, uint64_t step,
                       const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
-                      const float* eps, float* z, void* stream) {
-  if (loc == nullptr || scale == nullptr || z == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
+                      int64_t element_offset, const float* eps, float* z, void* stream) {
+  if (loc == nullptr || scale == nullptr || z == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu ||
+      element_offset < 0 || (element_offset & 3) != 0)
     return MI_EINVAL;
   const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
   const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(K, ceil_div(2048, gx)));
@@ -471,24 +472,24 @@ int mi_normal_rsample(const float* loc, int64_t loc_stride, const float* scale, 
   hipLaunchKernelGGL(mi::k_normal_rsample<false>, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
                      scale, scale_stride, K, N, seed, step, step_device, stream_id, particle_offset,
-                     eps, z, rows, nullptr);
+                     element_offset >> 2, eps, z, rows, nullptr);
   return to_code(hipGetLastError());
 }
 
 int mi_normal_rsample_exp(const float* loc, int64_t loc_stride, const float* u, int64_t u_stride,
                           float* scale_out, int64_t K, int64_t N, uint64_t seed, uint64_t step,
                           const uint64_t* step_device, uint32_t stream_id, int64_t particle_offset,
-                          const float* eps, float* z, void* stream) {
+                          int64_t element_offset, const float* eps, float* z, void* stream) {
   if (loc == nullptr || u == nullptr || scale_out == nullptr || z == nullptr || K < 1 || N < 1 ||
-      stream_id > 0xFFFFFFu)
+      stream_id > 0xFFFFFFu || element_offset < 0 || (element_offset & 3) != 0)
     return MI_EINVAL;
   const int64_t gx = ceil_div(N, 4 * mi::kGuideThreads);
   const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(K, ceil_div(2048, gx)));
   const int64_t rows = ceil_div(K, gy);
   hipLaunchKernelGGL(mi::k_normal_rsample<true>, dim3((unsigned)gx, (unsigned)ceil_div(K, rows)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), loc, loc_stride,
-                     u, u_stride, K, N, seed, step, step_device, stream_id, particle_offset, eps, z,
-                     rows, scale_out);
+                     u, u_stride, K, N, seed, step, step_device, stream_id, particle_offset,
+                     element_offset >> 2, eps, z, rows, scale_out);
   return to_code(hipGetLastError());
 }
 
@@ -502,10 +503,12 @@ int mi_normal_rsample_backward_workspace_bytes(int64_t K, int64_t N, size_t* byt
 int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_stride_i,
                                int64_t K, int64_t N, uint64_t seed, uint64_t step,
                                const uint64_t* step_device, uint32_t stream_id,
-                               int64_t particle_offset, const float* eps,
+                               int64_t particle_offset, int64_t element_offset, const float* eps,
                                void* workspace, size_t workspace_bytes, float* dloc, float* dscale,
                                void* stream) {
-  if (dz == nullptr || dloc == nullptr || dscale == nullptr || K < 1 || N < 1) return MI_EINVAL;
+  if (dz == nullptr || dloc == nullptr || dscale == nullptr || K < 1 || N < 1 ||
+      element_offset < 0 || (element_offset & 3) != 0)
+    return MI_EINVAL;
   size_t need = 0;
   mi_normal_rsample_backward_workspace_bytes(K, N, &need);
   if (need > 0 && (workspace == nullptr || workspace_bytes < need)) return MI_EWORKSPACE;
@@ -520,8 +523,8 @@ int mi_normal_rsample_backward(const float* dz, int64_t dz_stride_k, int64_t dz_
   }
   hipLaunchKernelGGL(mi::k_normal_rsample_bwd, dim3((unsigned)gx, (unsigned)gy),
                      dim3(mi::kGuideThreads), 0, s, dz, dz_stride_k, dz_stride_i, K, N, seed, step,
-                     step_device, stream_id, particle_offset, eps, out_loc, out_scale, N, rows,
-                     geo.ti);
+                     step_device, stream_id, particle_offset, element_offset >> 2, eps, out_loc,
+                     out_scale, N, rows, geo.ti);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || gy == 1) return to_code(e);
   const unsigned g = (unsigned)ceil_div(N, mi::kGuideThreads);

@@ -468,7 +468,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
       << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
-         "+ qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
+         "+ dqoff + qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
     o << in << "  float d" << draw << "[" << E << "];\n#pragma unroll\n" << in
       << "  for (int e = 0; e < " << E << "; ++e) d" << draw << "[e] = fmaf(ep[e], dws[e], dwl[e]);\n";
     for (int op = 0; op < g.num_operands; ++op)
@@ -528,6 +528,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
          "*G.draw.step_device : 0ull);\n";
     o << "  const unsigned dstream = G.draw.stream_id;\n";
     o << "  const long dpoff = G.draw.particle_offset;\n";
+    o << "  const long dqoff = G.draw.element_offset >> 2;   // data-sharded draws\n";
     if (plan.block_rows) {
       // every wave runs the loop (block barriers at the flushes): a wave past the last segment
       // re-reads the last one with all of its elements masked off

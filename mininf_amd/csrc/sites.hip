@@ -1015,6 +1015,7 @@ bool validate_group(const mi_group* g) {
   const int draw = g->draw.operand - 1;
   if (draw >= g->num_operands || draw < -1) return false;
   if (draw >= 0 && (g->draw.loc == nullptr || g->draw.scale == nullptr ||
+                    g->draw.element_offset < 0 || (g->draw.element_offset & 3) != 0 ||
                     (g->compute_grads && !(g->options & MI_GROUP_DRAW_PARTIALS) &&
                      (g->draw.dloc == nullptr || g->draw.dscale == nullptr))))
     return false;

@@ -11,10 +11,62 @@ optimizer step, so the guide parameters stay in sync without a broadcast.
 """
 from __future__ import annotations
 
-from typing import Iterable, Optional
+import dataclasses
+from typing import Iterable, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+@dataclasses.dataclass(frozen=True)
+class DataShard:
+    """
+    Data sharding of one ELBO over the ranks of a process group (the C5 row):
+    instead of splitting the particles, rank r owns the elements ``[start, stop)`` of the data
+    axis -- its slice of the observations and of every guide factor over them -- for ALL
+    particles. The rank's model and guide are written for its slice (``stop - start`` elements);
+    the factors and sites named in ``shared`` (global latents such as the hierarchical mean) are
+    replicated: every rank draws them identically and counts their log density and entropy with
+    weight 1/W, so the ranks' losses sum to the full ELBO. Only the shared parameters' gradients
+    (and the loss) need the all-reduce; each rank's optimizer updates its own slice.
+
+    The guide generator keys a sharded factor's draws by the GLOBAL element index
+    (``mi_draw.element_offset``), so the union of the slices draws exactly what one process drawing
+    every element would: ``start`` is a multiple of 4 (one Philox block per element quad).
+    """
+    start: int
+    stop: int
+    shared: Tuple[str, ...] = ()
+
+    def __post_init__(self) -> None:
+        if self.start < 0 or self.stop < self.start or (self.start % 4 and self.stop > self.start):
+            raise ValueError(f"invalid data shard [{self.start}, {self.stop}): start must be a "
+                             "non-negative multiple of 4 and stop >= start")
+        object.__setattr__(self, "shared", tuple(self.shared))
+
+    @property
+    def size(self) -> int:
+        return self.stop - self.start
+
+    @property
+    def slice(self) -> slice:
+        return slice(self.start, self.stop)
+
+
+def element_shard(n: int, group=None, shared: Sequence[str] = (), *, world: Optional[int] = None,
+                  rank: Optional[int] = None) -> DataShard:
+    """
+    This rank's :class:`DataShard` of ``n`` elements: contiguous slices of ``ceil(n / W)``
+    elements rounded up to a multiple of 4 (the last rank takes the remainder). ``world`` and
+    ``rank`` default to the group's.
+    """
+    if world is None:
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if rank is None:
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+    per = -(-n // world)
+    per = -(-per // 4) * 4
+    return DataShard(min(n, rank * per), min(n, (rank + 1) * per), tuple(shared))
 
 
 def all_reduce_gradients(parameters: Iterable[torch.nn.Parameter], group=None,
@@ -63,9 +115,12 @@ class GradientBucket:
         parameters: The parameters whose gradients to reduce (all of them must receive one).
         group: Process group (default: the world).
         with_loss: Reserve the loss element.
+        communicator: A :class:`mininf_amd.rccl.Communicator` to run the all-reduce on (RCCL
+            called directly: capturable into a hipGraph); default: ``torch.distributed`` over
+            ``group``.
     """
     def __init__(self, parameters: Iterable[torch.nn.Parameter], group=None,
-                 with_loss: bool = False) -> None:
+                 with_loss: bool = False, communicator=None) -> None:
         self.params = [p for p in parameters if p.requires_grad]
         if not self.params:
             raise ValueError("no parameters to reduce")
@@ -74,6 +129,7 @@ class GradientBucket:
             raise ValueError(f"parameters of one dtype expected, got {dtypes}")
         self.group = group
         self.with_loss = with_loss
+        self.communicator = communicator
         self.flat = torch.zeros(sum(p.numel() for p in self.params) + int(with_loss),
                                 dtype=dtypes.pop(), device=self.params[0].device)
         self.views = []
@@ -103,7 +159,10 @@ class GradientBucket:
 
     def all_reduce(self) -> None:
         """Sum the flat buffer over the ranks (in place)."""
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        if self.communicator is not None:
+            self.communicator.all_reduce(self.flat)
+        else:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
 
     def bind(self) -> None:
         """Make every ``param.grad`` the view of its slice of the flat buffer."""

@@ -296,6 +296,7 @@ class _GroupLauncher:
                 dw.seed, dw.step = guide._philox_key(d.cfg)
                 dw.step_device = nat.ptr(d.cfg.step_device)
                 dw.particle_offset = d.cfg.particle_offset
+                dw.element_offset = d.cfg.element_offset
                 if mode == nat.GRAD_DENSE and self.draw_partials:
                     group.options |= nat.GROUP_DRAW_PARTIALS
                 elif mode == nat.GRAD_DENSE:
@@ -889,6 +890,7 @@ class EntropyFactor:
     tensor: torch.Tensor
     name: Optional[str] = None
     distribution: Optional[object] = None
+    weight: float = 1.0   # mi_factor.weight: 1/W for a factor replicated on W data-sharded ranks
 
 
 @dataclasses.dataclass(eq=False)
@@ -1160,6 +1162,7 @@ class _ElboPlan:
         for j, f in enumerate(self.factors):
             d = E.factors[j]
             d.family, d.n = f.family, f.n
+            d.weight = f.weight
             base = f.tensor.data_ptr()
             if f.family in (nat.BETA, nat.GAMMA):
                 d.param[0], d.param[1] = base, base + 4
@@ -1210,6 +1213,7 @@ class _ElboPlan:
                 d.step_device = nat.ptr(guide.backward_step(cfg))   # read by the ELBO backward
                 d.stream_id = cfg.stream_id
                 d.particle_offset = cfg.particle_offset
+                d.element_offset = cfg.element_offset
             d.num_sources = len(plan.uses)
             for s, (kind, li, oi) in enumerate(plan.uses):
                 src = d.source[s]

@@ -152,8 +152,12 @@ def _abandon_capture(cuda_graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Str
     except Exception:   # invalidated: torch raised before ending the capture
         pass
     was = ctypes.c_int(0)
-    nat.check(nat.lib().mi_capture_abandon(stream.cuda_stream, ctypes.byref(was)),
-              "mi_capture_abandon")
+    code = nat.lib().mi_capture_abandon(stream.cuda_stream, ctypes.byref(was))
+    if code != 0:   # reported beside the original error, which the caller raises
+        import warnings
+        warnings.warn(f"mi_capture_abandon could not end the failed capture (hipError_t {code}); "
+                      "later GPU work in this process may fail", RuntimeWarning)
+        return
     torch.cuda.synchronize()
 
 

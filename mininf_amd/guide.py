@@ -36,6 +36,8 @@ class DrawConfig:
     # The word holding this evaluation's step once the forward has advanced `step_device`
     # (mi_elbo.step_snapshot): read by every kernel that runs after the ELBO forward.
     step_snapshot: Optional[torch.Tensor] = None
+    # global index of element 0 (data-sharded factors, mininf_amd.distributed.DataShard)
+    element_offset: int = 0
 
 
 def backward_step(cfg: DrawConfig) -> Optional[torch.Tensor]:
@@ -84,15 +86,15 @@ class _NormalRsampleFn(torch.autograd.Function):
             pending, u_ptr = source
             nat.check(nat.lib().mi_normal_rsample_exp(
                 loc.data_ptr(), loc_s, u_ptr, scale_s, scale.data_ptr(), K, N, seed, step,
-                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
-                z.data_ptr(), nat.stream_handle(loc.device)), "mi_normal_rsample_exp")
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
+                nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)), "mi_normal_rsample_exp")
             pending.filled = True
         else:
             fill_exp(scale)
             nat.check(nat.lib().mi_normal_rsample(
                 loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step,
-                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, nat.ptr(eps),
-                z.data_ptr(), nat.stream_handle(loc.device)),
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
+                nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)),
                 "mi_normal_rsample")
         ctx.cfg = cfg
         ctx.N = N
@@ -116,8 +118,8 @@ class _NormalRsampleFn(torch.autograd.Function):
         seed, step = _philox_key(cfg)
         nat.check(lib.mi_normal_rsample_backward(
             dz.data_ptr(), dz.stride(0), dz.stride(1), K, N, seed, step,
-            nat.ptr(backward_step(cfg)), cfg.stream_id, cfg.particle_offset, nat.ptr(cfg.noise),
-            workspace.data_ptr(), size.value,
+            nat.ptr(backward_step(cfg)), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
+            nat.ptr(cfg.noise), workspace.data_ptr(), size.value,
             dloc.data_ptr(), deps_scale.data_ptr(), nat.stream_handle(device)),
             "mi_normal_rsample_backward")
         # dz/dscale = eps: the kernel returns sum_k dz * eps directly.
@@ -530,6 +532,12 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
     K reparameterised draws of one guide factor: shape [K, *batch_shape, *event_shape].
     """
     cls = type(distribution)
+    if cfg.element_offset and cls is not Normal:
+        raise nat.NativeError(f"a data-sharded guide factor must be a Normal (got {cls.__name__}): "
+                              "only the Normal sampler draws element slices of a global draw")
+    if cfg.element_offset % 4:
+        raise ValueError(f"element offset {cfg.element_offset} of a data-sharded factor is not a "
+                         "multiple of 4 (mininf_amd.distributed.DataShard aligns slices)")
     if cls is Normal:
         shape = distribution.batch_shape
         N = max(1, int(shape.numel()))
@@ -580,10 +588,12 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
              particle_offset: int, noise: Optional[Dict[str, torch.Tensor]] = None,
              step_device: Optional[torch.Tensor] = None,
              lazy: bool = False,
-             step_snapshot: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+             step_snapshot: Optional[torch.Tensor] = None,
+             element_offsets: Optional[Dict[str, int]] = None) -> Dict[str, torch.Tensor]:
     """
     Draw every factor of a factorised guide (dict order = stream id order). With ``lazy``, large
     Normal factors become :class:`LazyDraw` placeholders evaluated inside the site kernels.
+    ``element_offsets``: global index of element 0 of data-sharded factors (multiples of 4).
     """
     _LAZY.clear()
     _DRAWN.clear()
@@ -592,6 +602,7 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
                          particle_offset=particle_offset,
                          noise=None if noise is None else noise.get(name),
-                         step_device=step_device, step_snapshot=step_snapshot)
+                         step_device=step_device, step_snapshot=step_snapshot,
+                         element_offset=(element_offsets or {}).get(name, 0))
         samples[name] = draw(factor, cfg, lazy)
     return samples

@@ -297,6 +297,11 @@ class EvidenceLowerBoundLoss(nn.Module):
         process_group: ``torch.distributed`` group to shard the particles over (one rank per GPU);
             each rank returns its share of the loss and gradients, combine them with
             :func:`mininf_amd.distributed.all_reduce_gradients`.
+        data_shard: Shard the data axis instead of the particles
+            (:class:`mininf_amd.distributed.DataShard`): every rank evaluates all
+            ``num_particles`` particles on its slice of the elements; the model and guide it is
+            called with are the rank's slice. Shared factors and sites count 1/W per rank, the
+            sharded factors draw their slice of the global draw.
 
     Example:
 
@@ -311,7 +316,7 @@ class EvidenceLowerBoundLoss(nn.Module):
         tensor(..., device='cuda:0')
     """
     def __init__(self, num_particles: int = 1, *, seed: Optional[int] = None,
-                 validate: bool = True, process_group=None) -> None:
+                 validate: bool = True, process_group=None, data_shard=None) -> None:
         super().__init__()
         if num_particles < 1:
             raise ValueError("num_particles must be positive")
@@ -319,6 +324,9 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.seed = int(seed if seed is not None else torch.initial_seed()) & ((1 << 64) - 1)
         self.validate = validate
         self.process_group = process_group
+        self.data_shard = data_shard
+        if data_shard is not None and process_group is None:
+            raise ValueError("data_shard needs the process_group it shards over")
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
         self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
         self._mirror: Optional[torch.Tensor] = None   # their pinned host copy
@@ -335,11 +343,20 @@ class EvidenceLowerBoundLoss(nn.Module):
         import torch.distributed as dist
         world = dist.get_world_size(self.process_group)
         rank = dist.get_rank(self.process_group)
+        if self.data_shard is not None:   # every rank holds every particle
+            return world, rank, self.num_particles, 0
         if self.num_particles % world:
             raise ValueError(f"num_particles={self.num_particles} is not divisible by the world "
                              f"size {world}")
         local = self.num_particles // world
         return world, rank, local, rank * local
+
+    def _element_offsets(self, approximation) -> Optional[Dict[str, int]]:
+        """Global element offsets of the data-sharded guide factors (None: no data sharding)."""
+        if self.data_shard is None:
+            return None
+        return {name: self.data_shard.start for name in approximation
+                if name not in self.data_shard.shared}
 
     def forward(self, model: Callable,
                 approximation: torch.distributions.Distribution | DistributionDict,
@@ -347,6 +364,8 @@ class EvidenceLowerBoundLoss(nn.Module):
         """"""
         if isinstance(approximation, Dict):
             approximation = FactorizedDistribution(approximation)
+        if self.data_shard is not None and not isinstance(approximation, dict):
+            raise TypeError("data sharding needs a factorised (dictionary) guide")
         world, _, K, offset = self._shard()
         if isinstance(approximation, dict):
             device = _guide_device(approximation)
@@ -383,14 +402,17 @@ class EvidenceLowerBoundLoss(nn.Module):
             # Large Normal factors are drawn lazily: the site kernels compute them in registers
             # (mi_draw). If the model uses a draw in any other operation, the trace is repeated
             # with real draws (same counter, same values).
+            offsets = self._element_offsets(approximation)
             samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
-                                     step_device=step, lazy=True, step_snapshot=snapshot)
+                                     step_device=step, lazy=True, step_snapshot=snapshot,
+                                     element_offsets=offsets)
             try:
                 trace = particles.trace_particles(model, samples, K, validate=self.validate)
             except linear.NeedsDraws:
                 guide.release_lazy()
                 samples = guide.draw_all(approximation, K, self.seed, 0, offset, _noise,
-                                         step_device=step, step_snapshot=snapshot)
+                                         step_device=step, step_snapshot=snapshot,
+                                         element_offsets=offsets)
                 trace = particles.trace_particles(model, samples, K, validate=self.validate)
         else:
             samples = approximation.rsample(torch.Size([K]))
@@ -402,11 +424,25 @@ class EvidenceLowerBoundLoss(nn.Module):
         g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
         device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)),
                       torch.device("cuda", torch.cuda.current_device()))
+        shared = set(self.data_shard.shared) if self.data_shard is not None else None
+        if shared is not None:
+            # data sharding: replicated sites count 1/W on every rank (the ranks' sum is the
+            # full log joint); the sharded sites' slices add up by themselves
+            for site in trace.sites:
+                if site.name in shared:
+                    site.scale /= world
+            trace.fallback = [(name, value / world if name in shared else value)
+                              for name, value in trace.fallback]
         if isinstance(approximation, dict):
             # Fused path: site kernels, guide entropy and the reduction in one autograd node.
             factors, rest = engine.entropy_factors(approximation)
+            entropy_scale = 1.0 / world
+            if shared is not None:
+                entropy_scale = 1.0
+                for f in factors:
+                    f.weight = 1.0 / world if f.name in shared else 1.0
             try:
-                loss, joint = engine.elbo(trace, g0, device, factors, 1.0 / world, samples,
+                loss, joint = engine.elbo(trace, g0, device, factors, entropy_scale, samples,
                                           flags=flags, step_words=step_words, mirror=mirror)
                 joint.sticky = sticky and joint.flags is not None and not joint.checks and \
                     joint.flags.data_ptr() == flags.data_ptr()
@@ -415,8 +451,11 @@ class EvidenceLowerBoundLoss(nn.Module):
                 # would keep this step's autograd graph (and its AccumulateGrad streams) alive.
                 guide.release_lazy()
             if rest:
-                extra = cast(torch.Tensor, sum(f.entropy().sum() for f in rest))
-                loss = loss - (extra / world if world > 1 else extra)
+                names = {id(f): name for name, f in approximation.items()}
+                extra = cast(torch.Tensor, sum(
+                    f.entropy().sum() / (world if shared is None or names[id(f)] in shared else 1)
+                    for f in rest))
+                loss = loss - extra
             if loss.is_cuda and loss.dim() == 0 and type(loss) is torch.Tensor:
                 loss.__class__ = _Loss   # the same tensor object and autograd node
         else:

@@ -607,6 +607,9 @@ class BroadcastTracer(ParticleTracer):
         sample_shape = _normalize_shape(sample_shape)
         value = state.get(name)
         if value is None:
+            if self.index is not None:
+                # constants such as Beta(2.0, 5.0)'s are host tensors: draw on the device
+                distribution = _on_device(distribution, self.index.device)
             if self.index is not None and predictive.supported(distribution):
                 # the HIP samplers, keyed by (seed, this draw's index, sample, element)
                 value = predictive.draw(distribution, sample_shape, self.index, self.seed,

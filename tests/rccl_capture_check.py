@@ -4,8 +4,9 @@ ELBO forward and backward, packing the gradients and the loss share into the fla
 RCCL all-reduce, binding the reduced gradients and the HIP Adam -- captured as ONE hipGraph with
 several steps per replay (bench.py's N > 1 path over RCCL), against the same steps run eagerly.
 
-A one-rank ``nccl`` process group (RCCL) on the box's single GPU: the collective is a real RCCL
-call inside the capture. The model is the reference's minibatch regression
+A one-rank ``nccl`` process group bootstraps a communicator of our own (mininf_amd.rccl: RCCL
+called directly) on the box's single GPU: the collective is a real ncclAllReduce inside the
+capture. The model is the reference's minibatch regression
 (examples/minibatch.md:24-33) on a device-resident loader, so every replay draws a new batch and
 new particles. Prints one JSON line.
 """
@@ -24,13 +25,14 @@ import mininf_amd as mi  # noqa: E402
 import mininf_amd.optim  # noqa: E402
 from mininf_amd.distributed import GradientBucket  # noqa: E402
 from mininf_amd.graph import StepGraph  # noqa: E402
+from mininf_amd.rccl import Communicator  # noqa: E402
 from torch.distributions import Normal  # noqa: E402
 
 N_ROWS, P, BATCH, K = 16384, 8, 2048, 32
 WARMUP, REPEAT = 2, 4
 
 
-def setup(device, group):
+def setup(device, group, comm):
     gen = torch.Generator().manual_seed(0)
     X = torch.randn(N_ROWS, P, generator=gen)
     y = X @ torch.randn(P, generator=gen) + torch.randn(N_ROWS, generator=gen)
@@ -48,7 +50,7 @@ def setup(device, group):
                                             scale=torch.ones(P)).to(device)
     optimizer = mininf_amd.optim.Adam(guide.parameters(), lr=0.01)
     loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=1, process_group=group)
-    bucket = GradientBucket(guide.parameters(), group, with_loss=True)
+    bucket = GradientBucket(guide.parameters(), group, with_loss=True, communicator=comm)
 
     def step():
         optimizer.zero_grad(set_to_none=True)
@@ -72,11 +74,12 @@ def main():
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=device)
     group = dist.group.WORLD
+    comm = Communicator(group, device)
     try:
-        eager_step, eager_guide = setup(device, group)
+        eager_step, eager_guide = setup(device, group, comm)
         eager = [float(eager_step()) for _ in range(WARMUP + 2 * REPEAT)]
 
-        graph_body, graph_guide = setup(device, group)
+        graph_body, graph_guide = setup(device, group, comm)
         captured = StepGraph(graph_body, warmup=WARMUP, repeat=REPEAT,
                              capture_error_mode="thread_local")
         losses = []
@@ -92,6 +95,7 @@ def main():
         print(json.dumps({"graph_losses": losses, "eager_losses": want,
                           "param_max_abs_diff": param_diff, "eager_all": eager}), flush=True)
     finally:
+        comm.close()
         dist.destroy_process_group()
 
 

@@ -5,6 +5,8 @@ after several steps, with weight decay / maximize, more than one launch's worth 
 spread over many blocks (two-level completion counts), grads that skip a parameter, and inside a
 captured graph.
 """
+import copy
+
 import pytest
 import torch
 
@@ -90,9 +92,12 @@ def test_loads_a_torch_adam_state_dict(device, source):
             a.copy_(s)
             b.copy_(s)
     opt, opt_ref = Adam(ours, lr=0.01), torch.optim.Adam(ref, lr=0.01, fused=True)
-    opt.load_state_dict(saved)
+    # independent copies: Optimizer.load_state_dict keeps a loaded tensor that already has the
+    # parameter's device and dtype (the two optimizers would share their moments)
+    opt.load_state_dict(copy.deepcopy(saved))
     # the reference continues as fused Adam (its groups' `fused` comes from the loaded dict)
-    opt_ref.load_state_dict({"state": saved["state"],
+    ref_saved = copy.deepcopy(saved)
+    opt_ref.load_state_dict({"state": ref_saved["state"],
                              "param_groups": [dict(g, fused=True) for g in saved["param_groups"]]})
     for g in grads[3:]:
         for a, b, gi in zip(ours, ref, g):

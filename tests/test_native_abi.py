@@ -52,8 +52,12 @@ def test_invalid_arguments_are_rejected():
     size = ctypes.c_size_t()
     group = nat.Group()
     assert lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)) == -1
-    assert lib.mi_normal_rsample(None, 0, None, 0, 1, 1, 0, 0, None, 0, 0, None, None,
+    assert lib.mi_normal_rsample(None, 0, None, 0, 1, 1, 0, 0, None, 0, 0, 0, None, None,
                                  None) == -1
+    # an element offset that is not a multiple of 4 (one Philox block per element quad)
+    buf = ctypes.c_float(0.0)
+    assert lib.mi_normal_rsample(ctypes.byref(buf), 0, ctypes.byref(buf), 0, 1, 1, 0, 0, None, 0,
+                                 0, 6, None, ctypes.byref(buf), None) == -1
     assert lib.mi_categorical_workspace_bytes(0, 1, ctypes.byref(size)) == -1
 
 
