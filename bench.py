@@ -151,33 +151,42 @@ def workload(name, device, world, rank):
             flop_note=f"{4 * p} FLOP/eval (2 x {p} FMA) x K x n",
             data=f"synthetic: X ~ N(0,1)[{n_total},{p}], y = X theta* + N(0,1) (seed 0)")
     if name == "c5":
-        n, k_local = 1_000_000, 128
+        n = 1_000_000
         mu_true = torch.randn((), generator=gen)
         z_true = mu_true + torch.randn(n, generator=gen)
-        y = (z_true + 0.5 * torch.randn(n, generator=gen)).to(device)
-        b = (torch.rand(n, generator=gen) < torch.sigmoid(z_true)).float().to(device)
-        mask = (torch.rand(n, generator=gen) > 0.2).to(device)
+        y = z_true + 0.5 * torch.randn(n, generator=gen)
+        b = (torch.rand(n, generator=gen) < torch.sigmoid(z_true)).float()
+        mask = torch.rand(n, generator=gen) > 0.2
+        shard = data_shard(n, world, rank) if name == "c5" and DATA_SHARD else None
+        if shard is None:   # particle sharding: every rank holds every element, K / W particles
+            k_local, sl, n_loc, layout = 128, slice(None), n, "particle-sharded"
+        else:   # data sharding: the rank's element slice, all particles (DataShard)
+            k_local, sl, n_loc = 1024, shard.slice, shard.size
+            layout = (f"data-sharded: elements [{shard.start}, {shard.stop}) of {n} "
+                      f"(rank {DATA_SHARD_RANK if world == 1 else rank} of {shard.world})")
+        y, b, mask = y[sl].to(device), b[sl].to(device), mask[sl].to(device)
         ym = torch.masked.as_masked_tensor(y, mask)
         bm = torch.masked.as_masked_tensor(b, mask)
 
         def model():
             mu = mininf_amd.sample("mu", Normal(0, 1))
-            z = mininf_amd.sample("z", Normal(mu, 1), sample_shape=[n])
+            z = mininf_amd.sample("z", Normal(mu, 1), sample_shape=[n_loc])
             mininf_amd.sample("y", Normal(z, 0.5))
             mininf_amd.sample("b", Bernoulli(logits=z))
 
         guide = mininf_amd.nn.ParameterizedFactorizedDistribution(
             mu=mininf_amd.nn.ParameterizedDistribution(Normal, loc=0.0, scale=1.0),
-            z=mininf_amd.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n),
-                                                      scale=torch.ones(n)),
+            z=mininf_amd.nn.ParameterizedDistribution(Normal, loc=torch.zeros(n_loc),
+                                                      scale=torch.ones(n_loc)),
         ).to(device)
         conditioned = mininf_amd.condition(model, y=ym, b=bm)
         observed = int(mask.sum())
         return dict(
-            desc=f"C5 masked hierarchical model, n={n}, {k_local} particles/GPU",
-            k_local=k_local, n=n, module=guide, guide=lambda: guide(),
-            conditioned=lambda: conditioned,
-            evals=k_local * (1 + n + 2 * observed), lr=0.01, dominant_N=n, bound="valu",
+            desc=f"C5 masked hierarchical model, n={n}, {k_local} particles/GPU, {layout}",
+            k_local=k_local, n=n_loc, module=guide, guide=lambda: guide(),
+            conditioned=lambda: conditioned, shard=shard,
+            reduce_params=list(guide["mu"].parameters()) if shard is not None else None,
+            evals=k_local * (1 + n_loc + 2 * observed), lr=0.01, dominant_N=n_loc, bound="valu",
             flops_per_eval=37.0, bytes_per_eval=None, observed=observed,
             kernel=("mi_site_program (fused z / y / b site group with the z ~ q(z) draw computed "
                     "in registers: Philox + Box-Muller, three log densities, dloc / dscale "
@@ -187,6 +196,21 @@ def workload(name, device, world, rank):
                        "accumulation 6; Philox integer rounds not counted"),
             data=f"synthetic: y ~ N(z, 0.5), b ~ Bernoulli(logits=z), 20% masked (seed 0)")
     raise SystemExit(f"unknown config {name}")
+
+
+# C5 layout (--shard): "particles" (default: every rank all elements, K / W particles) or "data"
+# (DataShard: every rank all K particles on its element slice; --shard-world W with one process
+# measures rank --shard-rank's slice of a W-rank run on one GPU, without the all-reduce)
+DATA_SHARD = False
+DATA_SHARD_WORLD = 0
+DATA_SHARD_RANK = 0
+
+
+def data_shard(n, world, rank):
+    from mininf_amd.distributed import element_shard
+    if world == 1 and DATA_SHARD_WORLD > 1:
+        return element_shard(n, shared=("mu",), world=DATA_SHARD_WORLD, rank=DATA_SHARD_RANK)
+    return element_shard(n, shared=("mu",), world=world, rank=rank)
 
 
 def measured_traffic(name):
@@ -303,9 +327,10 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         optimizer = torch.optim.Adam(module.parameters(), lr=w["lr"], capturable=True, fused=True)
     else:   # the same Adam in one HIP launch (mininf_amd.optim, bit-identical to torch's fused)
         optimizer = mininf_amd.optim.Adam(module.parameters(), lr=w["lr"])
+    shard = w.get("shard")
     loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(
-        num_particles=w["k_local"] * world, seed=1, validate=not args.no_validate,
-        process_group=group)
+        num_particles=w["k_local"] * (world if shard is None else 1), seed=1,
+        validate=not args.no_validate, process_group=group, data_shard=shard)
     timer = EventTimer()
     engine.KERNEL_TIMER = timer
 
@@ -319,7 +344,9 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     # over RCCL the all-reduce runs on a communicator of our own (mininf_amd.rccl: RCCL called
     # directly, no process-group watchdog polling events of the captured collective)
     comm = rccl.Communicator(group, device) if collective_in_graph else None
-    bucket = GradientBucket(module.parameters(), group, with_loss=True,
+    # data sharding reduces only the replicated (shared) parameters' gradients; every rank
+    # updates its own slice of the rest
+    bucket = GradientBucket(w.get("reduce_params") or module.parameters(), group, with_loss=True,
                             communicator=comm) if sharded else None
 
     def forward_backward():
@@ -468,8 +495,10 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         "warmup": warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": w["data"],
         "config": {"workload": w["desc"], "particles_per_gpu": w["k_local"],
-                   "global_particles": w["k_local"] * world, "evals_per_step_per_gpu": w["evals"],
-                   "parallelism": f"particle-sharded x{world}" + (
+                   "global_particles": w["k_local"] * (world if shard is None else 1),
+                   "evals_per_step_per_gpu": w["evals"],
+                   "parallelism": (f"particle-sharded x{world}" if shard is None else
+                                   f"data-sharded x{shard.world} (element slices)") + (
                        (" + RCCL grad all-reduce" if args.dist_backend == "nccl" else
                         f" + {args.dist_backend} grad all-reduce") if sharded else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
@@ -511,6 +540,13 @@ def main():
                          "torch.optim.Adam(fused=True, capturable=True)")
     ap.add_argument("--particles-per-gpu", type=int, default=0,
                     help="override the config's particles per GPU (0: the config's own)")
+    ap.add_argument("--shard", choices=("particles", "data"), default="particles",
+                    help="C5 layout over ranks: particles (K / W each, default) or data (element "
+                         "slices, all K particles each: mininf_amd.distributed.DataShard)")
+    ap.add_argument("--shard-world", type=int, default=0,
+                    help="with --shard data on ONE process: measure the slice of a run over this "
+                         "many ranks (rank --shard-rank), without the all-reduce")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--process-group", action="store_true",
                     help="run the sharded step (process group, gradient bucket, all-reduce) even "
                          "at N = 1: measures the N > 1 step's own overhead on one GPU")
@@ -532,6 +568,9 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
     if args.check_launch:
         raise SystemExit(check_launch(args, world, rank))
+    global DATA_SHARD, DATA_SHARD_WORLD, DATA_SHARD_RANK
+    DATA_SHARD = args.shard == "data"
+    DATA_SHARD_WORLD, DATA_SHARD_RANK = args.shard_world, args.shard_rank
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     group = None

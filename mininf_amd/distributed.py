@@ -37,6 +37,7 @@ class DataShard:
     start: int
     stop: int
     shared: Tuple[str, ...] = ()
+    world: Optional[int] = None   # ranks sharing the data axis (default: the group's size)
 
     def __post_init__(self) -> None:
         if self.start < 0 or self.stop < self.start or (self.start % 4 and self.stop > self.start):
@@ -66,7 +67,7 @@ def element_shard(n: int, group=None, shared: Sequence[str] = (), *, world: Opti
         rank = dist.get_rank(group) if dist.is_initialized() else 0
     per = -(-n // world)
     per = -(-per // 4) * 4
-    return DataShard(min(n, rank * per), min(n, (rank + 1) * per), tuple(shared))
+    return DataShard(min(n, rank * per), min(n, (rank + 1) * per), tuple(shared), world)
 
 
 def all_reduce_gradients(parameters: Iterable[torch.nn.Parameter], group=None,

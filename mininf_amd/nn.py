@@ -325,8 +325,8 @@ class EvidenceLowerBoundLoss(nn.Module):
         self.validate = validate
         self.process_group = process_group
         self.data_shard = data_shard
-        if data_shard is not None and process_group is None:
-            raise ValueError("data_shard needs the process_group it shards over")
+        if data_shard is not None and process_group is None and data_shard.world is None:
+            raise ValueError("data_shard needs the process_group it shards over (or its world)")
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
         self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
         self._mirror: Optional[torch.Tensor] = None   # their pinned host copy
@@ -338,13 +338,16 @@ class EvidenceLowerBoundLoss(nn.Module):
         """
         (world size, rank, local K, particle offset) of this rank.
         """
+        if self.data_shard is not None:   # every rank holds every particle
+            import torch.distributed as dist
+            world = self.data_shard.world or dist.get_world_size(self.process_group)
+            rank = dist.get_rank(self.process_group) if self.process_group is not None else 0
+            return world, rank, self.num_particles, 0
         if self.process_group is None:
             return 1, 0, self.num_particles, 0
         import torch.distributed as dist
         world = dist.get_world_size(self.process_group)
         rank = dist.get_rank(self.process_group)
-        if self.data_shard is not None:   # every rank holds every particle
-            return world, rank, self.num_particles, 0
         if self.num_particles % world:
             raise ValueError(f"num_particles={self.num_particles} is not divisible by the world "
                              f"size {world}")
