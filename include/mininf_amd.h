@@ -281,6 +281,17 @@ int mi_categorical_workspace_bytes(int64_t K, int64_t N, size_t* bytes);
  *   d/dvalue = -u, d/dloc = u, d/dL = tril(u w^T) - diag(1 / L_ii).
  * n <= MI_MVN_MAX_N. */
 #define MI_MVN_MAX_N 1024
+
+/* Cholesky factorisation A = L L^T (replaces torch.linalg.cholesky / cholesky_ex, which
+ * MultivariateNormal(loc, covariance_matrix) calls in its constructor, multivariate_normal.py:193,
+ * for the GP site of examples/missing-observations.md:40-42): batch row-major [n, n] matrices,
+ * float32 or float64 in and out (a_bytes / l_bytes = 4 or 8; n > 80 needs a float64 output),
+ * float64 arithmetic. Only the lower triangle of A is read; L's upper triangle is written as 0.
+ * info[b] (optional) = 0 or j + 1 for the first non-positive pivot (cholesky_ex's convention).
+ * Runs on the caller's stream with no host synchronisation, so a captured graph can hold it
+ * (rocSOLVER's potrf cannot be captured on this stack). n <= MI_MVN_MAX_N. */
+int mi_cholesky(const void* A, int32_t a_bytes, int64_t batch, int64_t n, void* L,
+                int32_t l_bytes, int32_t* info, void* stream);
 int mi_mvn_tril_forward(const double* value, const double* loc, const double* scale_tril,
                         int64_t batch, int64_t n, double* log_prob, double* w, double* u,
                         void* stream);

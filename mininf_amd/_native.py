@@ -197,6 +197,8 @@ _SIGNATURES = {
                                               c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_double,
                                               ctypes.c_float, c_vp, c_vp, ctypes.c_size_t, c_vp,
                                               c_vp, c_vp]),
+    "mi_cholesky": (ctypes.c_int, [c_vp, ctypes.c_int32, c_i64, c_i64, c_vp, ctypes.c_int32,
+                                   c_vp, c_vp]),
     "mi_mvn_tril_forward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                            c_vp]),
     "mi_normal_rsample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, ctypes.c_uint64,

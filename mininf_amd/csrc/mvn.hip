@@ -78,9 +78,130 @@ __global__ __launch_bounds__(kMvnThreads) void k_mvn_tril(const double* __restri
   for (int j = lane; j < n; j += kMvnThreads) u_out[b * n + j] = r[j];
 }
 
+// Cholesky factorisation A = L L^T of a batch of symmetric positive-definite matrices, float64
+// arithmetic (inputs and outputs float32 or float64): one 256-thread workgroup per matrix,
+// right-looking (column j: its diagonal, the column below it scaled, then the trailing lower
+// triangle updated by the threads together). The working triangle lives in LDS for
+// n <= kMvnLdsMaxN, else in the output buffer itself. info[b] = 0, or j + 1 for the first
+// column whose pivot is not positive (torch.linalg.cholesky_ex's convention); the factor is then
+// incomplete (NaN from that column on), as rocSOLVER leaves it.
+constexpr int kCholThreads = 256;
+
+template <typename TI, typename TO, bool kLds>
+__global__ __launch_bounds__(kCholThreads) void k_cholesky(const TI* __restrict__ A, int n,
+                                                           TO* __restrict__ Lout,
+                                                           int* __restrict__ info) {
+  extern __shared__ double wl[];   // kLds: [n][n + 1]
+  __shared__ double piv;
+  __shared__ int fail;
+  const int64_t b = blockIdx.x;
+  const int t = threadIdx.x;
+  const TI* Ab = A + b * (int64_t)n * n;
+  TO* Lb = Lout + b * (int64_t)n * n;
+  const int ld = kLds ? n + 1 : n;
+  double* W = kLds ? wl : nullptr;
+  // the lower triangle of A (the upper one is never read, as in LAPACK's potrf 'L')
+  auto at = [&](int i, int k) -> double& { return W[i * ld + k]; };
+  if (kLds) {
+    for (int e = t; e < n * n; e += kCholThreads) {
+      const int i = e / n, k = e - i * n;
+      if (k <= i) wl[i * ld + k] = (double)Ab[e];
+    }
+  }
+  if (t == 0) fail = 0;
+  __syncthreads();
+  if constexpr (kLds) {
+    for (int j = 0; j < n; ++j) {
+      if (t == 0) {
+        const double d = at(j, j);
+        if (!(d > 0.0) && fail == 0) fail = j + 1;
+        piv = sqrt(d);
+        at(j, j) = piv;
+      }
+      __syncthreads();
+      const double inv = 1.0 / piv;
+      for (int i = j + 1 + t; i < n; i += kCholThreads) at(i, j) *= inv;
+      __syncthreads();
+      const int m = n - j - 1;
+      for (int e = t; e < m * m; e += kCholThreads) {
+        const int i = j + 1 + e / m, k = j + 1 + e % m;
+        if (k <= i) at(i, k) = fma(-at(i, j), at(k, j), at(i, k));
+      }
+      __syncthreads();
+    }
+    for (int e = t; e < n * n; e += kCholThreads) {
+      const int i = e / n, k = e - i * n;
+      Lb[e] = k <= i ? (TO)wl[i * ld + k] : (TO)0;
+    }
+  } else {
+    // in place in the output (double precision output only: see mi_cholesky)
+    double* G = reinterpret_cast<double*>(Lb);
+    for (int e = t; e < n * n; e += kCholThreads) {
+      const int i = e / n, k = e - i * n;
+      G[e] = k <= i ? (double)Ab[e] : 0.0;
+    }
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      if (t == 0) {
+        const double d = G[j * n + j];
+        if (!(d > 0.0) && fail == 0) fail = j + 1;
+        piv = sqrt(d);
+        G[j * n + j] = piv;
+      }
+      __syncthreads();
+      const double inv = 1.0 / piv;
+      for (int i = j + 1 + t; i < n; i += kCholThreads) G[i * n + j] *= inv;
+      __syncthreads();
+      const int m = n - j - 1;
+      for (int64_t e = t; e < (int64_t)m * m; e += kCholThreads) {
+        const int i = j + 1 + (int)(e / m), k = j + 1 + (int)(e % m);
+        if (k <= i) G[i * n + k] = fma(-G[i * n + j], G[k * n + j], G[i * n + k]);
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0 && info != nullptr) info[b] = fail;
+}
+
 }  // namespace mi
 
 extern "C" {
+
+int mi_cholesky(const void* A, int32_t a_bytes, int64_t batch, int64_t n, void* L,
+                int32_t l_bytes, int32_t* info, void* stream) {
+  if (batch < 0 || n < 1 || n > MI_MVN_MAX_N || batch > 0x7fffffff ||
+      (a_bytes != 4 && a_bytes != 8) || (l_bytes != 4 && l_bytes != 8))
+    return MI_EINVAL;
+  if (batch == 0) return 0;
+  if (A == nullptr || L == nullptr) return MI_EINVAL;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)batch), block(mi::kCholThreads);
+  if (n <= mi::kMvnLdsMaxN) {
+    const size_t bytes = sizeof(double) * (size_t)n * (size_t)(n + 1);
+    if (a_bytes == 8 && l_bytes == 8)
+      hipLaunchKernelGGL((mi::k_cholesky<double, double, true>), grid, block, bytes, s,
+                         static_cast<const double*>(A), (int)n, static_cast<double*>(L), info);
+    else if (a_bytes == 4 && l_bytes == 4)
+      hipLaunchKernelGGL((mi::k_cholesky<float, float, true>), grid, block, bytes, s,
+                         static_cast<const float*>(A), (int)n, static_cast<float*>(L), info);
+    else if (a_bytes == 4)
+      hipLaunchKernelGGL((mi::k_cholesky<float, double, true>), grid, block, bytes, s,
+                         static_cast<const float*>(A), (int)n, static_cast<double*>(L), info);
+    else
+      hipLaunchKernelGGL((mi::k_cholesky<double, float, true>), grid, block, bytes, s,
+                         static_cast<const double*>(A), (int)n, static_cast<float*>(L), info);
+  } else {
+    if (l_bytes != 8) return MI_EUNSUPPORTED;   // larger factors work in the float64 output
+    if (a_bytes == 8)
+      hipLaunchKernelGGL((mi::k_cholesky<double, double, false>), grid, block, 0, s,
+                         static_cast<const double*>(A), (int)n, static_cast<double*>(L), info);
+    else
+      hipLaunchKernelGGL((mi::k_cholesky<float, double, false>), grid, block, 0, s,
+                         static_cast<const float*>(A), (int)n, static_cast<double*>(L), info);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
 
 int mi_mvn_tril_forward(const double* value, const double* loc, const double* scale_tril,
                         int64_t batch, int64_t n, double* log_prob, double* w, double* u,

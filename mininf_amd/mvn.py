@@ -102,6 +102,69 @@ class _MvnTrilLogProb(torch.autograd.Function):
         return _MvnTrilLogProb.apply(*phys), (0, 0, 0)
 
 
+def _cholesky_launch(A: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(L, info) of mi_cholesky over the leading batch dimensions of A [..., n, n]."""
+    n = A.shape[-1]
+    if A.shape[-2] != n or A.dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"cholesky of a float32/float64 [..., n, n] tensor, got "
+                         f"{tuple(A.shape)} {A.dtype}")
+    batch = A.shape[:-2]
+    B = math.prod(batch)
+    a = A.reshape(B, n, n).contiguous()
+    wide = n > 80 and A.dtype == torch.float32   # larger factors are formed in float64
+    L = torch.empty((B, n, n), dtype=torch.float64 if wide else A.dtype, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    nat.check(nat.lib().mi_cholesky(a.data_ptr(), a.element_size(), B, n, L.data_ptr(),
+                                    L.element_size(), info.data_ptr(),
+                                    nat.stream_handle(A.device)), "mi_cholesky")
+    if wide:
+        L = L.to(A.dtype)
+    return L.reshape(A.shape), info.reshape(batch)
+
+
+class _CholeskyFn(torch.autograd.Function):
+    """``torch.linalg.cholesky_ex(A)`` on mi_cholesky, with torch's backward
+    (FunctionsManual linalg_cholesky_backward restated: gA = sym(L^-T phi(L^T gL) L^-1), phi the
+    lower triangle with the diagonal halved) and a vmap rule for the particle trace."""
+    @staticmethod
+    def forward(A):  # type: ignore[override]
+        return _cholesky_launch(A)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):  # type: ignore[override]
+        L, info = output
+        ctx.mark_non_differentiable(info)
+        ctx.save_for_backward(L)
+
+    @staticmethod
+    def backward(ctx, gL, _ginfo):  # type: ignore[override]
+        (L,) = ctx.saved_tensors
+        if gL is None:
+            return None
+        P = (L.mT @ gL.tril()).tril()
+        P = P - 0.5 * torch.diag_embed(P.diagonal(dim1=-2, dim2=-1))
+        X = torch.linalg.solve_triangular(L.mT, P, upper=True, left=True)     # L^-T phi
+        gA = torch.linalg.solve_triangular(L, X, upper=False, left=False)     # ... L^-1
+        return 0.5 * (gA + gA.mT)
+
+    @staticmethod
+    def vmap(info, in_dims, A):  # type: ignore[override]
+        (d,) = in_dims
+        A = A.movedim(d, 0) if d is not None else A.expand(info.batch_size, *A.shape)
+        return _CholeskyFn.apply(A), (0, 0)
+
+
+def cholesky_ex(A: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``torch.linalg.cholesky_ex(A)`` (lower) on the HIP kernel: (L, info), no host sync."""
+    return _CholeskyFn.apply(A)
+
+
+def cholesky_supported(A: torch.Tensor) -> bool:
+    return os.environ.get("MININF_AMD_CHOLESKY_KERNEL", "1") != "0" and A.is_cuda and \
+        A.dtype in (torch.float32, torch.float64) and A.dim() >= 2 and \
+        A.shape[-1] == A.shape[-2] and 1 <= A.shape[-1] <= MAX_N
+
+
 def log_prob(distribution: MultivariateNormal, value: torch.Tensor) -> torch.Tensor:
     """``distribution.log_prob(value)`` on the kernel (float64; see :func:`enabled`)."""
     lp, _, _ = _MvnTrilLogProb.apply(value.to(torch.float64), distribution.loc,

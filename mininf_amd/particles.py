@@ -477,7 +477,12 @@ class TraceCompat(TorchFunctionMode):
                         device_copy(x, self.device)
                 args, kwargs = tree_map(lift, (args, kwargs))
         if func is torch.linalg.cholesky and not kwargs.get("upper", False) and "out" not in kwargs:
-            L, info = torch.linalg.cholesky_ex(*args, **kwargs)
+            A = args[0] if args else kwargs["input"]
+            if mvn.cholesky_supported(A):
+                # mi_cholesky: no host synchronisation, capturable (rocSOLVER's potrf is not)
+                L, info = mvn.cholesky_ex(A)
+            else:
+                L, info = torch.linalg.cholesky_ex(*args, **kwargs)
             ok = (info == 0).all()
             self.tracer.checks.append(CheckRecord("cholesky", self.tracer._emit(ok), (
                 "linalg.cholesky: The factorization could not be completed because the input is "

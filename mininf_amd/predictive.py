@@ -57,7 +57,7 @@ def _launch(family: int, params: Sequence[torch.Tensor], N: int, seed: int,
     seed &= 0xFFFFFFFFFFFFFFFF
     if family == NORMAL:
         nat.check(lib.mi_normal_rsample(a.data_ptr(), 1, b.data_ptr(), 1, 1, N, seed, 0, None,
-                                        stream_id, 0, None, out.data_ptr(), stream),
+                                        stream_id, 0, 0, None, out.data_ptr(), stream),
                   "mi_normal_rsample")
     elif family == GAMMA:
         g = torch.empty(N, dtype=torch.float32, device=device)

@@ -65,6 +65,46 @@ def test_mvn_kernel_under_vmap(device):
     assert rel(got, want) <= 1e-10
 
 
+@pytest.mark.parametrize("n,batch,dtype", [(1, (3,), torch.float64), (7, (2, 3), torch.float64),
+                                            (50, (16,), torch.float64), (80, (4,), torch.float32),
+                                            (81, (2,), torch.float64), (130, (), torch.float32)])
+def test_cholesky_kernel_matches_torch(device, n, batch, dtype):
+    """mi_cholesky (float64 arithmetic) against torch.linalg.cholesky, and its backward against
+    torch's autograd of the factorisation (float64 at 1e-10)."""
+    gen = torch.Generator().manual_seed(n)
+    A = spd(batch, n, device, gen)
+    L, info = mvn.cholesky_ex(A.to(dtype))
+    want = torch.linalg.cholesky(A)
+    assert L.dtype == dtype and L.shape == A.shape and info.shape == batch
+    assert int(info.abs().sum()) == 0
+    tol = 1e-10 if dtype == torch.float64 else 1e-6
+    assert rel(L.double(), want) <= tol, rel(L.double(), want)
+    if dtype == torch.float64:
+        weight = torch.randn(A.shape, generator=gen, dtype=torch.float64).to(device)
+        grads = []
+        for ours in (True, False):
+            a = A.clone().requires_grad_()
+            out = mvn.cholesky_ex(a)[0] if ours else torch.linalg.cholesky(a)
+            (out * weight).sum().backward()
+            grads.append(a.grad)
+        assert rel(grads[0], grads[1]) <= 1e-9, rel(grads[0], grads[1])
+
+
+def test_cholesky_kernel_reports_non_positive_pivots(device):
+    A = torch.eye(5, dtype=torch.float64, device=device).repeat(3, 1, 1)
+    A[1, 3, 3] = -1.0
+    _, info = mvn.cholesky_ex(A)
+    _, want = torch.linalg.cholesky_ex(A)
+    assert info.tolist() == want.tolist() == [0, 4, 0]
+
+
+def test_cholesky_kernel_under_vmap(device):
+    gen = torch.Generator().manual_seed(9)
+    A = spd((12,), 20, device, gen)
+    L, info = torch.func.vmap(mvn.cholesky_ex)(A)
+    assert rel(L, torch.linalg.cholesky(A)) <= 1e-10 and info.shape == (12,)
+
+
 def test_mvn_kernel_rejects_oversized_events(device):
     from mininf_amd import _native as nat
     buf = torch.zeros(8, dtype=torch.float64, device=device).data_ptr()
