@@ -446,6 +446,23 @@ int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t ke
  * applies (contiguous 16-byte aligned rows of X, P % 4 == 0); for cross-checks. */
 #define MI_LINEAR_VALU 2
 
+/* The rows of the next minibatch drawn by the kernel that reads them (instead of a separate
+ * mi_minibatch_rows launch): counter, n, batch, batches_per_epoch, shuffle and seed have
+ * mi_minibatch_rows's meaning; the kernel reads the batch number counter[0], draws its rows, writes
+ * them to `out` (when non-NULL, for later readers of the batch) and advances counter[0] once all
+ * of its blocks have read it (counter[1]: completion count, zero between launches).
+ * DataLoader(TensorDataset(X, y), batch_size, shuffle=True) of examples/minibatch.md:78. */
+typedef struct mi_rows {
+  uint64_t* counter;      /* NULL: no rows drawn here */
+  int64_t n;
+  int64_t batch;
+  int64_t batches;
+  uint64_t seed;
+  int32_t shuffle;
+  int32_t pad0;
+  int32_t* out;
+} mi_rows;
+
 typedef struct mi_linear {
   int64_t K;
   int64_t N;
@@ -471,6 +488,9 @@ typedef struct mi_linear {
   int32_t pad0;
   const int32_t* row_index; /* NULL, or row i of the site reads row row_index[i] of x, value and
                                mask (a device-resident minibatch, mi_minibatch_rows) */
+  mi_rows rows;           /* rows.counter non-NULL (row_index NULL): the site draws its batch's
+                             rows itself; only the matrix-core kernel with one row stage per
+                             block does (else MI_EUNSUPPORTED: launch mi_minibatch_rows first) */
 } mi_linear;
 
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes);

@@ -39,6 +39,7 @@ REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ABI_VERSION = 9   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
+MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
 c_i64 = ctypes.c_int64
 c_f32p = ctypes.POINTER(ctypes.c_float)
@@ -88,6 +89,12 @@ class Group(ctypes.Structure):
     ]
 
 
+class Rows(ctypes.Structure):
+    _fields_ = [("counter", c_vp), ("n", c_i64), ("batch", c_i64), ("batches", c_i64),
+                ("seed", ctypes.c_uint64), ("shuffle", ctypes.c_int32), ("pad0", ctypes.c_int32),
+                ("out", c_vp)]
+
+
 class Linear(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("N", c_i64), ("P", c_i64),
@@ -100,7 +107,7 @@ class Linear(ctypes.Structure):
         ("scale_constant", ctypes.c_float), ("grad_scale", ctypes.c_float),
         ("site_scale", ctypes.c_double),
         ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
-        ("row_index", c_vp),
+        ("row_index", c_vp), ("rows", Rows),
     ]
 
 

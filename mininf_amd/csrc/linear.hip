@@ -15,6 +15,7 @@
 // accumulators live in registers. Per-(tile, particle) partials are reduced in fp64 by k_finalize.
 #include "common.hpp"
 #include "internal.hpp"
+#include "rows.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -206,7 +207,8 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
                                                           int64_t stages_per_block,
                                                           int64_t ntile,
                                                           float* __restrict__ part,
-                                                          uint32_t* __restrict__ flags) {
+                                                          uint32_t* __restrict__ flags,
+                                                          int rows_half) {
   using S = MfShape<PT, NT>;
   constexpr int kMfThreads = NT;
   constexpr int kMfWaves = S::NW;
@@ -215,6 +217,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   const int64_t group = (bid / 8) % gy;
   __shared__ __attribute__((aligned(16))) float xs[S::CH * S::RSTR];
   __shared__ float2 yms[S::CH];
+  // rows drawn here (mi_linear.rows, ONESTAGE launches only): the stage's dataset rows
+  __shared__ int32_t grows[ONESTAGE ? S::CH : 1];
+  const bool gen_rows = ONESTAGE && L.rows.counter != nullptr;
+  uint64_t batch_no = 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), wave = tid / kWave;
@@ -268,14 +274,16 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
       const int64_t i = row0 + row;
-      const int64_t src = (i < N && L.row_index != nullptr) ? L.row_index[i] : i;
+      const int64_t src = (i < N && gen_rows) ? (int64_t)grows[ONESTAGE ? row : 0]
+                          : (i < N && L.row_index != nullptr) ? L.row_index[i] : i;
       xq[q] = (i < N && 4 * c4 < P)
                   ? *reinterpret_cast<const float4*>(L.x + src * L.x_stride_i + 4 * c4)
                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (tid < S::CH) {
       const int64_t row = row0 + tid;
-      const int64_t i = (row < N && L.row_index != nullptr) ? L.row_index[row] : row;
+      const int64_t i = (row < N && gen_rows) ? (int64_t)grows[ONESTAGE ? tid : 0]
+                        : (row < N && L.row_index != nullptr) ? L.row_index[row] : row;
       float y = 0.0f, m = 0.0f;
       if (row < N) {
         y = L.value[i * L.value_stride_i];
@@ -351,6 +359,22 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   };
 
   if constexpr (ONESTAGE) {
+    if (gen_rows) {
+      // this batch's rows of the block's stage, from the batch number every block reads before
+      // the last one to finish advances it (below)
+      batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid < S::CH && st0 < st1) {
+        const int64_t row = st0 * S::CH + tid;
+        int32_t r = 0;
+        if (row < N) {
+          const BatchOrder order = batch_order(batch_no, L.rows.batches, L.rows.seed);
+          r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
+          if (L.rows.out != nullptr && group == 0) L.rows.out[row] = r;
+        }
+        grows[tid] = r;
+      }
+      __syncthreads();
+    }
     if (st0 < st1) {
       load_stage(st0);
       store_stage();
@@ -501,6 +525,17 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   }
   publish_flags(flags, fl);
+  if (gen_rows) {
+    // the last block to finish advances the batch counter: every block has read it by then
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long done = atomicAdd((unsigned long long*)&L.rows.counter[1], 1ull);
+      if (done == (unsigned long long)gridDim.x - 1ull) {
+        L.rows.counter[1] = 0;
+        L.rows.counter[0] = batch_no + 1;
+      }
+    }
+  }
 }
 
 }  // namespace mi
@@ -510,6 +545,12 @@ namespace {
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 bool valid(const mi_linear* L) {
+  if (L != nullptr && L->rows.counter != nullptr) {
+    const mi_rows& R = L->rows;   // mi_minibatch_rows's conditions
+    if (L->row_index != nullptr || R.n < 1 || R.n > INT32_MAX || R.batch < 1 || R.batches < 1 ||
+        L->N > R.batch || (R.batches - 1) * R.batch >= R.n || R.batches * R.batch >= R.n + R.batch)
+      return false;
+  }
   return L != nullptr && L->K >= 1 && L->N >= 1 && L->P >= 1 && L->P <= MI_LINEAR_MAX_P &&
          (L->family == MI_NORMAL || L->family == MI_BERNOULLI_LOGITS) && L->x != nullptr &&
          L->theta != nullptr && L->value != nullptr;
@@ -611,7 +652,8 @@ void launch_mfma(const mi_linear& L, const Geometry& g, float* part, uint32_t* f
   const bool one = g.stages_per_block == 1;
 #define MI_LAUNCH_MFMA(GRADS, ONE)                                                              \
   hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, GRADS, ONE>), grid,      \
-                     dim3(NT), 0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags)
+                     dim3(NT), 0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags, \
+                     L.rows.counter != nullptr ? mi_feistel_half(L.rows.n) : 0)
   if (L.compute_grads) {
     if (one) MI_LAUNCH_MFMA(true, true); else MI_LAUNCH_MFMA(true, false);
   } else {
@@ -697,6 +739,8 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
     if (e != hipSuccess) return to_code(e);
   }
   const Geometry g = geometry(site);
+  if (site->rows.counter != nullptr && (!g.mfma || g.stages_per_block != 1))
+    return MI_EUNSUPPORTED;   // rows drawn only by one-stage matrix-core launches
   float* part = static_cast<float*>(workspace);
   if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
     return to_code(e);

@@ -10,37 +10,11 @@
 // (mi_linear.row_index); mi_gather_rows materialises a batch for any other use.
 #include "common.hpp"
 #include "internal.hpp"
+#include "rows.hpp"
 
 namespace mi {
 
 constexpr int kRowThreads = 256;
-constexpr int kFeistelRounds = 4;
-
-// murmur3's 32-bit finaliser of x ^ key: the Feistel round function.
-MI_DEV uint32_t round_fn(uint32_t x, uint32_t key) {
-  x ^= key;
-  x *= 0xcc9e2d51u;
-  x ^= x >> 16;
-  x *= 0x85ebca6bu;
-  x ^= x >> 13;
-  x *= 0xc2b2ae35u;
-  x ^= x >> 16;
-  return x;
-}
-
-// One pass of the balanced Feistel network over 2 * half bits.
-MI_DEV uint64_t feistel(uint64_t x, int half, const uint32_t (&keys)[kFeistelRounds]) {
-  const uint64_t mask = (1ull << half) - 1ull;
-  uint64_t l = x >> half, r = x & mask;
-#pragma unroll
-  for (int q = 0; q < kFeistelRounds; ++q) {
-    const uint64_t t = l ^ ((uint64_t)round_fn((uint32_t)r, keys[q]) & mask);
-    l = r;
-    r = t;
-  }
-  return (l << half) | r;
-}
-
 // counter[0]: batches drawn so far; counter[1]: completion count of the launch's blocks (zero
 // between launches). Every block reads counter[0]; the last block to finish advances it, so no
 // block can read the advanced value.
@@ -51,26 +25,9 @@ __global__ __launch_bounds__(kRowThreads) void k_minibatch_rows(uint64_t* __rest
                                                                 int32_t* __restrict__ rows,
                                                                 int64_t count) {
   const uint64_t c = counter[0];
-  const uint64_t epoch = c / (uint64_t)batches, b = c % (uint64_t)batches;
-  uint32_t keys[kFeistelRounds];
-#pragma unroll
-  for (int q = 0; q < kFeistelRounds; ++q)
-    keys[q] = round_fn((uint32_t)(seed ^ (seed >> 32)) ^ (uint32_t)q * 0x9e3779b9u,
-                       round_fn((uint32_t)epoch, (uint32_t)(epoch >> 32) + 0x7f4a7c15u));
+  const BatchOrder order = batch_order(c, batches, seed);
   const int64_t j = (int64_t)blockIdx.x * kRowThreads + threadIdx.x;
-  if (j < count) {
-    uint64_t x = b * (uint64_t)batch + (uint64_t)j;
-    if (x >= (uint64_t)n) {
-      x %= (uint64_t)n;   // (a batch position past the data: mi_minibatch_rows rejects it)
-    } else if (shuffle) {
-      // cycle walking: the orbit of x under the permutation of [0, 2^(2 half)) returns to
-      // [0, n) because x itself lies there
-      do {
-        x = feistel(x, half, keys);
-      } while (x >= (uint64_t)n);
-    }
-    rows[j] = (int32_t)x;
-  }
+  if (j < count) rows[j] = batch_row(order, j, n, batch, shuffle, half);
   __syncthreads();   // every thread of the block has read the counter
   if (threadIdx.x == 0) {
     const unsigned long long done = atomicAdd((unsigned long long*)&counter[1], 1ull);
@@ -99,12 +56,6 @@ namespace {
 
 int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
-int feistel_half(int64_t n) {
-  int bits = 2;
-  while (bits < 62 && (1ll << bits) < n) ++bits;
-  return (bits + 1) / 2;
-}
-
 }  // namespace
 
 extern "C" {
@@ -120,7 +71,7 @@ int mi_minibatch_rows(uint64_t* counter, int64_t n, int64_t batch, int64_t batch
                      dim3((unsigned)((count + mi::kRowThreads - 1) / mi::kRowThreads)),
                      dim3(mi::kRowThreads), 0,
                      static_cast<hipStream_t>(stream), counter, n, batch, batches_per_epoch,
-                     shuffle ? 1 : 0, seed, feistel_half(n), rows, count);
+                     shuffle ? 1 : 0, seed, mi_feistel_half(n), rows, count);
   return to_code(hipGetLastError());
 }
 

@@ -28,6 +28,7 @@ the same.) Sites evaluated by the kernels flag values of the rows they read, as 
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Dict, List, Optional, Tuple
 
@@ -54,13 +55,60 @@ def _storage_ptr(tensor) -> Optional[int]:
 
 
 class _Batch:
-    """One drawn minibatch: the device row indices and the (lazily gathered) column buffers."""
+    """
+    One drawn minibatch: the device row indices and the (lazily gathered) column buffers.
+
+    The rows themselves are drawn lazily too: the ``mi_minibatch_rows`` launch is held back until
+    something needs them, so that the one site kernel reading the batch can draw them itself
+    (``mi_linear.rows``, one launch less per step -- :meth:`take_rows`); any other reader
+    (:attr:`rows`, a gather) launches it first. Batches of one loader are launched in the order
+    they were drawn.
+    """
     def __init__(self, loader: "DeviceDataLoader", rows: torch.Tensor, count: int) -> None:
         self.loader = loader
-        self.rows = rows
+        self._rows = rows
         self.count = count
+        self.pending = True      # rows not drawn yet (no launch enqueued)
         self.buffers: List[torch.Tensor] = []
         self.filled: List[bool] = []
+
+    @property
+    def rows(self) -> torch.Tensor:
+        """The batch's int32 row indices (drawn now if still pending)."""
+        self.draw_rows()
+        return self._rows
+
+    def draw_rows(self) -> None:
+        """Enqueue the ``mi_minibatch_rows`` launch of a pending batch."""
+        if not self.pending:
+            return
+        self.pending = False
+        loader = self.loader
+        nat.check(nat.lib().mi_minibatch_rows(
+            loader.counter.data_ptr(), loader.n, loader.batch_size, loader.batches,
+            int(loader.shuffle), loader.seed, self._rows.data_ptr(), self.count,
+            nat.stream_handle(loader.device)), "mi_minibatch_rows")
+
+    def take_rows(self) -> Optional[nat.Rows]:
+        """
+        For the single kernel that reads this batch: a ``mi_rows`` descriptor drawing the rows
+        inside that kernel (and writing them to the row buffer for later readers), or None when
+        they are drawn already. The caller launches it next, or calls :meth:`draw_rows` first.
+        """
+        if not self.pending or self.count != self.loader.batch_size or \
+                os.environ.get("MININF_AMD_FUSE_ROWS", "1") == "0":
+            return None
+        loader = self.loader
+        R = nat.Rows()
+        R.counter = loader.counter.data_ptr()
+        R.n, R.batch, R.batches = loader.n, loader.batch_size, loader.batches
+        R.seed, R.shuffle = loader.seed, int(loader.shuffle)
+        R.out = self._rows.data_ptr()
+        return R
+
+    def rows_taken(self) -> None:
+        """The kernel given :meth:`take_rows`'s descriptor was launched: the rows are drawn."""
+        self.pending = False
 
     def fill(self, column: int) -> None:
         """Gather the column's rows into its buffer (once)."""
@@ -207,17 +255,21 @@ class DeviceDataLoader:
         # counter[1] is the rows kernel's completion count
         self.counter = torch.zeros(2, dtype=torch.int64, device=self.device)
         self._position = 0   # host mirror for eager iteration (ragged last batch)
+        self._last: Optional[_Batch] = None   # the last drawn batch (rows may be pending)
 
     def __len__(self) -> int:
         return self.batches
 
     def _draw(self, count: int) -> Tuple[Minibatch, ...]:
+        # the previous batch's rows, if nobody drew them yet, come first (the batch counter
+        # orders the batches)
+        if self._last is not None:
+            self._last.draw_rows()
         rows = torch.empty(count, dtype=torch.int32, device=self.device)
-        nat.check(nat.lib().mi_minibatch_rows(
-            self.counter.data_ptr(), self.n, self.batch_size, self.batches, int(self.shuffle),
-            self.seed, rows.data_ptr(), count, nat.stream_handle(self.device)),
-            "mi_minibatch_rows")
         batch = _Batch(self, rows, count)
+        # held until the next draw, which launches its rows if nothing else did (a batch drawn
+        # and dropped unused still advances the loader, as with an eager rows launch)
+        self._last = batch
         ref = weakref.ref(batch)
         ptrs: List[int] = []
         weakref.finalize(batch, _forget, ptrs, ref)

@@ -538,7 +538,7 @@ class _LinearLauncher:
         self.N, self.P = self.X.shape
         # device-resident minibatch read through its row index (mininf_amd.data): the dataset
         # columns of X and the value, and the batch's rows
-        self.rows: Optional[torch.Tensor] = None
+        self.batch: Optional["data._Batch"] = None
         self.X_src, self.value_src = self.X, None
         self.theta = theta
         self.sigma = sigma
@@ -560,7 +560,7 @@ class _LinearLauncher:
     def inputs(self) -> List[Optional[torch.Tensor]]:
         return [self.theta, self.sigma_input]
 
-    def describe(self, compute_grads: bool) -> nat.Linear:
+    def describe(self, compute_grads: bool, draw_rows: bool = True) -> nat.Linear:
         L = nat.Linear()
         L.K, L.N, L.P = self.K, self.N, self.P
         L.family = FAMILY_CODES[self.site.family]
@@ -568,8 +568,14 @@ class _LinearLauncher:
         L.x_stride_i, L.x_stride_j = self.X_src.stride()
         L.theta = self.theta.data_ptr()
         L.theta_stride_k, L.theta_stride_j = self.theta.stride()
-        if self.rows is not None:
-            L.row_index = self.rows.data_ptr()
+        if self.batch is not None:
+            # the batch's rows: drawn by this kernel when nothing has drawn them yet (one launch
+            # less per step), else read through the row index
+            R = self.batch.take_rows() if draw_rows else None
+            if R is not None:
+                L.rows = R
+            else:
+                L.row_index = self.batch.rows.data_ptr()
             L.value = self.value_src.data_ptr()
             L.value_stride_i = self.value_src.stride(0)
         else:
@@ -612,11 +618,21 @@ class _LinearLauncher:
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
         reduce = nat.Reduce()
-        nat.check(lib.mi_linear_forward_deferred(
-            ctypes.byref(L), workspace.data_ptr(), size.value, total.data_ptr(), nat.ptr(dslots),
-            flags.data_ptr(), None if start is None else start.cuda_event,
-            None if stop is None else stop.cuda_event, nat.stream_handle(device),
-            ctypes.byref(reduce) if defer else None), "mi_linear_forward_deferred")
+
+        def launch(L):
+            return lib.mi_linear_forward_deferred(
+                ctypes.byref(L), workspace.data_ptr(), size.value, total.data_ptr(),
+                nat.ptr(dslots), flags.data_ptr(), None if start is None else start.cuda_event,
+                None if stop is None else stop.cuda_event, nat.stream_handle(device),
+                ctypes.byref(reduce) if defer else None)
+        code = launch(L)
+        if L.rows.counter:
+            if code == nat.MI_EUNSUPPORTED:   # this launch shape does not draw rows: draw first
+                L = self.describe(compute_grads, draw_rows=False)
+                code = launch(L)
+            elif code == 0:
+                self.batch.rows_taken()
+        nat.check(code, "mi_linear_forward_deferred")
         self.reduce = reduce if defer and reduce.part else None
         self.workspace = workspace   # holds the deferred partials
         return total, dslots, flags
@@ -690,7 +706,7 @@ def plan_linear(trace: ParticleTrace, g0: float, device: torch.device) -> List[_
                 if xb is not None and vb is not None and xb[0] is vb[0] and mask is None and \
                         value.si == 1:
                     batch = xb[0]
-                    launcher.rows = batch.rows
+                    launcher.batch = batch
                     launcher.X_src = batch.loader.columns[xb[1]]
                     launcher.value_src = batch.loader.columns[vb[1]]
         if launcher is None:

@@ -134,5 +134,12 @@ def _positive_definite(value: torch.Tensor) -> torch.Tensor:
     (``if not sym_check.all()``), so that it also runs per particle under ``vmap``: symmetric
     within torch's tolerance AND a successful Cholesky factorisation -- the same result.
     """
-    symmetric = torch.isclose(value, value.mT, atol=1e-6).all(-2).all(-1)
+    from . import mvn
+    # torch.isclose(value, value.mT, atol=1e-6) spelled out (isclose has no vmap batching rule:
+    # its fallback launches per particle)
+    other = value.mT
+    close = (value == other) | ((value - other).abs() <= 1e-6 + 1e-5 * other.abs())
+    symmetric = close.all(-2).all(-1)
+    if mvn.cholesky_supported(value):   # mi_cholesky: no host sync, capturable
+        return symmetric & mvn.cholesky_ex(value.detach())[1].eq(0)
     return symmetric & torch.linalg.cholesky_ex(value).info.eq(0)

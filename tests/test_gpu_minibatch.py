@@ -191,3 +191,39 @@ def test_view_outlives_the_yielded_tensor(device):
     gc.collect()
     got = view.clone().as_subclass(torch.Tensor).reshape(batch, 2).cpu()
     assert torch.equal(got, X.cpu()[rows.long()])
+
+
+def test_linear_kernel_draws_the_batch_rows(device, monkeypatch):
+    """The linear site kernel draws the rows of the batch it reads (mi_linear.rows: no
+    mi_minibatch_rows launch): the rows it writes are the oracle's order, and the losses and
+    gradients of several eager steps equal those with the rows kernel (MININF_AMD_FUSE_ROWS=0)."""
+    model, X, y = regression(device, n=8192)
+    n, batch = 8192, 1024
+
+    def run():
+        loader = DeviceDataLoader(X, y, batch_size=batch, shuffle=True, drop_last=True, seed=4)
+        module = guide_module(device)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=32, seed=6)
+        out = []
+        for step in range(10):   # crosses an epoch (8 batches per epoch)
+            Xb, yb = loader.next()
+            b = Xb._mininf_batch
+            loss = loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": module()})
+            loss.backward()
+            taken_by_kernel = not b.pending
+            rows = b.rows.cpu().tolist()
+            assert rows == oracle.batch_rows(step, n, batch, 8, True, 4, batch)
+            out.append((float(loss), [q.grad.clone() for q in module.parameters()],
+                        taken_by_kernel))
+            for q in module.parameters():
+                q.grad = None
+        return out, int(loader.counter[0])
+
+    fused, c0 = run()
+    monkeypatch.setenv("MININF_AMD_FUSE_ROWS", "0")
+    plain, c1 = run()
+    assert c0 == c1 == 10
+    for (l0, g0, _), (l1, g1, _) in zip(fused, plain):
+        assert l0 == l1
+        for a, b in zip(g0, g1):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)

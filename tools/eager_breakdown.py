@@ -1,0 +1,92 @@
+"""
+Host-time breakdown of the README training loop run eagerly: where the
+~1 ms per C2 step goes between the user's calls and inside EvidenceLowerBoundLoss.forward.
+
+    python tools/eager_breakdown.py [c2|c3|c4|c5] [steps]
+
+Wraps the phases with perf_counter accumulators (no profiler overhead) and prints one JSON line
+of microseconds per step.
+"""
+import collections
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import mininf_amd  # noqa: E402
+import mininf_amd.optim  # noqa: E402
+from mininf_amd import engine, guide, nn, particles  # noqa: E402
+
+ACC = collections.defaultdict(float)
+
+
+def wrap(module, name, tag):
+    fn = getattr(module, name)
+
+    def timed(*args, **kwargs):
+        t0 = time.perf_counter()
+        try:
+            return fn(*args, **kwargs)
+        finally:
+            ACC[tag] += time.perf_counter() - t0
+    setattr(module, name, timed)
+
+
+def main():
+    config = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    device = torch.device("cuda", 0)
+    w = bench.workload(config, device, 1, 0)
+    optimizer = mininf_amd.optim.Adam(w["module"].parameters(), lr=w["lr"])
+    loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(num_particles=w["k_local"], seed=1)
+    wrap(guide, "draw_all", "loss.draw_all")
+    wrap(particles, "trace_particles", "loss.trace")
+    wrap(engine, "elbo", "loss.elbo(plan+launch)")
+    wrap(engine.LogJoint, "raise_on_violation", "loss.validation_sync")
+    wrap(engine.LogJoint, "flag_vector", "loss.flag_vector")
+    wrap(engine._ElboPlan, "forward", "loss.elbo.plan_forward")
+    wrap(engine, "plan_groups", "loss.elbo.plan_groups")
+    wrap(engine, "plan_absorption", "loss.elbo.plan_absorption")
+    wrap(engine, "entropy_factors", "loss.entropy_factors")
+    wrap(engine._ElboPlan, "backward", "backward.elbo_plan")
+
+    def step(record):
+        t = [time.perf_counter()]
+        optimizer.zero_grad(set_to_none=True)
+        t.append(time.perf_counter())
+        q = w["guide"]()
+        t.append(time.perf_counter())
+        loss = loss_fn(w["conditioned"](), q)
+        t.append(time.perf_counter())
+        loss.backward()
+        t.append(time.perf_counter())
+        optimizer.step()
+        t.append(time.perf_counter())
+        if record:
+            for tag, a, b in zip(("zero_grad", "guide()", "loss()", "backward", "adam"), t, t[1:]):
+                ACC["step." + tag] += b - a
+            ACC["step.total"] += t[-1] - t[0]
+
+    for _ in range(5):
+        step(False)
+    torch.cuda.synchronize()
+    ACC.clear()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    out = {k: round(1e6 * v / steps, 1) for k, v in sorted(ACC.items())}
+    out["wall_us_per_step"] = round(1e6 * wall / steps, 1)
+    out["config"] = config
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
