@@ -1179,6 +1179,9 @@ class _ElboPlan:
             d = E.factors[j]
             d.family, d.n = f.family, f.n
             d.weight = f.weight
+            # the entropy kernels read the parameters directly: a deferred exp transform no draw
+            # kernel has written yet runs first (a no-op once a draw kernel wrote it)
+            guide.fill_exp(f.tensor)
             base = f.tensor.data_ptr()
             if f.family in (nat.BETA, nat.GAMMA):
                 d.param[0], d.param[1] = base, base + 4

@@ -349,6 +349,11 @@ class _GammaRsampleFn(torch.autograd.Function):
     def forward(ctx, cfg: DrawConfig, conc: torch.Tensor, conc_s: int, rate: torch.Tensor,
                 rate_s: int):  # type: ignore[override]
         N, K = conc.shape[0], cfg.K
+        # a deferred exp transform of the guide's parameters runs before the sampler reads them
+        # (no validation read has forced it when torch's argument validation is off, e.g. in a
+        # captured step)
+        fill_exp(conc)
+        fill_exp(rate)
         x = torch.empty((K, N), dtype=torch.float32, device=conc.device)
         g = torch.empty((K, N), dtype=torch.float32, device=conc.device)
         seed, step = _philox_key(cfg)

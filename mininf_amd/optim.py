@@ -45,6 +45,10 @@ class Adam(torch.optim.Optimizer):
                                       maximize=maximize, amsgrad=False, capturable=True,
                                       foreach=None, fused=None, differentiable=False))
         self._counters: Dict[torch.device, torch.Tensor] = {}
+        # per parameter group: the launch descriptors of the last step, reused while the group's
+        # parameters, state tensors and hyper-parameters are unchanged (only the gradients'
+        # addresses are rewritten): a step costs microseconds of Python, not a rebuild
+        self._plans: Dict[int, "_Plan"] = {}
 
     def _counter_words(self, device: torch.device) -> torch.Tensor:
         words = self._counters.get(device)
@@ -60,12 +64,15 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = nat.lib()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
+            active = [p for p in group["params"] if p.grad is not None]
+            plan = self._plans.get(gi)
+            if plan is not None and plan.matches(group, active, self.state):
+                plan.launch(active, lib, self._counter_words)
+                continue
             beta1, beta2 = group["betas"]
             batch = []
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            for p in active:
                 if p.grad.is_sparse:
                     raise RuntimeError("Adam does not support sparse gradients")
                 nat.require_device(p, "Adam parameter")
@@ -95,6 +102,7 @@ class Adam(torch.optim.Optimizer):
                         state[key] = moment.to(device=p.device, dtype=torch.float32) \
                             .reshape(p.shape).contiguous()
                 batch.append((p, state))
+            descs = []
             for start in range(0, len(batch), nat.ADAM_MAX_TENSORS):
                 chunk = batch[start:start + nat.ADAM_MAX_TENSORS]
                 desc = nat.Adam()
@@ -108,8 +116,45 @@ class Adam(torch.optim.Optimizer):
                     t.exp_avg, t.exp_avg_sq = (state["exp_avg"].data_ptr(),
                                                state["exp_avg_sq"].data_ptr())
                     t.step, t.numel = state["step"].data_ptr(), p.numel()
-                device = chunk[0][0].device
-                nat.check(lib.mi_adam_step(ctypes.byref(desc),
-                                           self._counter_words(device).data_ptr(),
-                                           nat.stream_handle(device)), "mi_adam_step")
+                descs.append((desc, chunk[0][0].device))
+            plan = _Plan(group, batch, descs)
+            self._plans[gi] = plan
+            plan.launch(active, lib, self._counter_words, fresh=True)
         return loss
+
+
+class _Plan:
+    """The ``mi_adam`` descriptors of one parameter group, reusable across steps."""
+    def __init__(self, group: dict, batch, descs) -> None:
+        self.params = [p for p, _ in batch]
+        self.states = [(s, s["step"], s["exp_avg"], s["exp_avg_sq"]) for _, s in batch]
+        self.hyper = self._hyper(group)
+        self.descs = descs
+        self.ptrs = [p.data_ptr() for p in self.params]
+
+    @staticmethod
+    def _hyper(group: dict):
+        return (group["lr"], tuple(group["betas"]), group["eps"], group["weight_decay"],
+                group["maximize"])
+
+    def matches(self, group: dict, active, state) -> bool:
+        if len(active) != len(self.params) or self._hyper(group) != self.hyper:
+            return False
+        for p, q, ptr, (s, step, m, v) in zip(active, self.params, self.ptrs, self.states):
+            g = p.grad
+            if p is not q or p.data_ptr() != ptr or state.get(p) is not s or \
+                    s.get("step") is not step or s.get("exp_avg") is not m or \
+                    s.get("exp_avg_sq") is not v or g.is_sparse or \
+                    g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device:
+                return False
+        return True
+
+    def launch(self, active, lib, counter_words, fresh: bool = False) -> None:
+        cursor = 0
+        for desc, device in self.descs:
+            if not fresh:
+                for j in range(desc.num):
+                    desc.tensors[j].grad = active[cursor + j].grad.data_ptr()
+            cursor += desc.num
+            nat.check(lib.mi_adam_step(ctypes.byref(desc), counter_words(device).data_ptr(),
+                                       nat.stream_handle(device)), "mi_adam_step")
