@@ -49,6 +49,19 @@ class Adam(torch.optim.Optimizer):
         # parameters, state tensors and hyper-parameters are unchanged (only the gradients'
         # addresses are rewritten): a step costs microseconds of Python, not a rebuild
         self._plans: Dict[int, "_Plan"] = {}
+        # torch wraps Optimizer.step in a profiling / hook dispatcher (tens of microseconds of
+        # Python per call); with no hooks registered this instance calls the step directly
+        self.step = self._dispatch_step  # type: ignore[method-assign]
+
+    def _dispatch_step(self, closure=None):
+        from torch.optim import optimizer as torch_optimizer
+        if self._optimizer_step_pre_hooks or self._optimizer_step_post_hooks or \
+                torch_optimizer._global_optimizer_pre_hooks or \
+                torch_optimizer._global_optimizer_post_hooks:
+            return type(self).step(self, closure)   # torch's hooked path
+        with torch.no_grad():
+            return type(self).step.__wrapped__(self, closure) \
+                if hasattr(type(self).step, "__wrapped__") else type(self).step(self, closure)
 
     def _counter_words(self, device: torch.device) -> torch.Tensor:
         words = self._counters.get(device)

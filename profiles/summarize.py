@@ -11,7 +11,8 @@ files committed here:
   HBM section; confirmed on our own kernels, whose algorithmic read bytes are known, see
   DESIGN.md). The C2 site kernel reads its data through the scalar unit (64-byte s_load), which
   FETCH_SIZE counts in full (4 MB of x -> 4.33 MB raw): no doubling there.
-* ``<round>_valu_pmc.json`` -- issue counters of the VALU-bound kernels (``SQ_INSTS_VALU`` and its
+* ``<round>_valu_pmc.json`` -- where the waves' cycles go (``SQ_WAVE_CYCLES`` split into
+  ``SQ_ACTIVE_INST_ANY`` / ``SQ_WAIT_ANY`` / ``SQ_WAIT_INST_ANY``, from r03) and issue counters of the VALU-bound kernels (``SQ_INSTS_VALU`` and its
   per-type split, ``GRBM_GUI_ACTIVE``), with the VALU pipe's busy fraction from measured issue
   costs (tools/valu_peak.hip: 2 cycles per wave64 instruction, 4 for v_pk_fma_f32, 8 for a
   transcendental, 6 for v_mad_u64_u32).
@@ -117,7 +118,7 @@ def valu(raw: str, round_tag: str) -> None:
     result = {}
     for cfg, pattern in DOMINANT.items():
         per = {}
-        for kind in ("valu", "vtype"):
+        for kind in ("valu", "vtype", "wait"):
             src = os.path.join(raw, f"{kind}_{cfg}", "run_counter_collection.csv")
             if not os.path.exists(src):
                 continue
@@ -151,6 +152,13 @@ def valu(raw: str, round_tag: str) -> None:
                     int64 * COST["int64"])
             per["valu_issue_cycles"] = busy
             per["valu_busy"] = busy / (SIMDS * cycles)
+        if "SQ_WAVE_CYCLES" in per and per["SQ_WAVE_CYCLES"]:
+            # where the waves' cycles go (disjoint: issuing, parked on s_waitcnt / barriers,
+            # ready but issue-stalled on a dependency or a busy pipe; MI355X_MICROARCH.md)
+            wc = per["SQ_WAVE_CYCLES"]
+            for name in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+                if name in per:
+                    per[name.lower() + "_frac"] = per[name] / wc
         if "SQ_VALU_MFMA_BUSY_CYCLES" in per:
             per["mfma_busy"] = per["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cycles)
         result[cfg] = per
