@@ -525,15 +525,14 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   }
   publish_flags(flags, fl);
-  if (gen_rows) {
-    // the last block to finish advances the batch counter: every block has read it by then
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned long long done = atomicAdd((unsigned long long*)&L.rows.counter[1], 1ull);
-      if (done == (unsigned long long)gridDim.x - 1ull) {
-        L.rows.counter[1] = 0;
-        L.rows.counter[0] = batch_no + 1;
-      }
+  // the last block to finish advances the batch counter: every block has read it by then. (A
+  // count taken right after the read instead made all blocks hit one address at once: measured
+  // slower.)
+  if (gen_rows && tid == 0) {
+    const unsigned long long done = atomicAdd((unsigned long long*)&L.rows.counter[1], 1ull);
+    if (done == (unsigned long long)gridDim.x - 1ull) {
+      L.rows.counter[1] = 0;
+      L.rows.counter[0] = batch_no + 1;
     }
   }
 }

@@ -1156,7 +1156,11 @@ Plan make_plan(const mi_group* g) {
                                    : row_elems();
     p.nseg = ceil_div(g->N, 64 * p.elems);
     const int64_t gx = ceil_div(p.nseg, 4);
-    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(kTargetBlocks, gx)));
+    // fused draws: about one round of 4-wave blocks (MININF_AMD_DRAW_TARGET_BLOCKS) -- fewer,
+    // longer particle blocks write fewer d loc / d scale partial rows for the same balance
+    const int64_t target = p.draw ? env_int("MININF_AMD_DRAW_TARGET_BLOCKS", (int)kTargetBlocks)
+                                  : kTargetBlocks;
+    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(target, gx)));
     p.rows_per_block = ceil_div(g->K, gy);
     gy = ceil_div(g->K, p.rows_per_block);
     p.grid = dim3((unsigned)gx, (unsigned)gy);

@@ -131,3 +131,35 @@ def test_gradient_bucket_matches_all_reduce_gradients():
         assert p.exitcode == 0
     for rank, out in results:
         assert all(all(step) for step in out), (rank, out)
+
+
+# ------------------------------------------------------------------------------------------------
+# Data sharding (DataShard): the element slices and the loss's replicated-site bookkeeping
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [9, 10, 4097, 1_000_000])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_element_shards_tile_the_data_axis(n, world):
+    from mininf_amd.distributed import element_shard
+    shards = [element_shard(n, world=world, rank=r, shared=("mu",)) for r in range(world)]
+    assert shards[0].start == 0 and shards[-1].stop == n
+    for a, b in zip(shards, shards[1:]):
+        assert a.stop == b.start
+    for s in shards:
+        assert s.size == 0 or s.start % 4 == 0   # one Philox block per element quad
+        assert s.shared == ("mu",) and s.world == world
+
+
+def test_data_shard_validation():
+    from mininf_amd.distributed import DataShard
+    with pytest.raises(ValueError, match="multiple of 4"):
+        DataShard(6, 10)
+    with pytest.raises(ValueError, match="stop >= start"):
+        DataShard(8, 4)
+    shard = DataShard(8, 20, ["mu"], world=4)
+    assert shard.shared == ("mu",) and shard.slice == slice(8, 20) and shard.size == 12
+    with pytest.raises(ValueError, match="process_group"):
+        EvidenceLowerBoundLoss(num_particles=4, data_shard=DataShard(0, 8))
+    loss = EvidenceLowerBoundLoss(num_particles=16, data_shard=DataShard(0, 8, ("mu",), world=4))
+    # every rank evaluates every particle; the loss knows the world from the shard
+    assert loss._shard() == (4, 0, 16, 0)
+    assert loss._element_offsets({"mu": None, "z": None}) == {"z": 0}
