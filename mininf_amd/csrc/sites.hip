@@ -591,7 +591,8 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
                                                                    int mode,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
-  // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below)
+  // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below); bit 2: L2
+  // prefetch of the chunk
   const int rank1 = mode & 1;
   const bool balance = (mode & 2) != 0;
   const int64_t chunks = nseg - 1;
@@ -609,6 +610,12 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int64_t i0 = c * kSmemChunk;
   const int len = (int)min((int64_t)kSmemChunk, G.N - i0);
   uint32_t fl = 0u;
+  // mode bit 2: the chunk pulled into L2 by one vector load per 64-byte line at the start, so the
+  // scalar loads of the main loop hit L2 instead of waiting on HBM (the value is only consumed at
+  // the end: no wait inside the loop, one register)
+  const bool prefetch = (mode & 4) != 0;
+  float pf = 0.0f;
+  if (prefetch && (int)threadIdx.x * 16 < len) pf = xg[i0 + (int)threadIdx.x * 16];
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
   const int64_t K = G.K;
@@ -736,6 +743,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       }
     }
   }
+  if (prefetch && !(pf == 0.0f || pf == 1.0f)) fl |= MI_FLAG_SUPPORT;   // (checked again above)
   s_a = block_sum(s_a, scratch);
   if (SUFF) {
 #pragma unroll
@@ -1241,7 +1249,8 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   const int64_t side = (int64_t)p.grid.x - chunks;
   const int gy = (int)p.grid.y;
   const dim3 grid((unsigned)(ceil_div(chunks, 8) * 8 * gy + side));
-  const int rank1 = (smem_rank1(&G, p) ? 1 : 0) | (env_int("MININF_AMD_BCAST_BALANCE", 1) ? 2 : 0);
+  const int rank1 = (smem_rank1(&G, p) ? 1 : 0) | (env_int("MININF_AMD_BCAST_BALANCE", 1) ? 2 : 0) |
+                    (env_int("MININF_AMD_BCAST_PREFETCH", 0) ? 4 : 0);
 #define MI_SMEM(P, CH) \
   hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, rank1, flags)
   switch (smem_variant()) {
