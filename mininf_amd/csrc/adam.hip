@@ -46,8 +46,26 @@ MI_DEV mi_adam_tensor tensor_at(const mi_adam& A, int t) {
   }
 }
 
+// NT: non-temporal 16-byte loads and stores (streamed once per step; MININF_AMD_ADAM_NT)
+typedef float f4v __attribute__((ext_vector_type(4)));
+MI_DEV float4 ld(const float4* p, bool nt) {
+  if (!nt) return *p;
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+MI_DEV void st(float4* p, const float4& v, bool nt) {
+  if (!nt) {
+    *p = v;
+    return;
+  }
+  const f4v w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+}
+
+template <bool NT, int U>
 __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, const AdamPlan P,
-                                                             unsigned* __restrict__ counters) {
+                                                             unsigned* __restrict__ counters,
+                                                             int count) {
   int t = 0;
 #pragma unroll
   for (int q = 1; q < MI_ADAM_MAX_TENSORS; ++q)
@@ -58,79 +76,45 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
   const int64_t chunk = pick_adam(P.chunk, t);
   const int b = (int)blockIdx.x - first;
 
-  // bias corrections in double, then handed to the update as float (adam_math's opmath_t
-  // parameters)
-  const float s1 = *T.step + 1.0f;
-  const float bc1 = (float)(1.0 - pow(A.beta1, (double)s1));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow(A.beta2, (double)s1));
-  const float step_size = (float)(A.lr / (double)bc1);
   const int64_t i0 = (int64_t)b * chunk;
   const int64_t i1 = min(T.numel, i0 + chunk);
-  auto update = [&](float& param, float grad, float& m, float& v) {
-    if (A.maximize) grad = -grad;
-    // the contractions spelled out: fma(beta, moment, (1 - beta) * grad [* grad]), the form
-    // torch's kernel compiles to (the compiler may pick another when left to itself)
-    if (A.weight_decay != 0.0) grad = (float)fma((double)param, A.weight_decay, (double)grad);
-    m = (float)fma(A.beta1, (double)m, (1.0 - A.beta1) * (double)grad);
-    v = (float)fma(A.beta2, (double)v, ((1.0 - A.beta2) * (double)grad) * (double)grad);
-    const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + A.eps);
-    param -= step_size * m / denom;
-  };
   const bool vec = ((reinterpret_cast<uintptr_t>(T.param) | reinterpret_cast<uintptr_t>(T.grad) |
                      reinterpret_cast<uintptr_t>(T.exp_avg) |
                      reinterpret_cast<uintptr_t>(T.exp_avg_sq)) & 15) == 0;
+  float4* __restrict__ param = reinterpret_cast<float4*>(T.param);
+  const float4* __restrict__ grad = reinterpret_cast<const float4*>(T.grad);
+  float4* __restrict__ exp_avg = reinterpret_cast<float4*>(T.exp_avg);
+  float4* __restrict__ exp_avg_sq = reinterpret_cast<float4*>(T.exp_avg_sq);
+  // U quads per lane per pass (16-byte accesses; chunk is a multiple of 4 * kAdamThreads, so a
+  // lane's quads are whole except the tensor's last, partial one)
+  constexpr int64_t kStride = 4 * kAdamThreads;
+  float4 p[U], g[U], m[U], v[U];
+  auto load_pass = [&](int64_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = base + u * kStride;
+      if (e + 3 < i1) {
+        const int64_t q = e >> 2;
+        p[u] = ld(param + q, NT);
+        g[u] = ld(grad + q, NT);
+        m[u] = ld(exp_avg + q, NT);
+        v[u] = ld(exp_avg_sq + q, NT);
+      }
+    }
+  };
   int64_t i = i0 + 4 * (int64_t)threadIdx.x;
-  if (vec) {   // 16-byte loads and stores (chunk is a multiple of 4 * kAdamThreads)
-    float4* __restrict__ param = reinterpret_cast<float4*>(T.param);
-    const float4* __restrict__ grad = reinterpret_cast<const float4*>(T.grad);
-    float4* __restrict__ exp_avg = reinterpret_cast<float4*>(T.exp_avg);
-    float4* __restrict__ exp_avg_sq = reinterpret_cast<float4*>(T.exp_avg_sq);
-    auto step4 = [&](float4& p, const float4& g, float4& m, float4& v) {
-      update(p.x, g.x, m.x, v.x);
-      update(p.y, g.y, m.y, v.y);
-      update(p.z, g.z, m.z, v.z);
-      update(p.w, g.w, m.w, v.w);
-    };
-    // two quads per lane per pass: all eight 16-byte loads in flight before the first update
-    constexpr int64_t kStride = 4 * kAdamThreads;
-    for (; i + kStride + 3 < i1; i += 2 * kStride) {
-      const int64_t q0 = i >> 2, q1 = (i + kStride) >> 2;
-      float4 p0 = param[q0], p1 = param[q1];
-      const float4 g0 = grad[q0], g1 = grad[q1];
-      float4 m0 = exp_avg[q0], m1 = exp_avg[q1];
-      float4 v0 = exp_avg_sq[q0], v1 = exp_avg_sq[q1];
-      step4(p0, g0, m0, v0);
-      step4(p1, g1, m1, v1);
-      param[q0] = p0;
-      param[q1] = p1;
-      exp_avg[q0] = m0;
-      exp_avg[q1] = m1;
-      exp_avg_sq[q0] = v0;
-      exp_avg_sq[q1] = v1;
-    }
-    for (; i + 3 < i1; i += kStride) {
-      const int64_t q = i >> 2;
-      float4 p = param[q];
-      const float4 g = grad[q];
-      float4 m = exp_avg[q], v = exp_avg_sq[q];
-      step4(p, g, m, v);
-      param[q] = p;
-      exp_avg[q] = m;
-      exp_avg_sq[q] = v;
-    }
-  }
-  // the rest (the tail, or unaligned tensors) element by element
-  for (int64_t j = (vec ? i : i0 + threadIdx.x); j < i1; j += vec ? 1 : kAdamThreads) {
-    if (vec && j >= i + 4) break;
-    float p = T.param[j], m = T.exp_avg[j], v = T.exp_avg_sq[j];
-    update(p, T.grad[j], m, v);
-    T.param[j] = p;
-    T.exp_avg[j] = m;
-    T.exp_avg_sq[j] = v;
-  }
+  // the first pass's loads go out before the bias corrections (two double pows, a few hundred
+  // dependent instructions): without the barrier the compiler hoists them ahead of every load
+  if (vec) load_pass(i);
+  __builtin_amdgcn_sched_barrier(0);
 
-  __syncthreads();   // every thread of the block has read the step
-  if (threadIdx.x == 0) {
+  // bias corrections in double, then handed to the update as float (adam_math's opmath_t
+  // parameters)
+  const float s1 = *T.step + 1.0f;
+  // The step advances once every workgroup of the tensor has read it: counted at the end
+  // (count 1), or right after the read (count 2: the atomic's return is awaited only at the end,
+  // behind this workgroup's own traffic); count 0 leaves the step alone (timing probes only).
+  auto last_block = [&]() {
     unsigned* tc = counters + t * (1 + kAdamGroup);
     const int groups = (nblocks + kAdamGroup - 1) / kAdamGroup;
     bool done = true;
@@ -143,8 +127,72 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
     }
     if (done && atomicAdd(tc, 1u) == (unsigned)(groups > 1 ? groups : nblocks) - 1u) {
       *tc = 0u;
-      *T.step = s1;
+      return true;
     }
+    return false;
+  };
+  bool started_last = false;
+  if (count == 2) {
+    // every wave's step read complete (lgkmcnt(0) only: the first pass's loads stay in flight),
+    // then the barrier
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (threadIdx.x == 0) started_last = last_block();
+  }
+  const float bc1 = (float)(1.0 - pow(A.beta1, (double)s1));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(A.beta2, (double)s1));
+  const float step_size = (float)(A.lr / (double)bc1);
+  auto update = [&](float& param, float grad, float& m, float& v) {
+    if (A.maximize) grad = -grad;
+    // the contractions spelled out: fma(beta, moment, (1 - beta) * grad [* grad]), the form
+    // torch's kernel compiles to (the compiler may pick another when left to itself)
+    if (A.weight_decay != 0.0) grad = (float)fma((double)param, A.weight_decay, (double)grad);
+    m = (float)fma(A.beta1, (double)m, (1.0 - A.beta1) * (double)grad);
+    v = (float)fma(A.beta2, (double)v, ((1.0 - A.beta2) * (double)grad) * (double)grad);
+    const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + A.eps);
+    param -= step_size * m / denom;
+  };
+  auto step4 = [&](float4& p, const float4& g, float4& m, float4& v) {
+    update(p.x, g.x, m.x, v.x);
+    update(p.y, g.y, m.y, v.y);
+    update(p.z, g.z, m.z, v.z);
+    update(p.w, g.w, m.w, v.w);
+  };
+  if (vec) {
+    for (; i + 3 < i1; i += U * kStride) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i + u * kStride + 3 < i1) step4(p[u], g[u], m[u], v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = i + u * kStride;
+        if (e + 3 < i1) {
+          const int64_t q = e >> 2;
+          st(param + q, p[u], NT);
+          st(exp_avg + q, m[u], NT);
+          st(exp_avg_sq + q, v[u], NT);
+        }
+      }
+      load_pass(i + U * kStride);
+    }
+  }
+  // element by element: the partial last quad (its lane), or every element of an unaligned tensor
+  const int64_t tail = i1 & ~int64_t{3};
+  const bool owns_tail = tail < i1 && ((tail - i0) >> 2) % kAdamThreads == threadIdx.x;
+  for (int64_t j = vec ? (owns_tail ? tail : i1) : i0 + threadIdx.x; j < i1;
+       j += vec ? 1 : kAdamThreads) {
+    float pe = T.param[j], me = T.exp_avg[j], ve = T.exp_avg_sq[j];
+    update(pe, T.grad[j], me, ve);
+    T.param[j] = pe;
+    T.exp_avg[j] = me;
+    T.exp_avg_sq[j] = ve;
+  }
+
+  if (count == 1) {
+    __syncthreads();   // every thread of the block has read the step
+    if (threadIdx.x == 0 && last_block()) *T.step = s1;
+  } else if (count == 2 && threadIdx.x == 0 && started_last) {
+    *T.step = s1;
   }
 }
 
@@ -163,29 +211,62 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
       adam->num > MI_ADAM_MAX_TENSORS)
     return MI_EINVAL;
   mi::AdamPlan P{};
-  int blocks = 0;
+  int64_t total = 0;
   for (int t = 0; t < adam->num; ++t) {
     const mi_adam_tensor& T = adam->tensors[t];
     if (T.param == nullptr || T.grad == nullptr || T.exp_avg == nullptr ||
         T.exp_avg_sq == nullptr || T.step == nullptr || T.numel < 1)
       return MI_EINVAL;
-    // at most kAdamGroup^2 blocks per tensor, 8 elements per thread at least
-    static const int64_t min_chunk = [] {   // elements per block at least (MININF_AMD_ADAM_CHUNK)
-      const char* v = std::getenv("MININF_AMD_ADAM_CHUNK");
-      const int64_t n = v != nullptr ? std::atoll(v) : 8 * mi::kAdamThreads;
-      return std::max<int64_t>(4 * mi::kAdamThreads, n);
-    }();
-    int64_t chunk = std::max<int64_t>(min_chunk,
-                                      (T.numel + mi::kAdamGroup * mi::kAdamGroup - 1) /
-                                          (mi::kAdamGroup * mi::kAdamGroup));
+    total += T.numel;
+  }
+  // A few hundred workgroups over all tensors (MININF_AMD_ADAM_BLOCKS, default 512): measured on
+  // C5's 2 x 1e6 parameters (tools/adam_probe.py, profiles/r03_adam_sweep.log), 500 workgroups of
+  // 4096 elements run at 12.5 us, 980 of 2048 at 17 us; at least MININF_AMD_ADAM_CHUNK elements
+  // per workgroup and at most kAdamGroup^2 workgroups per tensor.
+  static const int64_t target_blocks = [] {
+    const char* v = std::getenv("MININF_AMD_ADAM_BLOCKS");
+    return std::max<int64_t>(1, v != nullptr ? std::atoll(v) : 512);
+  }();
+  static const int64_t min_chunk = [] {
+    const char* v = std::getenv("MININF_AMD_ADAM_CHUNK");
+    const int64_t n = v != nullptr ? std::atoll(v) : 4 * mi::kAdamThreads;
+    return std::max<int64_t>(4 * mi::kAdamThreads, n);
+  }();
+  const int64_t even = (total + target_blocks - 1) / target_blocks;
+  int blocks = 0;
+  for (int t = 0; t < adam->num; ++t) {
+    const mi_adam_tensor& T = adam->tensors[t];
+    int64_t chunk = std::max({min_chunk, even,
+                              (T.numel + mi::kAdamGroup * mi::kAdamGroup - 1) /
+                                  (mi::kAdamGroup * mi::kAdamGroup)});
     chunk = (chunk + 4 * mi::kAdamThreads - 1) / (4 * mi::kAdamThreads) * (4 * mi::kAdamThreads);
     P.first[t] = blocks;
     P.chunk[t] = chunk;
     blocks += (int)((T.numel + chunk - 1) / chunk);
   }
   for (int t = adam->num; t <= MI_ADAM_MAX_TENSORS; ++t) P.first[t] = blocks;
-  hipLaunchKernelGGL(mi::k_adam_step, dim3((unsigned)blocks), dim3(mi::kAdamThreads), 0,
-                     static_cast<hipStream_t>(stream), *adam, P, counters);
+  // variants (MININF_AMD_ADAM_NT=1: non-temporal accesses; MININF_AMD_ADAM_UNROLL=4: four quads
+  // per lane per pass)
+  static const int variant = [] {
+    const char* nt = std::getenv("MININF_AMD_ADAM_NT");
+    const char* un = std::getenv("MININF_AMD_ADAM_UNROLL");
+    return (nt != nullptr && nt[0] == '1' ? 1 : 0) | (un != nullptr && un[0] == '4' ? 2 : 0);
+  }();
+  // MININF_AMD_ADAM_COUNT: 2 count at the start (default; 12.5 us vs 14.2 us counting at the
+  // end, C5), 1 at the end, 0 never (timing probes only: the step does not advance)
+  static const int count = [] {
+    const char* v = std::getenv("MININF_AMD_ADAM_COUNT");
+    const int c = v != nullptr ? std::atoi(v) : 2;
+    return (c == 0 || c == 1) ? c : 2;
+  }();
+  const dim3 grid((unsigned)blocks), block(mi::kAdamThreads);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (variant) {
+    case 1: hipLaunchKernelGGL((mi::k_adam_step<true, 2>), grid, block, 0, s, *adam, P, counters, count); break;
+    case 2: hipLaunchKernelGGL((mi::k_adam_step<false, 4>), grid, block, 0, s, *adam, P, counters, count); break;
+    case 3: hipLaunchKernelGGL((mi::k_adam_step<true, 4>), grid, block, 0, s, *adam, P, counters, count); break;
+    default: hipLaunchKernelGGL((mi::k_adam_step<false, 2>), grid, block, 0, s, *adam, P, counters, count); break;
+  }
   return to_code(hipGetLastError());
 }
 

@@ -234,6 +234,75 @@ MI_DEV void eval_bernoulli_logits(float l, float v, Elem& e) {
   e.support_bad = !(v == 0.0f || v == 1.0f);
 }
 
+// ---- packed pairs ---------------------------------------------------------------------------
+// The same Normal / Bernoulli-logits arithmetic on two elements at once, written on two-wide float
+// vectors so that the adds, multiplies and FMAs issue as v_pk_add_f32 / v_pk_mul_f32 /
+// v_pk_fma_f32 (two fp32 lanes per instruction on CDNA4, the same IEEE rounding per element as the
+// scalar forms above); compares, selects and transcendentals stay per element. The fused-draw site
+// programs use them for their element pairs (jit.cpp, "packed").
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+MI_DEV f2 splat2(float a) { return f2{a, a}; }
+MI_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+struct Elem2 {
+  f2 lp;
+  f2 d[3];
+  bool param_bad;        // either element
+  bool support_bad[2];
+};
+
+// guide_normals for one quad as two pairs (elements 0-1 and 2-3): the uniforms' scale-and-offset,
+// the radius' multiply and the final products on packed instructions; per element the same
+// operations as box_muller, so the values are bit-identical.
+MI_DEV void guide_normals2(uint64_t seed, uint64_t step, uint32_t stream_id, uint64_t quad,
+                           uint64_t particle, f2& n01, f2& n23) {
+  const U4 b = guide_bits(seed, step, stream_id, 0, quad, particle);
+  const f2 ua = fma2(f2{(float)(b.x >> 8), (float)(b.z >> 8)}, splat2(5.9604644775390625e-08f),
+                     splat2(2.98023223876953125e-08f));
+  const f2 ut = fma2(f2{(float)(b.y >> 8), (float)(b.w >> 8)}, splat2(5.9604644775390625e-08f),
+                     splat2(2.98023223876953125e-08f));
+  const f2 l = -1.38629436111989061883f * f2{__builtin_amdgcn_logf(ua.x), __builtin_amdgcn_logf(ua.y)};
+  const f2 r = f2{__builtin_amdgcn_sqrtf(l.x), __builtin_amdgcn_sqrtf(l.y)};
+  n01 = splat2(r.x) * f2{__builtin_amdgcn_cosf(ut.x), __builtin_amdgcn_sinf(ut.x)};
+  n23 = splat2(r.y) * f2{__builtin_amdgcn_cosf(ut.y), __builtin_amdgcn_sinf(ut.y)};
+}
+
+MI_DEV void eval_normal2(f2 loc, f2 scale, f2 v, Elem2& e) {
+  const f2 inv = f2{rcp(scale.x), rcp(scale.y)};
+  const f2 inv2 = inv * inv;
+  const f2 diff = v - loc;
+  const f2 c = -(f2{logf(scale.x), logf(scale.y)} + kHalfLog2Pi);
+  e.lp = fma2((-0.5f * inv2) * diff, diff, c);
+  const f2 g = diff * inv2;
+  e.d[0] = g;
+  e.d[1] = fma2(diff, g, splat2(-1.0f)) * inv;
+  e.d[2] = -g;
+  // bitwise, not short-circuit, combinations: lane masks the compiler keeps in SGPR pairs
+  e.param_bad = !(scale.x > 0.0f) | (loc.x != loc.x) | !(scale.y > 0.0f) | (loc.y != loc.y);
+  e.support_bad[0] = (v.x != v.x);
+  e.support_bad[1] = (v.y != v.y);
+}
+
+MI_DEV void eval_bernoulli_logits2(f2 l, f2 v, Elem2& e) {
+  const f2 t = f2{fast_exp(-fabsf(l.x)), fast_exp(-fabsf(l.y))};
+  const f2 u = 1.0f + t;
+  const f2 r = f2{rcp(u.x), rcp(u.y)};
+  // log1p_unit per element: fma(t - (u - 1), r, log(u) * ln 2)
+  const f2 lu = f2{__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)} * 0.69314718055994531f;
+  const f2 l1p = fma2(t - (u - 1.0f), r, lu);
+  const f2 mx = f2{fmaxf(l.x, 0.0f), fmaxf(l.y, 0.0f)};
+  e.lp = -(mx - l * v + l1p);
+  const f2 tr = t * r;
+  const f2 sig = f2{l.x >= 0.0f ? r.x : tr.x, l.y >= 0.0f ? r.y : tr.y};
+  e.d[0] = v - sig;
+  e.d[1] = splat2(0.0f);
+  e.d[2] = l;
+  e.param_bad = (l.x != l.x) | (l.y != l.y);
+  e.support_bad[0] = !((v.x == 0.0f) | (v.x == 1.0f));
+  e.support_bad[1] = !((v.y == 0.0f) | (v.y == 1.0f));
+}
+
 // Bernoulli(probs): logits = log(p_c) - log1p(-p_c), p_c = clamp(p, eps, 1 - eps)
 // (bernoulli.py:104-106 -> utils.py probs_to_logits / clamp_probs); clamp passes the gradient
 // only inside [eps, 1 - eps].

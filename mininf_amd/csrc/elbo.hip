@@ -252,7 +252,8 @@ MI_DEV void partial_lane_elements(const mi_factor& F, int64_t base, int ti, int6
     ic[e] = ok[e] ? i : 0;
     s0[e] = s1[e] = 0.0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) pm[e][j] = F.param[j] != nullptr ? F.param[j][ic[e] * F.stride[j]] : 1.0f;
+    for (int j = 0; j < 2; ++j)   // only what the exp transforms read (C5's loc is not)
+      pm[e][j] = F.transform[j] == MI_TRANSFORM_EXP ? F.param[j][ic[e] * F.stride[j]] : 1.0f;
   }
   // rows outermost: each row's eight loads (four elements, two sums) issue together
   for (int64_t r = 0; r < rows; ++r) {
@@ -285,6 +286,69 @@ MI_DEV void partial_lane_elements(const mi_factor& F, int64_t base, int ti, int6
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       if (F.grad[j] != nullptr) F.grad[j][i * F.grad_stride[j]] = (float)g[e][j];
+  }
+}
+
+// The same backward with 16-byte accesses (Normal factors, n % 4 == 0, unit strides, aligned --
+// checked by the plan): lane quads q = first + p * ti, p < NP, every load of all NP quads in flight
+// before the first gradient is computed; the arithmetic and its order are those of
+// partial_lane_elements.
+template <int NP>
+MI_DEV void partial_lane_quads(const mi_factor& F, int64_t first, int ti, int64_t rows, float u,
+                               double w) {
+  const bool exp0 = F.transform[0] == MI_TRANSFORM_EXP, exp1 = F.transform[1] == MI_TRANSFORM_EXP;
+  const int64_t nq = F.n >> 2;
+  const float4* __restrict__ sc = reinterpret_cast<const float4*>(F.param[1]);
+  const float4* __restrict__ lc = reinterpret_cast<const float4*>(F.param[0]);
+  float4 scale[NP], loc[NP];
+  double s0[NP][4], s1[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int64_t q = min(first + (int64_t)p * ti, nq - 1);
+    scale[p] = sc[q];
+    loc[p] = exp0 ? lc[q] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s0[p][e] = s1[p][e] = 0.0;
+  }
+  for (int64_t r = 0; r < rows; ++r) {
+    const float4* __restrict__ r0 = reinterpret_cast<const float4*>(F.partial[0] + r * F.n);
+    const float4* __restrict__ r1 = reinterpret_cast<const float4*>(F.partial[1] + r * F.n);
+    float4 a0[NP], a1[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int64_t q = min(first + (int64_t)p * ti, nq - 1);
+      a0[p] = r0[q];
+      a1[p] = r1[q];
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      s0[p][0] += (double)a0[p].x; s0[p][1] += (double)a0[p].y;
+      s0[p][2] += (double)a0[p].z; s0[p][3] += (double)a0[p].w;
+      s1[p][0] += (double)a1[p].x; s1[p][1] += (double)a1[p].y;
+      s1[p][2] += (double)a1[p].z; s1[p][3] += (double)a1[p].w;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int64_t q = first + (int64_t)p * ti;
+    if (q >= nq) continue;
+    const float sv[4] = {scale[p].x, scale[p].y, scale[p].z, scale[p].w};
+    const float lv[4] = {loc[p].x, loc[p].y, loc[p].z, loc[p].w};
+    float g0[4], g1[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // entropy_grad of a Normal: (0, 1 / scale)
+      double d0 = (double)u * s0[p][e] + w * 0.0;
+      double d1 = (double)u * s1[p][e] + w * (double)(1.0f / sv[e]);
+      if (exp0) d0 *= (double)lv[e];
+      if (exp1) d1 *= (double)sv[e];
+      g0[e] = (float)d0;
+      g1[e] = (float)d1;
+    }
+    if (F.grad[0] != nullptr)
+      reinterpret_cast<float4*>(F.grad[0])[q] = make_float4(g0[0], g0[1], g0[2], g0[3]);
+    if (F.grad[1] != nullptr)
+      reinterpret_cast<float4*>(F.grad[1])[q] = make_float4(g1[0], g1[1], g1[2], g1[3]);
   }
 }
 
@@ -321,6 +385,16 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   double s0 = 0.0, s1 = 0.0;
   if (!FORWARD && pick(P.epl, a) == 4) {   // a fused draw's few partial rows: 4 elements per lane
     partial_lane_elements(F, (int64_t)col * ti * 4 + tx, ti, rows, u, w);
+    return;
+  }
+  if (!FORWARD && pick(P.epl, a) < 0) {   // the same over quads: -epl quads per lane
+    const int np = -pick(P.epl, a);
+    const int64_t q0 = (int64_t)col * ti * np + tx;
+    switch (np) {
+      case 2: partial_lane_quads<2>(F, q0, ti, rows, u, w); break;
+      case 4: partial_lane_quads<4>(F, q0, ti, rows, u, w); break;
+      default: partial_lane_quads<1>(F, q0, ti, rows, u, w); break;
+    }
     return;
   }
   if (tk == 1 && slices == 1) {   // a lane per element: no block reduction, and no barrier
@@ -884,6 +958,31 @@ struct Layout {
   int64_t doubles;
 };
 
+// quads per lane of partial_lane_quads (MININF_AMD_ELBO_QUADS: 0 off, 1, 2 or 4)
+int env_quads() {
+  static const int v = [] {
+    const char* e = getenv("MININF_AMD_ELBO_QUADS");
+    // measured on C5 (two partial rows of 1e6): step 0.2427 ms with 2, 0.2457-0.2484 without
+    const int n = e != nullptr ? atoi(e) : 2;
+    return (n == 1 || n == 2 || n == 4) ? n : 0;
+  }();
+  return v;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// partial_lane_quads' layout: a Normal factor of whole quads, unit strides, 16-byte aligned rows
+bool quad_layout(const mi_factor& F) {
+  if (F.family != MI_NORMAL || (F.n & 3) != 0 || F.stride[1] != 1 || !aligned16(F.param[1]) ||
+      !aligned16(F.partial[0]) || !aligned16(F.partial[1]))
+    return false;
+  if (F.transform[0] == MI_TRANSFORM_EXP && (F.stride[0] != 1 || !aligned16(F.param[0])))
+    return false;
+  for (int j = 0; j < 2; ++j)
+    if (F.grad[j] != nullptr && (F.grad_stride[j] != 1 || !aligned16(F.grad[j]))) return false;
+  return true;
+}
+
 // finish: the backward only combines the sums the forward left in F.saved
 void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::AbsorbPlan& P,
                   int64_t& counters, int64_t& doubles, int& blocks) {
@@ -925,8 +1024,13 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
   slices = ceil_div(rows, rps);
   // a backward over a few partial rows, one lane per element: four elements per lane instead
   P.epl[a] = (!forward && F.draw_kind == MI_DRAW_PARTIALS && tk == 1 && slices == 1) ? 4 : 1;
+  // ... as 16-byte quads when the layout allows (MININF_AMD_ELBO_QUADS: quads per lane, 0 = off)
+  const int quads = env_quads();
+  if (P.epl[a] == 4 && quads > 0 && quad_layout(F)) P.epl[a] = -quads;
   P.ti[a] = ti;
-  P.gx[a] = (int)(P.epl[a] == 4 ? ceil_div(F.n, (int64_t)ti * 4) : gx);
+  P.gx[a] = (int)(P.epl[a] == 4    ? ceil_div(F.n, (int64_t)ti * 4)
+                  : P.epl[a] < 0 ? ceil_div(F.n >> 2, (int64_t)ti * -P.epl[a])
+                                 : gx);
   P.slices[a] = (int)slices;
   P.rows_per_slice[a] = rps;
   P.counter[a] = counters;

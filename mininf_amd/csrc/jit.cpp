@@ -67,6 +67,18 @@ bool one_param(int family) {
 
 bool role_used(int family, int q) { return !(one_param(family) && q == 1); }
 
+// Families with packed-pair evaluations (device_math.hpp eval_*2).
+bool packed_family(int family) { return family == MI_NORMAL || family == MI_BERNOULLI_LOGITS; }
+
+// Whether the fused-draw loop of `g` runs on element pairs (PlanInfo.packed, when every site has a
+// packed form and the lane's elements pair up).
+bool use_packed(const mi_group& g, const PlanInfo& plan) {
+  if (!plan.packed || plan.elems % 2 != 0) return false;
+  for (int s = 0; s < g.num_sites; ++s)
+    if (!packed_family(g.sites[s].family)) return false;
+  return true;
+}
+
 // Everything about a group that changes the generated code.
 struct Signature {
   std::string text;
@@ -101,7 +113,7 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
     << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll
-    << (plan.block_rows ? "B" : "") << "|"
+    << (plan.block_rows ? "B" : "") << (use_packed(g, plan) ? "P" : "") << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -166,12 +178,77 @@ void emit_site_eval(std::ostringstream& o, const mi_group& g, int s, const std::
   o << in << "}\n";
 }
 
+// Element `comp` (0 or 1) of pair h of a per-element expression ("s2[e]" -> "s2[2 * h + 1]").
+std::string at_pair(std::string x, int comp) {
+  const std::string to = comp ? "[2 * h + 1]" : "[2 * h]";
+  for (size_t i = x.find("[e]"); i != std::string::npos; i = x.find("[e]", i + to.size()))
+    x.replace(i, 3, to);
+  return x;
+}
+
+// A role's value for pair h as an f2: per-element operands pair up, the rest are splatted.
+std::string pair_role(const std::string& x) {
+  if (x.find("[e]") == std::string::npos) return "mi::splat2(" + x + ")";
+  return "mi::f2{" + at_pair(x, 0) + ", " + at_pair(x, 1) + "}";
+}
+
+// emit_site_eval for element pair h (elements 2h, 2h + 1): the arithmetic of each element is that
+// of the scalar form, the log-probability and slot sums keep the scalar order (element 2h, then
+// 2h + 1), dense gradients accumulate per element as f2.
+void emit_site_eval2(std::ostringstream& o, const mi_group& g, int s, const std::string& valid,
+                     const char* in) {
+  const mi_site& st = g.sites[s];
+  std::string r[3];
+  for (int q = 0; q < 3; ++q) {
+    if (!role_used(st.family, q)) r[q] = "0.0f";
+    else if (st.operand[q] < 0) r[q] = "c" + std::to_string(s) + "_" + std::to_string(q);
+    else r[q] = operand_var(g, st.operand[q]);
+  }
+  o << in << "{\n" << in << "  mi::Elem2 el;\n";
+  if (one_param(st.family))
+    o << in << "  mi::" << eval_fn(st.family) << "2(" << pair_role(r[0]) << ", " << pair_role(r[2])
+      << ", el);\n";
+  else
+    o << in << "  mi::" << eval_fn(st.family) << "2(" << pair_role(r[0]) << ", " << pair_role(r[1])
+      << ", " << pair_role(r[2]) << ", el);\n";
+  std::string obs = valid;
+  if (st.mask != nullptr) obs = "(" + obs + " && " + mask_var(st, s) + ")";
+  o << in << "  const bool obs0 = " << at_pair(obs, 0) << ", obs1 = " << at_pair(obs, 1) << ";\n";
+  o << in << "  lp" << s << " += obs0 ? el.lp.x : 0.0f;\n";
+  o << in << "  lp" << s << " += obs1 ? el.lp.y : 0.0f;\n";
+  o << in << "  pb" << s << " |= el.param_bad;\n" << in << "  sb" << s
+    << " |= (obs0 & el.support_bad[0]) | (obs1 & el.support_bad[1]);\n";
+  if (g.compute_grads) {
+    bool any = false;
+    for (int q = 0; q < 3; ++q) {
+      const int op = st.operand[q];
+      if (op >= 0 && role_used(st.family, q) && g.operands[op].grad_mode != MI_GRAD_NONE) any = true;
+    }
+    if (any)
+      o << in << "  const mi::f2 w = mi::f2{obs0 ? scale" << s << " : 0.0f, obs1 ? scale" << s
+        << " : 0.0f};\n";
+    for (int q = 0; q < 3; ++q) {
+      const int op = st.operand[q];
+      if (op < 0 || !role_used(st.family, q)) continue;
+      if (g.operands[op].grad_mode == MI_GRAD_DENSE)
+        o << in << "  g" << op << "[h] = mi::fma2(w, el.d[" << q << "], g" << op << "[h]);\n";
+      else if (g.operands[op].grad_mode == MI_GRAD_PARTICLE) {
+        const std::string sl = "sl" + std::to_string(g.operands[op].slot);
+        o << in << "  " << sl << " = fmaf(w.x, el.d[" << q << "].x, " << sl << ");\n";
+        o << in << "  " << sl << " = fmaf(w.y, el.d[" << q << "].y, " << sl << ");\n";
+      }
+    }
+  }
+  o << in << "}\n";
+}
+
 std::string generate(const mi_group& g, const PlanInfo& plan) {
   const bool row = plan.row;
   const int E = plan.elems;
   const std::string Es = std::to_string(E);
   const int nsite_values = plan.combined ? 1 : g.num_sites;
   const int nv = nsite_values + (g.compute_grads ? g.num_slots : 0);
+  const bool packed = use_packed(g, plan);
   std::ostringstream o;
   auto is = [&](int op, Kind k) { return kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == k; };
   auto mask_is = [&](int s, Kind k) {
@@ -466,11 +543,22 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
-    o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
-      << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
-         "+ dqoff + qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
-    o << in << "  float d" << draw << "[" << E << "];\n#pragma unroll\n" << in
-      << "  for (int e = 0; e < " << E << "; ++e) d" << draw << "[e] = fmaf(ep[e], dws[e], dwl[e]);\n";
+    if (packed) {   // pairs: eps and z = loc + eps * scale on packed instructions
+      o << in << "  mi::f2 ep2[" << E / 2 << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
+        << E / 4 << "; ++qq) mi::guide_normals2(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
+           "+ dqoff + qq * 64 + lane), (unsigned long long)(dpoff + k), ep2[2 * qq], ep2[2 * qq + 1]);\n";
+      o << in << "  float ep[" << E << "], d" << draw << "[" << E << "];\n#pragma unroll\n" << in
+        << "  for (int h = 0; h < " << E / 2 << "; ++h) { const mi::f2 z = mi::fma2(ep2[h], "
+           "mi::f2{dws[2 * h], dws[2 * h + 1]}, mi::f2{dwl[2 * h], dwl[2 * h + 1]}); d" << draw
+        << "[2 * h] = z.x; d" << draw << "[2 * h + 1] = z.y; ep[2 * h] = ep2[h].x; ep[2 * h + 1] = "
+           "ep2[h].y; }\n";
+    } else {
+      o << in << "  float ep[" << E << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
+        << E / 4 << "; ++qq) mi::guide_normals(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
+           "+ dqoff + qq * 64 + lane), (unsigned long long)(dpoff + k), &ep[4 * qq]);\n";
+      o << in << "  float d" << draw << "[" << E << "];\n#pragma unroll\n" << in
+        << "  for (int e = 0; e < " << E << "; ++e) d" << draw << "[e] = fmaf(ep[e], dws[e], dwl[e]);\n";
+    }
     for (int op = 0; op < g.num_operands; ++op)
       if (op != draw && is(op, kDense))
         o << in << "  float d" << op << "[" << E << "];\n" << in
@@ -488,23 +576,46 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
         o << in << "  const bool mp" << st << " = mk" << st << "[k * msk" << st << "] != 0;\n";
     zero_accumulators("      ");
     const char* in2 = "      ";
-    for (int op = 0; op < g.num_operands; ++op)
-      if (dense_grad(op)) o << in2 << "float g" << op << "[" << E << "];\n";
-    o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) {\n";
-    const std::string inner = std::string(in2) + "  ";
-    for (int op = 0; op < g.num_operands; ++op)
-      if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
-    for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, valid, inner.c_str());
-    o << in2 << "}\n";
+    if (packed) {   // element pairs on the packed fp32 instructions
+      for (int op = 0; op < g.num_operands; ++op)
+        if (dense_grad(op)) o << in2 << "mi::f2 g" << op << "[" << E / 2 << "];\n";
+      o << in2 << "#pragma unroll\n" << in2 << "for (int h = 0; h < " << E / 2 << "; ++h) {\n";
+      const std::string inner = std::string(in2) + "  ";
+      for (int op = 0; op < g.num_operands; ++op)
+        if (dense_grad(op)) o << inner << "g" << op << "[h] = mi::splat2(0.0f);\n";
+      for (int st = 0; st < g.num_sites; ++st) emit_site_eval2(o, g, st, valid, inner.c_str());
+      o << in2 << "}\n";
+    } else {
+      for (int op = 0; op < g.num_operands; ++op)
+        if (dense_grad(op)) o << in2 << "float g" << op << "[" << E << "];\n";
+      o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) {\n";
+      const std::string inner = std::string(in2) + "  ";
+      for (int op = 0; op < g.num_operands; ++op)
+        if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
+      for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, valid, inner.c_str());
+      o << in2 << "}\n";
+    }
+    // g<op>[e] of either form
+    auto gel = [&](int op, const char* e) {
+      return packed ? "g" + std::to_string(op) + "[(" + e + ") >> 1][(" + e + ") & 1]"
+                         : "g" + std::to_string(op) + "[" + e + "]";
+    };
     for (int op = 0; op < g.num_operands; ++op) {
       if (!dense_grad(op)) continue;
-      if (op == draw)
+      if (op == draw && packed)
+        o << in2 << "#pragma unroll\n" << in2 << "for (int h = 0; h < " << E / 2
+          << "; ++h) { const mi::f2 a = mi::f2{dal[2 * h], dal[2 * h + 1]} + g" << op
+          << "[h]; const mi::f2 b = mi::fma2(g" << op << "[h], mi::f2{ep[2 * h], ep[2 * h + 1]}, "
+             "mi::f2{das[2 * h], das[2 * h + 1]}); dal[2 * h] = a.x; dal[2 * h + 1] = a.y; "
+             "das[2 * h] = b.x; das[2 * h + 1] = b.y; }\n";
+      else if (op == draw)
         o << in2 << "#pragma unroll\n" << in2 << "for (int e = 0; e < " << E << "; ++e) { dal[e] += g"
           << op << "[e]; das[e] = fmaf(g" << op << "[e], ep[e], das[e]); }\n";
       else
         o << in2 << "{ float* __restrict__ r = gx" << op << " + k * gsk" << op
           << " + base + lane * 4;\n#pragma unroll\n" << in2 << "for (int e = 0; e < " << E
-          << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * g" << op << "[e]; }\n";
+          << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * " << gel(op, "e")
+          << "; }\n";
     }
     emit_particle_sums(in2, plan.block_rows);
     o << in << "}\n";

@@ -16,6 +16,7 @@ struct PlanInfo {
   bool balance;    // ROW: progress-balanced wave priority over the particle loop
   int unroll;      // fused-draw row loop: particles unrolled per iteration (1 = none)
   bool block_rows; // fused-draw row loop: one partial row per block (gridDim.x rows), not per wave
+  bool packed;     // fused-draw row loop: element pairs on packed fp32 math where the families allow
   unsigned grid_x;
   unsigned grid_y;
 };

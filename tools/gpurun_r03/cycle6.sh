@@ -1,0 +1,8 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+run() { local t=$1; shift; local log=$1; shift; timeout -k 10 "$t" "$@" > "gpurun_out/$log" 2>&1; local rc=$?; echo "$log rc=$rc"; return $rc; }
+run 900 r03_tests6.log python -u -m pytest tests -m gpu -v --maxfail=5 --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1
+run 120 r03_adam_default.log python -u tools/adam_probe.py || exit 1
+run 400 r03_bench6.log python -u bench.py || exit 1
+exit 0
