@@ -113,7 +113,8 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
     << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll
-    << (plan.block_rows ? "B" : "") << (use_packed(g, plan) ? "P" : "") << "|"
+    << (plan.block_rows ? "B" : "") << (use_packed(g, plan) ? "P" : "") << "t" << plan.tile_rows
+    << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -265,7 +266,10 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
   // LDS of the row loops' particle sums: nv tiles of [tile_rows][65] floats per wave
-  const int tile_rows = nv <= 2 ? 16 : 8;
+  // (plan.tile_rows overrides: 8 halves the LDS, which caps a 256-thread block at 4 waves / SIMD
+  // with 16 rows and two values)
+  const int tile_rows = plan.tile_rows == 8 || plan.tile_rows == 16 ? plan.tile_rows
+                                                                     : (nv <= 2 ? 16 : 8);
   if (row)
     o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
       << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";

@@ -17,6 +17,7 @@ struct PlanInfo {
   int unroll;      // fused-draw row loop: particles unrolled per iteration (1 = none)
   bool block_rows; // fused-draw row loop: one partial row per block (gridDim.x rows), not per wave
   bool packed;     // fused-draw row loop: element pairs on packed fp32 math where the families allow
+  int tile_rows;   // row loops: particles per LDS tile flush (8 or 16; 0 = by the value count)
   unsigned grid_x;
   unsigned grid_y;
 };

@@ -1203,6 +1203,7 @@ PlanInfo plan_info(const Plan& p, bool combined) {
   // C5's 3907 segments become 977 rows, within the ELBO forward's fused reduction)
   info.block_rows = info.row && p.draw && env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0;
   info.packed = info.row && p.draw && env_int("MININF_AMD_PACKED", 1) != 0;
+  info.tile_rows = env_int("MININF_AMD_TILE_ROWS", 0);
   info.balance = info.row && env_int("MININF_AMD_ROW_BALANCE", 0) != 0;   // measured: no gain on C5 (two rounds of waves, not a lone-wave tail)
   info.kw = p.kw;
   info.grid_x = p.grid.x;
