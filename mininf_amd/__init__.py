@@ -7,7 +7,7 @@ path behind :class:`mininf_amd.nn.EvidenceLowerBoundLoss` runs on hand-written H
 (``mininf_amd/csrc``) through the C ABI declared in ``include/mininf_amd.h``.
 """
 from .core import batch, broadcast_samples, condition, no_log_prob, value, sample, State
-from . import data, nn
+from . import data, nn, optim
 from .data import DeviceDataLoader
 
 

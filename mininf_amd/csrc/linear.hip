@@ -185,6 +185,26 @@ __global__ __launch_bounds__(kLinThreads) void k_linear(const mi_linear L, int k
 // subset), reduced in fp64 by k_finalize as for the VALU kernel.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Phase timestamps (MI_LINEAR_TIMING builds only, tools/linear_timing.py): wall clock at 8 points of
+// every wave of k_linear_mfma, into a buffer behind the launch's workspace.
+#ifndef MI_LINEAR_TIMING
+#define MI_LINEAR_TIMING 0
+#endif
+#if MI_LINEAR_TIMING
+__device__ unsigned long long* mi_lin_tbuf;
+#define MI_LIN_STAMP(i) do { if ((threadIdx.x & 63) == 0) ts_[i] = wall_clock64(); } while (0)
+#else
+#define MI_LIN_STAMP(i) do { } while (0)
+#endif
+
+// x if keep, else +0: a bit mask the compiler cannot see through, so "keep ? load : 0" is not
+// turned back into a branch around the load (and a wait at its join).
+MI_DEV float keep_if(float x, bool keep) {
+  uint32_t m = keep ? 0xffffffffu : 0u;
+  asm volatile("" : "+v"(m));
+  return __uint_as_float(__float_as_uint(x) & m);
+}
+
 template <int PT, int NT>
 struct MfShape {
   static constexpr int NW = NT / kWave;    // waves per block
@@ -212,6 +232,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   using S = MfShape<PT, NT>;
   constexpr int kMfThreads = NT;
   constexpr int kMfWaves = S::NW;
+#if MI_LINEAR_TIMING
+  unsigned long long ts_[8] = {};
+#endif
+  MI_LIN_STAMP(0);
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
@@ -234,14 +258,18 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   const bool per_particle_sigma = FAMILY == MI_NORMAL && L.scale != nullptr;
   uint32_t fl = 0u;
 
-  // B fragment of the first product: theta[k0 + c][2 s + h]
+  // B fragment of the first product: theta[k0 + c][2 s + h]. Branch-free: every load from a
+  // clamped (valid) address, zeroed after -- guarded loads compile to one branch and one exec mask
+  // per load, and a one-stage launch is a single pass through this code.
   float thf[S::HS];
   {
     const int64_t kk = k0 + c;
+    const int64_t kc = kk < K ? kk : K - 1;
 #pragma unroll
     for (int s = 0; s < S::HS; ++s) {
       const int p = 2 * s + h;
-      thf[s] = (kk < K && p < P) ? L.theta[kk * L.theta_stride_k + p * L.theta_stride_j] : 0.0f;
+      const float v = L.theta[kc * L.theta_stride_k + (int64_t)(p < P ? p : P - 1) * L.theta_stride_j];
+      thf[s] = keep_if(v, kk < K && p < P);
     }
   }
 
@@ -267,27 +295,45 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   // ---- staging: X quads and (y, mask) of one stage into registers, then into LDS ---------------
   float4 xq[S::QPT];
   float2 ymr = make_float2(0.0f, 0.0f);
+  // Source rows first (one uniform branch on how rows are given), then every X quad and the
+  // (y, mask) of the stage issued together with no wait in between: a guarded load per quad
+  // compiled to a branch and a wait per load, one memory round trip each.
   auto load_stage = [&](int64_t st) {
     const int64_t row0 = st * S::CH;
+    int64_t src[S::QPT + 1];   // [QPT]: the (y, mask) row of lane tid < CH
+    int64_t rows[S::QPT + 1];
+#pragma unroll
+    for (int q = 0; q < S::QPT; ++q) rows[q] = row0 + (tid + q * kMfThreads) / (S::PM / 4);
+    rows[S::QPT] = row0 + (tid < S::CH ? tid : 0);
+#pragma unroll
+    for (int q = 0; q <= S::QPT; ++q) rows[q] = rows[q] < N ? rows[q] : N - 1;
+    if (gen_rows) {
+#pragma unroll
+      for (int q = 0; q <= S::QPT; ++q) src[q] = (int64_t)grows[ONESTAGE ? (int)(rows[q] - row0) : 0];
+    } else if (L.row_index != nullptr) {
+#pragma unroll
+      for (int q = 0; q <= S::QPT; ++q) src[q] = (int64_t)L.row_index[rows[q]];
+    } else {
+#pragma unroll
+      for (int q = 0; q <= S::QPT; ++q) src[q] = rows[q];
+    }
 #pragma unroll
     for (int q = 0; q < S::QPT; ++q) {
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
-      const int64_t i = row0 + row;
-      const int64_t src = (i < N && gen_rows) ? (int64_t)grows[ONESTAGE ? row : 0]
-                          : (i < N && L.row_index != nullptr) ? L.row_index[i] : i;
-      xq[q] = (i < N && 4 * c4 < P)
-                  ? *reinterpret_cast<const float4*>(L.x + src * L.x_stride_i + 4 * c4)
-                  : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      const float4 v = *reinterpret_cast<const float4*>(L.x + src[q] * L.x_stride_i +
+                                                        4 * (4 * c4 < P ? c4 : 0));
+      const bool in = row0 + row < N && 4 * c4 < P;
+      xq[q] = make_float4(keep_if(v.x, in), keep_if(v.y, in), keep_if(v.z, in), keep_if(v.w, in));
     }
+    const float yv = L.value[src[S::QPT] * L.value_stride_i];
+    const bool mv = L.mask == nullptr ? true : L.mask[src[S::QPT] * L.mask_stride_i] != 0;
     if (tid < S::CH) {
       const int64_t row = row0 + tid;
-      const int64_t i = (row < N && gen_rows) ? (int64_t)grows[ONESTAGE ? tid : 0]
-                        : (row < N && L.row_index != nullptr) ? L.row_index[row] : row;
       float y = 0.0f, m = 0.0f;
       if (row < N) {
-        y = L.value[i * L.value_stride_i];
-        m = (L.mask == nullptr || L.mask[i * L.mask_stride_i] != 0) ? 1.0f : 0.0f;
+        y = yv;
+        m = mv ? 1.0f : 0.0f;
         const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
         fl |= (m != 0.0f && bad) ? MI_FLAG_SUPPORT : 0u;
       }
@@ -375,11 +421,14 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       }
       __syncthreads();
     }
+    MI_LIN_STAMP(1);
     if (st0 < st1) {
       load_stage(st0);
       store_stage();
     }
+    MI_LIN_STAMP(2);
     __syncthreads();
+    MI_LIN_STAMP(3);
     if (st0 < st1) {
       const int ntl = (S::TILES - rs + rs_count - 1) / rs_count;
 #pragma unroll 1
@@ -399,6 +448,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
         }
       }
     }
+    MI_LIN_STAMP(4);
     __syncthreads();
   }
   if (!ONESTAGE && st0 < st1) {
@@ -485,6 +535,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       val[r * PT + t] = grads ? (float)(v * w) : 0.0f;
     }
   }
+  MI_LIN_STAMP(5);
   const bool combine = rs_count > 1 && (rs_count - 1) * wt * kWave * kItems <= S::CH * S::RSTR;
   int64_t tile_id = row_block * rs_count + rs;
   if (combine) {
@@ -505,6 +556,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
     tile_id = row_block;
   }
+  MI_LIN_STAMP(6);
   if (!combine || rs == 0) {
     if (h == 0 && k0 + c < K) {
       part[tile_id * K + k0 + c] = val[16 * PT];
@@ -525,6 +577,13 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   }
   publish_flags(flags, fl);
+  MI_LIN_STAMP(7);
+#if MI_LINEAR_TIMING
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* o = mi_lin_tbuf + ((int64_t)blockIdx.x * (NT / 64) + threadIdx.x / 64) * 8;
+    for (int i = 0; i < 8; ++i) o[i] = ts_[i];
+  }
+#endif
   // the last block to finish advances the batch counter: every block has read it by then. (A
   // count taken right after the read instead made all blocks hit one address at once: measured
   // slower.)
@@ -711,6 +770,9 @@ int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes) {
   if (!valid(site) || bytes == nullptr) return MI_EINVAL;
   const Geometry g = geometry(site);
   *bytes = partial_bytes(site, g) + mi_finalize_scratch_bytes(g.ntile, site->K, g.nv);
+#if MI_LINEAR_TIMING
+  *bytes = (*bytes + 255) / 256 * 256 + (size_t)g.gx * g.gy * 8 * 8 * sizeof(unsigned long long);
+#endif
   return 0;
 }
 
@@ -741,6 +803,16 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
   if (site->rows.counter != nullptr && (!g.mfma || g.stages_per_block != 1))
     return MI_EUNSUPPORTED;   // rows drawn only by one-stage matrix-core launches
   float* part = static_cast<float*>(workspace);
+#if MI_LINEAR_TIMING
+  {
+    unsigned long long* tb = reinterpret_cast<unsigned long long*>(
+        static_cast<char*>(workspace) +
+        (partial_bytes(site, g) + mi_finalize_scratch_bytes(g.ntile, site->K, g.nv) + 255) / 256 * 256);
+    if ((e = hipMemcpyToSymbolAsync(HIP_SYMBOL(mi::mi_lin_tbuf), &tb, sizeof(tb), 0,
+                                    hipMemcpyHostToDevice, s)) != hipSuccess)
+      return to_code(e);
+  }
+#endif
   if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
     return to_code(e);
   if (site->family == MI_NORMAL)

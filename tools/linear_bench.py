@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--valu", action="store_true")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--only", default=None, help="run one shape (C3, C3-bern, C4, P64)")
+    ap.add_argument("--gather", choices=("none", "seq", "random"), default="none",
+                    help="rows through mi_linear.row_index over a 10M-row X: sequential or random")
     ap.add_argument("--shape", action="append", default=[],
                     help="extra N,P,K shape (Normal); repeatable")
     args = ap.parse_args()
@@ -40,16 +42,25 @@ def main():
             continue
         if args.only not in (None, "__shapes__") and name != args.only:
             continue
-        X = torch.randn(N, P, device=dev)
+        if args.gather == "none":
+            X = torch.randn(N, P, device=dev)
+            rows = None
+        else:
+            X = torch.randn(10_000_000, P, device=dev)
+            rows = (torch.arange(N, device=dev, dtype=torch.int32) if args.gather == "seq" else
+                    torch.randperm(10_000_000, device=dev)[:N].to(torch.int32))
         theta = 0.3 * torch.randn(K, P, device=dev)
-        y = torch.randn(N, device=dev) if fam == nat.NORMAL else \
-            (torch.rand(N, device=dev) < 0.5).float()
+        ny = X.shape[0]
+        y = torch.randn(ny, device=dev) if fam == nat.NORMAL else \
+            (torch.rand(ny, device=dev) < 0.5).float()
         L = nat.Linear()
         L.K, L.N, L.P, L.family = K, N, P, fam
         L.options = nat.LINEAR_VALU if args.valu else 0
         L.x, (L.x_stride_i, L.x_stride_j) = X.data_ptr(), X.stride()
         L.theta, (L.theta_stride_k, L.theta_stride_j) = theta.data_ptr(), theta.stride()
         L.value, L.value_stride_i = y.data_ptr(), 1
+        if rows is not None:
+            L.row_index = rows.data_ptr()
         L.scale_constant, L.grad_scale, L.site_scale, L.compute_grads = 1.0, -1.0 / K, 1.0, 1
         size = ctypes.c_size_t()
         nat.check(lib.mi_linear_workspace_bytes(ctypes.byref(L), ctypes.byref(size)), "ws")
@@ -71,7 +82,7 @@ def main():
         torch.cuda.synchronize()
         ms = sum(a.elapsed_time(b) for a, b in times) / len(times)
         tf = 4 * P * K * N / (ms * 1e-3) / 1e12
-        print(f"{name:8s} N={N} P={P} K={K}: {ms * 1e3:8.1f} us  {tf:6.1f} TFLOP/s "
+        print(f"{name:8s} gather={args.gather} N={N} P={P} K={K}: {ms * 1e3:8.1f} us  {tf:6.1f} TFLOP/s "
               f"({tf / 157.3:.3f} of 157.3)", flush=True)
 
 
