@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 9
+#define MI_ABI_VERSION 10
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -148,6 +148,20 @@ typedef struct mi_side {
   double* out;
 } mi_side;
 
+/* A one-element-per-particle site folded into a group's launch (replaces the prior site's own launch
+ * of the README model, README.md:43-47, `sample("theta", Beta(2, 2))`): its value is operand
+ * sites[0].operand[0] of the group -- the per-particle parameter of the group's site, e.g. the
+ * coin's theta -- its parameters are constants, and its scale is sites[0].scale. Its log-density
+ * joins site 0's value, d log p / d value joins that operand's slot gradient, and its validation
+ * bits go to *flags. Only the Bernoulli BCAST kernel carries it
+ * (mi_group_prior_supported); mi_group_forward returns MI_EUNSUPPORTED otherwise. */
+typedef struct mi_prior {
+  int32_t present;       /* 0: no folded prior site */
+  int32_t family;        /* MI_BETA (c1, c0), MI_NORMAL (loc, scale) or MI_GAMMA (conc., rate) */
+  float constant[2];
+  uint32_t* flags;       /* the prior site's validation word (MI_FLAG_*) */
+} mi_prior;
+
 /* A group of sites evaluated over one shared [K, N] element space in a single pass, so that an
  * operand read by several sites (e.g. a latent z that is the value of one site and the loc of
  * another) is loaded once and its gradient accumulated in registers. */
@@ -164,6 +178,7 @@ typedef struct mi_group {
   mi_operand operands[MI_MAX_OPERANDS];
   mi_draw draw;          /* draw.operand == 0: no operand is a fused guide draw */
   mi_side side;          /* side.out == NULL: no side job */
+  mi_prior prior;        /* prior.present == 0: no folded prior site */
 } mi_group;
 
 /* Library identification: returns MI_ABI_VERSION and writes the offload target ("gfx950"). */
@@ -177,6 +192,10 @@ int mi_struct_sizes(size_t* operand, size_t* site, size_t* group);
 /* *supported = 1 when mi_group_forward runs `group`'s side job (the Bernoulli BCAST kernel over
  * unmasked contiguous data carries it), else 0: the caller then computes the factors elsewhere. */
 int mi_group_side_supported(const mi_group* group, int* supported);
+
+/* *supported = 1 when mi_group_forward evaluates `group`'s folded prior site (mi_prior), else 0:
+ * the caller then launches that site on its own. */
+int mi_group_prior_supported(const mi_group* group, int* supported);
 
 /* Workspace needed by mi_group_forward for this descriptor. */
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);

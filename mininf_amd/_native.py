@@ -37,7 +37,7 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 9   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 10   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -78,6 +78,11 @@ class Side(ctypes.Structure):
                 ("c0_stride", c_i64), ("K", c_i64), ("N", c_i64), ("out", c_vp)]
 
 
+class Prior(ctypes.Structure):
+    _fields_ = [("present", ctypes.c_int32), ("family", ctypes.c_int32),
+                ("constant", ctypes.c_float * 2), ("flags", c_vp)]
+
+
 class Group(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("N", c_i64),
@@ -85,7 +90,7 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
-        ("draw", Draw), ("side", Side),
+        ("draw", Draw), ("side", Side), ("prior", Prior),
     ]
 
 
@@ -231,6 +236,8 @@ _SIGNATURES = {
     "mi_step_begin": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
     "mi_group_side_supported": (ctypes.c_int, [ctypes.POINTER(Group),
                                                ctypes.POINTER(ctypes.c_int)]),
+    "mi_group_prior_supported": (ctypes.c_int, [ctypes.POINTER(Group),
+                                                ctypes.POINTER(ctypes.c_int)]),
     "mi_transform_params": (ctypes.c_int, [ctypes.POINTER(Params), c_vp, c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),

@@ -105,6 +105,15 @@ MI_DEV void guide_normals(uint64_t seed, uint64_t step, uint32_t stream_id, uint
   box_muller(b.z, b.w, out[2], out[3]);
 }
 
+// x if keep, else +0, through a bit mask the compiler cannot see through: "keep ? load : 0" is
+// otherwise turned back into a branch around the load, with a wait for it at the join -- a chain
+// of such loads then costs one memory round trip each instead of one for all.
+MI_DEV float keep_if(float x, bool keep) {
+  uint32_t m = keep ? 0xffffffffu : 0u;
+  asm volatile("" : "+v"(m));
+  return __uint_as_float(__float_as_uint(x) & m);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Wavefront reductions.
 // ---------------------------------------------------------------------------------------------

@@ -68,6 +68,45 @@ MI_DEV double factor_entropy(const mi_factor& f, int64_t i) {
          (double)((b - 1.0f) * digammaf(b));
 }
 
+// The element's two parameters, loaded together up front (a missing one reads as 1): the entropy
+// derivatives and the exp-transform chain rule below then wait for one round trip, not three.
+struct Params2 {
+  float p0, p1;
+};
+MI_DEV Params2 load_params(const mi_factor& f, int64_t i) {
+  // (a Normal's loc only feeds its exp transform)
+  const bool has0 = f.param[0] != nullptr &&
+                    (f.family != MI_NORMAL || f.transform[0] == MI_TRANSFORM_EXP);
+  const float* a = has0 ? f.param[0] + i * f.stride[0] : f.param[1] + i * f.stride[1];
+  const float v0 = *a, v1 = f.param[1][i * f.stride[1]];
+  return Params2{has0 ? v0 : 1.0f, v1};
+}
+
+// entropy_grad from loaded parameters
+MI_DEV void entropy_grad_of(const mi_factor& f, const Params2& q, double& d0, double& d1) {
+  if (f.family == MI_NORMAL) {
+    d0 = 0.0;
+    d1 = (double)(1.0f / q.p1);
+    return;
+  }
+  if (f.family == MI_GAMMA) {
+    d0 = (double)(1.0f + (1.0f - q.p0) * trigammaf(q.p0));
+    d1 = (double)(-1.0f / q.p1);
+    return;
+  }
+  const float t = q.p0 + q.p1;
+  const float tt = (t - 2.0f) * trigammaf(t);
+  d0 = (double)(tt - (q.p0 - 1.0f) * trigammaf(q.p0));
+  d1 = (double)(tt - (q.p1 - 1.0f) * trigammaf(q.p1));
+}
+
+// write_grad from loaded parameters
+MI_DEV void write_grad_of(const mi_factor& F, int j, int64_t i, double g, const Params2& q) {
+  if (F.grad[j] == nullptr) return;
+  if (F.transform[j] == MI_TRANSFORM_EXP) g *= (double)(j == 0 ? q.p0 : q.p1);
+  F.grad[j][i * F.grad_stride[j]] = (float)g;
+}
+
 // dH(i) / dparam_j. Normal: (0, 1 / scale); Beta: (a0 - 2) psi'(a0) - (a - 1) psi'(a) and the
 // same with b.
 MI_DEV void entropy_grad(const mi_factor& f, int64_t i, double& d0, double& d1) {
@@ -157,11 +196,15 @@ MI_DEV void write_grad(const mi_factor& F, int j, int64_t i, double g) {
 }
 
 // d T / d z[k, i] summed over the sources (fp32, as autograd accumulates the groups' gradients).
+// Branch-free: every slot reads (source 0 stands in for the unused ones) and the unused terms are
+// +0 -- the loads of several rows can then be in flight together.
 MI_DEV float source_sum(const mi_factor& F, int64_t k, int64_t i) {
   float g = 0.0f;
 #pragma unroll
-  for (int s = 0; s < MI_MAX_SOURCES; ++s)
-    if (s < F.num_sources) g += F.source[s].ptr[k * F.source[s].stride_k + i * F.source[s].stride_i];
+  for (int s = 0; s < MI_MAX_SOURCES; ++s) {
+    const mi_source& S = F.source[s < F.num_sources ? s : 0];
+    g += keep_if(S.ptr[k * S.stride_k + i * S.stride_i], s < F.num_sources);
+  }
   return g;
 }
 
@@ -184,9 +227,9 @@ MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int64_t k = k0 + (int64_t)u * tk;
-        g[u] = k < r1 ? source_sum(F, k, i) : 0.0f;
-        d[u] = k < r1 ? *reinterpret_cast<const double2*>(F.dgrad + 2 * (k * n + i))
-                      : make_double2(0.0, 0.0);
+        const int64_t kc = k < r1 ? k : r1 - 1;
+        g[u] = keep_if(source_sum(F, kc, i), k < r1);
+        d[u] = *reinterpret_cast<const double2*>(F.dgrad + 2 * (kc * n + i));
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -217,19 +260,30 @@ MI_DEV void draw_sums(const mi_factor& F, int64_t i, int64_t r0, int64_t r1, int
   } else if (F.family == MI_NORMAL) {
     uint64_t step = F.step;
     if (F.step_device != nullptr) step += *F.step_device;
-    for (int64_t k = r0; k < r1; k += tk) {
-      const float g = source_sum(F, k, i);
-      float e;
-      if (F.eps != nullptr) {
-        e = F.eps[k * n + i];
-      } else {
-        float q[4];
-        guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
-                      (uint64_t)(F.particle_offset + k), q);
-        e = q[i & 3];
+    // four rows' loads (sources, eps) in flight per lane, then the sums in row order
+    constexpr int kU = 4;
+    for (int64_t k0 = r0; k0 < r1; k0 += kU * (int64_t)tk) {
+      float g[kU], e[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t k = k0 + (int64_t)u * tk;
+        const int64_t kc = k < r1 ? k : r1 - 1;
+        g[u] = keep_if(source_sum(F, kc, i), k < r1);
+        if (F.eps != nullptr) {
+          e[u] = F.eps[kc * n + i];
+        } else {
+          float q[4];
+          guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
+                        (uint64_t)(F.particle_offset + kc), q);
+          e[u] = q[i & 3];
+        }
       }
-      s0 += (double)g;
-      s1 += (double)g * (double)e;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (k0 + (int64_t)u * tk >= r1) break;
+        s0 += (double)g[u];
+        s1 += (double)g[u] * (double)e[u];
+      }
     }
   }
 }
@@ -400,9 +454,10 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   if (tk == 1 && slices == 1) {   // a lane per element: no block reduction, and no barrier
                                   // between its loads
     if (i < F.n) {
+      const Params2 q = load_params(F, i);   // in flight during the draw sums
       draw_sums<FORWARD>(F, i, r0, r1, 1, s0, s1);
       double d0, d1;
-      entropy_grad(F, i, d0, d1);
+      entropy_grad_of(F, q, d0, d1);
       if (FORWARD) {
         double* pre = F.saved + 4 * i;
         pre[0] = s0;
@@ -410,12 +465,14 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
         pre[2] = d0;
         pre[3] = d1;
       } else {
-        write_grad(F, 0, i, (double)u * s0 + w * d0);
-        write_grad(F, 1, i, (double)u * s1 + w * d1);
+        write_grad_of(F, 0, i, (double)u * s0 + w * d0, q);
+        write_grad_of(F, 1, i, (double)u * s1 + w * d1, q);
       }
     }
     return;
   }
+  // the element's parameters, in flight during the sums (the lanes that finish the element)
+  const Params2 q = load_params(F, i < F.n ? i : F.n - 1);
   if (i < F.n) draw_sums<FORWARD>(F, i, r0 + ty, r1, tk, s0, s1);
   red[threadIdx.x][0] = s0;
   red[threadIdx.x][1] = s1;
@@ -459,7 +516,7 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   }
   if (ty == 0 && i < F.n) {
     double d0, d1;
-    entropy_grad(F, i, d0, d1);
+    entropy_grad_of(F, q, d0, d1);
     if (FORWARD) {
       double* pre = F.saved + 4 * i;
       pre[0] = s0;
@@ -467,8 +524,8 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
       pre[2] = d0;
       pre[3] = d1;
     } else {
-      write_grad(F, 0, i, (double)u * s0 + w * d0);
-      write_grad(F, 1, i, (double)u * s1 + w * d1);
+      write_grad_of(F, 0, i, (double)u * s0 + w * d0, q);
+      write_grad_of(F, 1, i, (double)u * s1 + w * d1, q);
     }
   }
   if (counter != nullptr && threadIdx.x == 0) *counter = 0u;
@@ -571,6 +628,13 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
   const int64_t kc = k < K ? k : K - 1;
   double* lds = &red[0][0];   // [kRedG][kRedK] doubles
   double t = 0.0;
+  // the tails' factors of this lane's particle, fetched ahead of the reduction that decides whether
+  // they are needed (a load behind that test costs a round trip of its own at the end)
+  double2 tdg[kMaxTails];
+#pragma unroll
+  for (int q = 0; q < kMaxTails; ++q)
+    tdg[q] = (q < R.tails && gl == 0) ? *reinterpret_cast<const double2*>(pick(R.tail_dgrad, q) + 2 * kc)
+                                      : make_double2(0.0, 0.0);
   for (int v = v0; v < v1; ++v) {
     // rank-one values (mi_reduce.rank1): the particle-independent u[seg], then f[k] u + e[k]
     const bool r1 = (J.rank1 >> v) & 1;
@@ -618,9 +682,8 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
 #pragma unroll
         for (int q = 0; q < kMaxTails; ++q)
           if (((mask >> q) & 1) && gv != 0.0f) {   // a zero upstream never meets the factor
-            const double2 d = *reinterpret_cast<const double2*>(pick(R.tail_dgrad, q) + 2 * k);
-            c[q][0] += (double)gv * d.x;
-            c[q][1] += (double)gv * d.y;
+            c[q][0] += (double)gv * tdg[q].x;
+            c[q][1] += (double)gv * tdg[q].y;
           }
       }
     }
@@ -729,13 +792,19 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       for (int q = 0; q < kMaxTails; ++q) {
         const int mask = q < R.tails ? R.tail_ext[q] : 0;
         if (mask == 0) continue;
+        // every source slot and the factor read unconditionally (an unused slot reads the first
+        // used one and adds +0): one memory round trip instead of one per load
+        const int on0 = __builtin_ctz((unsigned)mask);
         for (int64_t k = first; k < E.K; k += stride) {
           float g = 0.0f;
 #pragma unroll
-          for (int src = 0; src < MI_MAX_SOURCES; ++src)
-            if ((mask >> src) & 1) g += R.tail_src[q][src][k * R.tail_src_stride[q][src]];
-          if (g == 0.0f) continue;   // a zero upstream never meets the factor
+          for (int src = 0; src < MI_MAX_SOURCES; ++src) {
+            const bool on = (mask >> src) & 1;
+            const int sc = on ? src : on0;
+            g += keep_if(R.tail_src[q][sc][k * R.tail_src_stride[q][sc]], on);
+          }
           const double2 d = *reinterpret_cast<const double2*>(R.tail_dgrad[q] + 2 * k);
+          if (g == 0.0f) continue;   // a zero upstream never meets the factor
           c[q][0] += (double)g * d.x;
           c[q][1] += (double)g * d.y;
         }
@@ -851,10 +920,11 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_backward(const mi_elbo E,
     const mi_factor& F = E.factors[f];
     if (F.draw_kind != MI_DRAW_NONE) continue;
     for (int64_t i = first; i < F.n; i += stride) {
+      const Params2 q = load_params(F, i);
       double d0, d1;
-      entropy_grad(F, i, d0, d1);
-      write_grad(F, 0, i, w * F.weight * d0);
-      write_grad(F, 1, i, w * F.weight * d1);
+      entropy_grad_of(F, q, d0, d1);
+      write_grad_of(F, 0, i, w * F.weight * d0, q);
+      write_grad_of(F, 1, i, w * F.weight * d1, q);
     }
   }
   if (u == 1.0f) return;  // the site groups' gradients were computed for exactly this upstream

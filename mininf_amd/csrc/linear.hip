@@ -197,14 +197,6 @@ __device__ unsigned long long* mi_lin_tbuf;
 #define MI_LIN_STAMP(i) do { } while (0)
 #endif
 
-// x if keep, else +0: a bit mask the compiler cannot see through, so "keep ? load : 0" is not
-// turned back into a branch around the load (and a wait at its join).
-MI_DEV float keep_if(float x, bool keep) {
-  uint32_t m = keep ? 0xffffffffu : 0u;
-  asm volatile("" : "+v"(m));
-  return __uint_as_float(__float_as_uint(x) & m);
-}
-
 template <int PT, int NT>
 struct MfShape {
   static constexpr int NW = NT / kWave;    // waves per block

@@ -756,6 +756,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
                          ? G.operands[o_a].slot : -1;
   const float w = (float)st.scale;
   const int64_t extra = nseg - 1;
+  uint32_t fl_prior = 0u;
   float* slot_part = part + (int64_t)(1 + slot_a) * nseg * K;   // (slot_a >= 0)
   if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0) slot_part[c] = s_a;   // u[c]
 #pragma unroll
@@ -770,9 +771,21 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       const double softplus = (double)(fmaxf(l, 0.0f) + log1pf(t));
       const double sig = (double)(l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t));
       const double n = (double)G.N;
-      part[extra * K + k] = (float)(-n * softplus);
+      // the folded prior site (mi_prior): log p(a_k) and d/da_k of the per-particle parameter a_k
+      float prior_lp = 0.0f, prior_d = 0.0f;
+      if (G.prior.present != 0) {
+        const float a = role_scalar(G, st, 0, k);
+        Elem pe;
+        if (G.prior.family == MI_BETA) eval_beta(G.prior.constant[0], G.prior.constant[1], a, pe);
+        else if (G.prior.family == MI_NORMAL) eval_normal(G.prior.constant[0], G.prior.constant[1], a, pe);
+        else eval_gamma(G.prior.constant[0], G.prior.constant[1], a, pe);
+        prior_lp = pe.lp;
+        prior_d = pe.d[2];
+        fl_prior |= (pe.param_bad ? MI_FLAG_PARAM : 0u) | (pe.support_bad ? MI_FLAG_SUPPORT : 0u);
+      }
+      part[extra * K + k] = (float)(-n * softplus) + prior_lp;
       if (slot_a >= 0) {
-        const float e = w * (float)(-n * sig * (double)dl[p]);
+        const float e = w * (float)(-n * sig * (double)dl[p]) + w * prior_d;
         if (rank1) {
           slot_part[nseg + k] = w * dl[p];       // f[k]
           slot_part[nseg + K + k] = e;           // e[k]
@@ -784,6 +797,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   }
   if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0 && c == 0) slot_part[extra] = 0.0f;
   publish_flags(flags, fl);
+  if (G.prior.present != 0) publish_flags(G.prior.flags, fl_prior);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1030,6 +1044,10 @@ bool validate_group(const mi_group* g) {
   if (g->side.out != nullptr &&
       (g->side.x == nullptr || g->side.c1 == nullptr || g->side.c0 == nullptr || g->side.K < 1 ||
        g->side.N < 1))
+    return false;
+  if (g->prior.present != 0 &&
+      ((g->prior.family != MI_BETA && g->prior.family != MI_NORMAL && g->prior.family != MI_GAMMA) ||
+       g->prior.flags == nullptr || g->sites[0].operand[0] < 0))
     return false;
   for (int o = 0; o < g->num_operands; ++o) {
     const mi_operand& op = g->operands[o];
@@ -1339,6 +1357,16 @@ int mi_group_side_supported(const mi_group* group, int* supported) {
   return 0;
 }
 
+int mi_group_prior_supported(const mi_group* group, int* supported) {
+  if (!validate_group(group) || supported == nullptr) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  // the BCAST kernel's one site, its per-particle parameter an operand (stride_i == 0)
+  const int o = group->sites[0].operand[0];
+  *supported = (p.shape == kBcast && bcast_smem(group) && group->num_sites == 1 && o >= 0 &&
+                group->operands[o].stride_i == 0) ? 1 : 0;
+  return 0;
+}
+
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
   if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -1373,6 +1401,8 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   hipError_t e = hipSuccess;
   if (!(group->options & MI_GROUP_FLAGS_ZEROED)) {
     e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
+    if (e == hipSuccess && group->prior.present != 0)
+      e = hipMemsetAsync(group->prior.flags, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return to_code(e);
   }
   const mi_group G = *group;
@@ -1385,6 +1415,11 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   float* prep = reinterpret_cast<float*>(static_cast<char*>(workspace) + prep_offset(group, p));
   if (group->draw.operand != 0 && (p.shape != kRow || !draw_supported(group))) return MI_EUNSUPPORTED;
   if (group->side.out != nullptr && !(p.shape == kBcast && bcast_smem(group))) return MI_EUNSUPPORTED;
+  if (group->prior.present != 0) {
+    int ok = 0;
+    mi_group_prior_supported(group, &ok);
+    if (!ok) return MI_EUNSUPPORTED;
+  }
   float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
   const bool smem = p.shape == kBcast && bcast_smem(group);
   if (p.shape == kBcast && !smem) {

@@ -177,6 +177,14 @@ class _GroupLauncher:
         # result of the last run, or None when the group's kernel cannot carry the job
         self.side: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         self.side_out: Optional[torch.Tensor] = None
+        # a one-element prior site folded into this launch (mi_prior, fold_priors): (site, family
+        # code, (constant, constant)); its validation word follows the group's own
+        self.prior: Optional[Tuple[SiteRecord, int, Tuple[float, float]]] = None
+
+    @property
+    def flag_sites(self) -> List[SiteRecord]:
+        """The sites whose validation words this launch writes, in word order."""
+        return [site for site, _, _ in self.sites] + ([self.prior[0]] if self.prior else [])
 
     def try_add(self, site: SiteRecord, views: List[_View], mask: Optional[_View]) -> bool:
         constants = [v.constant for v in views]
@@ -333,6 +341,10 @@ class _GroupLauncher:
                 desc.mask = mask.tensor.data_ptr()
                 desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
             desc.scale = site.scale
+        if self.prior is not None:
+            pr = group.prior
+            pr.present, pr.family = 1, self.prior[1]
+            pr.constant[0], pr.constant[1] = self.prior[2]
         return group, grads
 
     def source(self) -> str:
@@ -372,6 +384,12 @@ class _GroupLauncher:
         K, N = self.K, self.N
         self.exp_pending = None
         group, grads = self.describe(compute_grads, fuse_exp=True)
+        if flags is None:
+            flags = torch.empty(len(self.flag_sites), dtype=torch.int32, device=device)
+        else:
+            group.options |= nat.GROUP_FLAGS_ZEROED
+        if self.prior is not None:   # its word after the group's own
+            group.prior.flags = flags.data_ptr() + 4 * len(self.sites)
         size = ctypes.c_size_t()
         lib = nat.lib()
         nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
@@ -399,10 +417,6 @@ class _GroupLauncher:
         site_lp = torch.empty((len(self.sites), K), dtype=torch.float64, device=device) \
             if self.per_site else None
         slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
-        if flags is None:
-            flags = torch.empty(len(self.sites), dtype=torch.int32, device=device)
-        else:
-            group.options |= nat.GROUP_FLAGS_ZEROED
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
@@ -855,6 +869,53 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
     return [launcher for _, launcher in groups], categorical
 
 
+_PRIOR_FAMILIES = ("beta", "normal", "gamma")
+
+
+def fold_priors(launchers: List[_GroupLauncher]) -> List[_GroupLauncher]:
+    """
+    Fold one-element-per-particle prior sites into the launch of the site that reads the same
+    per-particle tensor as its parameter (``mi_prior``; the README model's ``theta ~ Beta(2, 2)``
+    under ``x ~ Bernoulli(theta)``, README.md:43-47): the prior's log density and its gradient are
+    evaluated by that launch's particle-constant workgroups instead of a launch of their own.
+    Only when the library's kernel for the host group carries it (``mi_group_prior_supported``)
+    and both sites have the same scale; MININF_AMD_FOLD_PRIOR=0 disables it.
+    """
+    if os.environ.get("MININF_AMD_FOLD_PRIOR", "1") == "0":
+        return launchers
+    out = list(launchers)
+    lib = nat.lib()
+    for prior in launchers:
+        if len(prior.sites) != 1 or prior.N != 1 or prior.draw is not None or prior.per_site:
+            continue
+        site, roles, mask = prior.sites[0]
+        if mask is not None or site.family not in _PRIOR_FAMILIES or roles[0][0] != -1 or \
+                roles[1][0] != -1 or roles[2][0] < 0:
+            continue
+        value = prior.operands[roles[2][0]]
+        for host in out:
+            if host is prior or len(host.sites) != 1 or host.prior is not None or host.per_site:
+                continue
+            hsite, hroles, _ = host.sites[0]
+            if hroles[0][0] < 0 or hsite.scale != site.scale:
+                continue
+            param = host.operands[hroles[0][0]]
+            if param.view.key != value.view.key or param.mode != value.mode:
+                continue
+            host.prior = (site, FAMILY_CODES[site.family], (roles[0][1], roles[1][1]))
+            group, _ = host.describe(True)
+            group.prior.flags = 1 << 20   # (any non-null word: only the plan is queried)
+            supported = ctypes.c_int(0)
+            nat.check(lib.mi_group_prior_supported(ctypes.byref(group), ctypes.byref(supported)),
+                      "mi_group_prior_supported")
+            if not supported.value:
+                host.prior = None
+                continue
+            out.remove(prior)
+            break
+    return out
+
+
 def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint:
     """
     Launch the site kernels for every recorded site and return the per-particle log joint.
@@ -878,7 +939,7 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
     for launcher in launchers:
         holder = {}
         totals.append(_SiteGroupFn.apply(launcher, holder, *launcher.inputs()))
-        pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
+        pending.append(("group", holder, launcher.flag_sites))
     for _, value in trace.fallback:
         totals.append(value.to(device=device, dtype=torch.float32))
     if totals:
@@ -1258,7 +1319,7 @@ class _ElboPlan:
         deferred: List[Tuple[nat.Reduce, torch.Tensor]] = []   # finalize reductions left to us
         # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
         sizes = [1] * (len(self.categorical) + len(self.linears)) + \
-            [len(l.sites) for l in self.launchers]
+            [len(l.flag_sites) for l in self.launchers]
         words = max(1, sum(sizes))
         zeroed, self.zeroed_flags = self.zeroed_flags, None   # zero only for the first forward
         if zeroed is not None and zeroed.numel() >= words:
@@ -1279,8 +1340,8 @@ class _ElboPlan:
             job = side_jobs[0] if side_jobs else None
             launcher.side = None if job is None else (
                 job.drawn.base.reshape(self.K, job.drawn.N), job.drawn.conc)
-            part = self.flags[cursor:cursor + len(launcher.sites)]
-            cursor += len(launcher.sites)
+            part = self.flags[cursor:cursor + len(launcher.flag_sites)]
+            cursor += len(launcher.flag_sites)
             total, site_lp, grads, slot_grad, flags = launcher.run(need, part, defer=True)
             if launcher.reduce is not None:
                 deferred.append((launcher.reduce, total))
@@ -1572,6 +1633,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         if not bad:
             break
         _materialize_draws(trace, bad)
+    launchers = fold_priors(launchers)
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
@@ -1583,7 +1645,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     for linear, holder in zip(linears, plan.lin_holders):
         pending.append(("linear", holder, [linear.site]))
     for launcher, holder in zip(launchers, plan.holders):
-        pending.append(("group", holder, [site for site, _, _ in launcher.sites]))
+        pending.append(("group", holder, launcher.flag_sites))
     joint = LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)
     if mirror is not None and plan.flags is not None and plan.flags.numel() <= mirror.numel():
         joint.mirror = mirror[:plan.flags.numel()]
