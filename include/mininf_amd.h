@@ -159,6 +159,7 @@ typedef struct mi_prior {
   int32_t present;       /* 0: no folded prior site */
   int32_t family;        /* MI_BETA (c1, c0), MI_NORMAL (loc, scale) or MI_GAMMA (conc., rate) */
   float constant[2];
+  double scale;          /* the prior site's scale (a group's: equal to sites[0].scale) */
   uint32_t* flags;       /* the prior site's validation word (MI_FLAG_*) */
 } mi_prior;
 
@@ -510,7 +511,14 @@ typedef struct mi_linear {
   mi_rows rows;           /* rows.counter non-NULL (row_index NULL): the site draws its batch's
                              rows itself; only the matrix-core kernel with one row stage per
                              block does (else MI_EUNSUPPORTED: launch mi_minibatch_rows first) */
+  mi_prior prior;         /* prior.present: a site over theta itself ([K, P], every element; the
+                             regression's `theta ~ Normal(0, 1)`, examples/minibatch.md:45-50)
+                             evaluated by this launch: its log density joins the site's total,
+                             d log p / d theta joins dslots (mi_linear_prior_supported) */
 } mi_linear;
+
+/* *supported = 1 when mi_linear_forward evaluates `site`'s folded prior (the matrix-core kernel). */
+int mi_linear_prior_supported(const mi_linear* site, int* supported);
 
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes);
 int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,

@@ -80,7 +80,7 @@ class Side(ctypes.Structure):
 
 class Prior(ctypes.Structure):
     _fields_ = [("present", ctypes.c_int32), ("family", ctypes.c_int32),
-                ("constant", ctypes.c_float * 2), ("flags", c_vp)]
+                ("constant", ctypes.c_float * 2), ("scale", ctypes.c_double), ("flags", c_vp)]
 
 
 class Group(ctypes.Structure):
@@ -112,7 +112,7 @@ class Linear(ctypes.Structure):
         ("scale_constant", ctypes.c_float), ("grad_scale", ctypes.c_float),
         ("site_scale", ctypes.c_double),
         ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
-        ("row_index", c_vp), ("rows", Rows),
+        ("row_index", c_vp), ("rows", Rows), ("prior", Prior),
     ]
 
 
@@ -238,6 +238,8 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_int)]),
     "mi_group_prior_supported": (ctypes.c_int, [ctypes.POINTER(Group),
                                                 ctypes.POINTER(ctypes.c_int)]),
+    "mi_linear_prior_supported": (ctypes.c_int, [ctypes.POINTER(Linear),
+                                                 ctypes.POINTER(ctypes.c_int)]),
     "mi_transform_params": (ctypes.c_int, [ctypes.POINTER(Params), c_vp, c_vp]),
     "mi_beta_rsample_backward_workspace_bytes": (ctypes.c_int, [
         c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),

@@ -569,6 +569,35 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     }
   }
   publish_flags(flags, fl);
+  // The folded prior site over theta itself (mi_linear.prior): the first row block's first row
+  // subset of every particle tile already holds theta[k0 + c][2 s + h] in thf -- no load -- and
+  // writes the prior's value and d/dtheta as the slab's last tile.
+  if (L.prior.present != 0 && row_block == 0 && rs == 0) {
+    const int64_t kk = k0 + c;
+    const int64_t ptile = ntile - 1;
+    uint32_t pfl = 0u;
+    float plp = 0.0f;
+#pragma unroll
+    for (int s = 0; s < S::HS; ++s) {
+      const int p = 2 * s + h;
+      if (kk < K && p < P) {
+        Elem e;
+        if (L.prior.family == MI_BETA) eval_beta(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+        else if (L.prior.family == MI_NORMAL) eval_normal(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+        else eval_gamma(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+        plp += e.lp;
+        pfl |= (e.param_bad ? MI_FLAG_PARAM : 0u) | (e.support_bad ? MI_FLAG_SUPPORT : 0u);
+        if (grads) part[((int64_t)(1 + p) * ntile + ptile) * K + kk] = (float)(L.prior.scale * (double)e.d[2]);
+      }
+    }
+    plp += __shfl_xor(plp, 32, kWave);   // the particle's two feature parities
+    if (h == 0 && kk < K) {
+      // the reduction scales the value row by the site's scale
+      part[ptile * K + kk] = (float)((double)plp * L.prior.scale / L.site_scale);
+      if (per_particle_sigma && grads) part[((int64_t)(1 + P) * ntile + ptile) * K + kk] = 0.0f;
+    }
+    publish_flags(L.prior.flags, pfl);
+  }
   MI_LIN_STAMP(7);
 #if MI_LINEAR_TIMING
   if ((threadIdx.x & 63) == 0) {
@@ -601,6 +630,10 @@ bool valid(const mi_linear* L) {
         L->N > R.batch || (R.batches - 1) * R.batch >= R.n || R.batches * R.batch >= R.n + R.batch)
       return false;
   }
+  if (L != nullptr && L->prior.present != 0 &&
+      ((L->prior.family != MI_BETA && L->prior.family != MI_NORMAL && L->prior.family != MI_GAMMA) ||
+       L->prior.flags == nullptr || !(L->site_scale != 0.0)))
+    return false;
   return L != nullptr && L->K >= 1 && L->N >= 1 && L->P >= 1 && L->P <= MI_LINEAR_MAX_P &&
          (L->family == MI_NORMAL || L->family == MI_BERNOULLI_LOGITS) && L->x != nullptr &&
          L->theta != nullptr && L->value != nullptr;
@@ -673,7 +706,7 @@ Geometry geometry(const mi_linear* L) {
     const int items = 16 * g.pt + 2;
     const int64_t lds_floats = ch * (32 * g.pt + 4);
     const bool combine = rs_count > 1 && (int64_t)(rs_count - 1) * wt * 64 * items <= lds_floats;
-    g.ntile = combine ? g.gx : g.gx * rs_count;
+    g.ntile = (combine ? g.gx : g.gx * rs_count) + (L->prior.present != 0 ? 1 : 0);
     return g;
   }
   int kb = 1;
@@ -758,6 +791,12 @@ int mi_linear_struct_size(size_t* bytes) {
   return 0;
 }
 
+int mi_linear_prior_supported(const mi_linear* site, int* supported) {
+  if (!valid(site) || supported == nullptr) return MI_EINVAL;
+  *supported = geometry(site).mfma ? 1 : 0;
+  return 0;
+}
+
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes) {
   if (!valid(site) || bytes == nullptr) return MI_EINVAL;
   const Geometry g = geometry(site);
@@ -789,9 +828,12 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
   hipError_t e;
   if (!(site->options & MI_GROUP_FLAGS_ZEROED)) {
     e = hipMemsetAsync(flags, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && site->prior.present != 0)
+      e = hipMemsetAsync(site->prior.flags, 0, sizeof(uint32_t), s);
     if (e != hipSuccess) return to_code(e);
   }
   const Geometry g = geometry(site);
+  if (site->prior.present != 0 && !g.mfma) return MI_EUNSUPPORTED;   // (the VALU kernel has none)
   if (site->rows.counter != nullptr && (!g.mfma || g.stages_per_block != 1))
     return MI_EUNSUPPORTED;   // rows drawn only by one-stage matrix-core launches
   float* part = static_cast<float*>(workspace);

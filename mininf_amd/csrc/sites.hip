@@ -1363,7 +1363,8 @@ int mi_group_prior_supported(const mi_group* group, int* supported) {
   // the BCAST kernel's one site, its per-particle parameter an operand (stride_i == 0)
   const int o = group->sites[0].operand[0];
   *supported = (p.shape == kBcast && bcast_smem(group) && group->num_sites == 1 && o >= 0 &&
-                group->operands[o].stride_i == 0) ? 1 : 0;
+                group->operands[o].stride_i == 0 &&
+                group->prior.scale == group->sites[0].scale) ? 1 : 0;
   return 0;
 }
 

@@ -345,6 +345,7 @@ class _GroupLauncher:
             pr = group.prior
             pr.present, pr.family = 1, self.prior[1]
             pr.constant[0], pr.constant[1] = self.prior[2]
+            pr.scale = self.prior[0].scale
         return group, grads
 
     def source(self) -> str:
@@ -561,12 +562,19 @@ class _LinearLauncher:
             self.sigma_input = sigma.tensor[:, :1]
         self.value = value
         self.mask = mask
-        self.sites = [(site, None, mask)]   # flag layout: one word
+        self.sites = [(site, None, mask)]   # flag layout: one word (+ the folded prior's)
+        # a prior site over theta itself folded into this launch (mi_linear.prior,
+        # fold_linear_priors): (site, family code, (constant, constant))
+        self.prior: Optional[Tuple[SiteRecord, int, Tuple[float, float]]] = None
         # decided here, outside the autograd Function (whose forward runs with grad disabled)
         grad_on = torch.is_grad_enabled()
         self.theta_grad = grad_on and theta.requires_grad
         self.sigma_grad = grad_on and self.sigma_input is not None and \
             self.sigma_input.requires_grad
+
+    @property
+    def flag_sites(self) -> List[SiteRecord]:
+        return [self.site] + ([self.prior[0]] if self.prior else [])
 
     def needs_grads(self) -> bool:
         return self.theta_grad or self.sigma_grad
@@ -574,7 +582,12 @@ class _LinearLauncher:
     def inputs(self) -> List[Optional[torch.Tensor]]:
         return [self.theta, self.sigma_input]
 
-    def describe(self, compute_grads: bool, draw_rows: bool = True) -> nat.Linear:
+    def describe(self, compute_grads: bool, draw_rows: bool = True,
+                 query: bool = False) -> nat.Linear:
+        """
+        The ``mi_linear`` descriptor. ``query``: for a support query only -- a minibatch's rows
+        are neither drawn nor taken (the descriptor reads the dataset's first rows).
+        """
         L = nat.Linear()
         L.K, L.N, L.P = self.K, self.N, self.P
         L.family = FAMILY_CODES[self.site.family]
@@ -582,7 +595,10 @@ class _LinearLauncher:
         L.x_stride_i, L.x_stride_j = self.X_src.stride()
         L.theta = self.theta.data_ptr()
         L.theta_stride_k, L.theta_stride_j = self.theta.stride()
-        if self.batch is not None:
+        if self.batch is not None and query:
+            L.value = self.value_src.data_ptr()
+            L.value_stride_i = self.value_src.stride(0)
+        elif self.batch is not None:
             # the batch's rows: drawn by this kernel when nothing has drawn them yet (one launch
             # less per step), else read through the row index
             R = self.batch.take_rows() if draw_rows else None
@@ -609,14 +625,25 @@ class _LinearLauncher:
         L.grad_scale = self.g0
         L.site_scale = self.site.scale
         L.compute_grads = int(compute_grads)
+        if self.prior is not None:
+            pr = L.prior
+            pr.present, pr.family = 1, self.prior[1]
+            pr.constant[0], pr.constant[1] = self.prior[2]
+            pr.scale = self.prior[0].scale
         return L
 
     def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None,
             defer: bool = False):
         device = self.device
         L = self.describe(compute_grads)
+        if flags is None:
+            flags = torch.empty(len(self.flag_sites), dtype=torch.int32, device=device)
+        else:
+            L.options |= nat.GROUP_FLAGS_ZEROED
         size = ctypes.c_size_t()
         lib = nat.lib()
+        if self.prior is not None:   # its word after the site's
+            L.prior.flags = flags.data_ptr() + 4
         nat.check(lib.mi_linear_workspace_bytes(ctypes.byref(L), ctypes.byref(size)),
                   "mi_linear_workspace_bytes")
         workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
@@ -624,10 +651,6 @@ class _LinearLauncher:
         nslots = self.P + (1 if L.scale else 0)
         dslots = torch.empty((nslots, self.K), dtype=torch.float32, device=device) \
             if compute_grads else None
-        if flags is None:
-            flags = torch.empty(1, dtype=torch.int32, device=device)
-        else:
-            L.options |= nat.GROUP_FLAGS_ZEROED
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
@@ -642,7 +665,10 @@ class _LinearLauncher:
         code = launch(L)
         if L.rows.counter:
             if code == nat.MI_EUNSUPPORTED:   # this launch shape does not draw rows: draw first
+                zeroed, prior_flags = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags
                 L = self.describe(compute_grads, draw_rows=False)
+                L.options |= zeroed
+                L.prior.flags = prior_flags
                 code = launch(L)
             elif code == 0:
                 self.batch.rows_taken()
@@ -916,6 +942,47 @@ def fold_priors(launchers: List[_GroupLauncher]) -> List[_GroupLauncher]:
     return out
 
 
+def fold_linear_priors(launchers: List[_GroupLauncher],
+                       linears: List["_LinearLauncher"]) -> List[_GroupLauncher]:
+    """
+    Fold a prior site over a linear site's theta itself (every element, constant parameters: the
+    regression's ``theta ~ Normal(0, 1)``, examples/minibatch.md:45-50) into the linear launch
+    (``mi_linear.prior``): the first row block's workgroups evaluate it from the theta fragment
+    they already hold, so the prior has no launch of its own. MININF_AMD_FOLD_PRIOR=0 disables it.
+    """
+    if os.environ.get("MININF_AMD_FOLD_PRIOR", "1") == "0" or not linears:
+        return launchers
+    out = list(launchers)
+    lib = nat.lib()
+    for prior in launchers:
+        if len(prior.sites) != 1 or prior.draw is not None or prior.per_site:
+            continue
+        site, roles, mask = prior.sites[0]
+        if mask is not None or site.family not in _PRIOR_FAMILIES or roles[0][0] != -1 or \
+                roles[1][0] != -1 or roles[2][0] < 0:
+            continue
+        value = prior.operands[roles[2][0]]
+        t = value.view.tensor
+        for linear in linears:
+            theta = linear.theta
+            if linear.prior is not None or prior.N != linear.P or t is None or \
+                    t.data_ptr() != theta.data_ptr() or (value.view.sk, value.view.si) != \
+                    tuple(theta.stride()) or (value.mode == nat.GRAD_DENSE) != linear.theta_grad:
+                continue
+            linear.prior = (site, FAMILY_CODES[site.family], (roles[0][1], roles[1][1]))
+            L = linear.describe(True, query=True)
+            L.prior.flags = 1 << 20   # (any non-null word: only the launch shape is queried)
+            supported = ctypes.c_int(0)
+            nat.check(lib.mi_linear_prior_supported(ctypes.byref(L), ctypes.byref(supported)),
+                      "mi_linear_prior_supported")
+            if not supported.value:
+                linear.prior = None
+                continue
+            out.remove(prior)
+            break
+    return out
+
+
 def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint:
     """
     Launch the site kernels for every recorded site and return the per-particle log joint.
@@ -935,7 +1002,7 @@ def log_joint(trace: ParticleTrace, g0: float, device: torch.device) -> LogJoint
     for linear in linears:
         holder = {}
         totals.append(_LinearSiteFn.apply(linear, holder, *linear.inputs()))
-        pending.append(("linear", holder, [linear.site]))
+        pending.append(("linear", holder, linear.flag_sites))
     for launcher in launchers:
         holder = {}
         totals.append(_SiteGroupFn.apply(launcher, holder, *launcher.inputs()))
@@ -1318,7 +1385,7 @@ class _ElboPlan:
         results = []
         deferred: List[Tuple[nat.Reduce, torch.Tensor]] = []   # finalize reductions left to us
         # one zeroed flag buffer for every site of the step, in `pending` order (categorical first)
-        sizes = [1] * (len(self.categorical) + len(self.linears)) + \
+        sizes = [1] * len(self.categorical) + [len(l.flag_sites) for l in self.linears] + \
             [len(l.flag_sites) for l in self.launchers]
         words = max(1, sum(sizes))
         zeroed, self.zeroed_flags = self.zeroed_flags, None   # zero only for the first forward
@@ -1326,7 +1393,7 @@ class _ElboPlan:
             self.flags = zeroed[:words]
         else:
             self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
-        cursor = len(self.categorical) + len(self.linears)
+        cursor = len(self.categorical) + sum(len(l.flag_sites) for l in self.linears)
         # absorbed Beta draws whose implicit-gradient factors a site launch can carry (mi_side)
         side_jobs = [plan for plan in self.absorbed.values()
                      if plan.drawn is not None and plan.drawn.family == guide.BETA_FAMILY and
@@ -1384,8 +1451,10 @@ class _ElboPlan:
         lin_results = []
         base = len(self.categorical)
         for j, (linear, holder) in enumerate(zip(self.linears, self.lin_holders)):
+            words = len(linear.flag_sites)
             total, dslots, flags = linear.run(linear.needs_grads(),
-                                              self.flags[base + j:base + j + 1], defer=True)
+                                              self.flags[base:base + words], defer=True)
+            base += words
             if linear.reduce is not None:
                 deferred.append((linear.reduce, total))
             holder["flags"] = flags
@@ -1633,7 +1702,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         if not bad:
             break
         _materialize_draws(trace, bad)
-    launchers = fold_priors(launchers)
+    launchers = fold_linear_priors(fold_priors(launchers), linears)
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
@@ -1643,7 +1712,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):
         pending.append(("categorical", holder, [site]))
     for linear, holder in zip(linears, plan.lin_holders):
-        pending.append(("linear", holder, [linear.site]))
+        pending.append(("linear", holder, linear.flag_sites))
     for launcher, holder in zip(launchers, plan.holders):
         pending.append(("group", holder, launcher.flag_sites))
     joint = LogJoint(total=loss, pending=pending, checks=trace.checks, flags=plan.flags)

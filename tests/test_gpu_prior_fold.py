@@ -96,3 +96,53 @@ def test_folded_prior_reports_its_own_support(device, monkeypatch):
     loss_fn = EvidenceLowerBoundLoss(num_particles=K, seed=1)
     with pytest.raises(ValueError, match="'theta'"):
         loss_fn(mininf_amd.condition(model, x=x), {"theta": guide()})
+
+
+def _regression(device, monkeypatch, fold, minibatch):
+    """C3 / C4-shaped regression (examples/minibatch.md): theta ~ Normal(0, 1) under the fused
+    linear site, over a device minibatch when `minibatch`."""
+    monkeypatch.setenv("MININF_AMD_FOLD_PRIOR", "1" if fold else "0")
+    gen = torch.Generator().manual_seed(5)
+    n, p, K = 8192, 32, 64
+    X = torch.randn(n, p, generator=gen)
+    y = X @ torch.randn(p, generator=gen) + torch.randn(n, generator=gen)
+    X, y = X.to(device), y.to(device)
+
+    def model():
+        theta = mininf_amd.sample("theta", Normal(0, 1), sample_shape=p)
+        with mininf_amd.batch(n):
+            with mininf_amd.no_log_prob():
+                Xs = mininf_amd.sample("X", Normal(0, 1), sample_shape=(n, p))
+            mininf_amd.sample("y", Normal(Xs @ theta, 1))
+
+    guide = ParameterizedDistribution(Normal, loc=torch.zeros(p), scale=torch.ones(p)).to(device)
+    loss_fn = EvidenceLowerBoundLoss(num_particles=K, seed=2)
+    if minibatch:
+        loader = mininf_amd.DeviceDataLoader(X, y, batch_size=1024, shuffle=True, drop_last=True,
+                                             seed=7)
+        Xb, yb = loader.next()
+    else:
+        Xb, yb = X, y
+    loss = loss_fn(mininf_amd.condition(model, X=Xb, y=yb), {"theta": guide()})
+    loss.backward()
+    torch.cuda.synchronize()
+    return float(loss), [q.grad.clone() for q in guide.parameters()]
+
+
+@pytest.mark.parametrize("minibatch", [False, True])
+def test_folded_linear_prior_matches_separate_launch(device, monkeypatch, minibatch):
+    folds = []
+    real = engine.fold_linear_priors
+
+    def spy(launchers, linears):
+        out = real(launchers, linears)
+        folds.append([l.prior is not None for l in linears])
+        return out
+
+    monkeypatch.setattr(engine, "fold_linear_priors", spy)
+    lf, gf = _regression(device, monkeypatch, True, minibatch)
+    assert folds == [[True]]
+    lu, gu = _regression(device, monkeypatch, False, minibatch)
+    assert lf == pytest.approx(lu, rel=1e-6)
+    for a, b in zip(gf, gu):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
