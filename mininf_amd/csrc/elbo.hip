@@ -585,33 +585,6 @@ MI_DEV void lds_tree(double* lds, int n) {
   }
 }
 
-// Block partials (c0, c1) of the tails from per-lane contributions (fixed-order wave sums, then the
-// waves in order); thread 0 stores them.
-MI_DEV void tail_partials(const ReducePlan& R, int bid, int nshare, const double (&c)[kMaxTails][2],
-                          double (*red)[2], double* work) {
-  constexpr int kWaves = kElboThreads / kWave;
-  double* lds = &red[0][0];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < kMaxTails; ++t)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const double v = wave_sum(c[t][q]);
-      if (lane == 0) lds[(t * 2 + q) * kWaves + wave] = v;
-    }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int t = 0; t < R.tails; ++t)
-      for (int q = 0; q < 2; ++q) {
-        double v = 0.0;
-        for (int w = 0; w < kWaves; ++w) v += lds[(t * 2 + q) * kWaves + w];
-        __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + bid) * 2 + q], v,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-  __syncthreads();
-}
-
 // Writes job J's outputs for one block's particles (local block `local` of the job) and returns
 // g0 * the sum of its (fp32) totals (0 from blocks that do not write totals): the block's share of
 // the loss.
@@ -640,6 +613,13 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
     const bool r1 = (J.rank1 >> v) & 1;
     const float* __restrict__ p = J.part + (int64_t)v * J.nseg * K + (r1 ? 0 : kc);
     const int64_t stride = r1 ? 1 : K;
+    // the rank-one factors of this lane's particle, fetched with the segments (not after them)
+    float r1f = 0.0f, r1e = 0.0f;
+    if (r1 && gl == 0) {
+      const float* __restrict__ q = J.part + (int64_t)v * J.nseg * K + J.nseg;
+      r1f = q[kc];
+      r1e = q[K + kc];
+    }
     double acc = 0.0;
     int64_t g = gl;
     // sixteen loads in flight per lane (a C2-sized list, ~250 segments over 8 groups, is two
@@ -666,10 +646,7 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
     if (gl == 0 && k < K) {
       double s = 0.0;
       for (int j = 0; j < kRedG; ++j) s += lds[j * kRedK + kl];
-      if (r1) {
-        const float* __restrict__ q = J.part + (int64_t)v * J.nseg * K + J.nseg;
-        s = (double)q[k] * s + (double)q[K + k];
-      }
+      if (r1) s = (double)r1f * s + (double)r1e;
       if (v < J.num_sites) {
         s *= pick(J.scale, v);
         if (J.site_lp != nullptr) J.site_lp[(int64_t)v * K + k] = s;
@@ -718,6 +695,21 @@ MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
   return share;
 }
 
+// Phase timestamps (MI_ELBO_TIMING builds only, tools/elbo_timing.py): wall clock at 6 points of
+// every block of k_elbo_forward (thread 0), into a buffer the timing build allocates.
+#ifndef MI_ELBO_TIMING
+#define MI_ELBO_TIMING 0
+#endif
+#if MI_ELBO_TIMING
+__device__ unsigned long long* mi_elbo_tbuf;
+#define MI_ELBO_STAMP(i) do { if (threadIdx.x == 0) ets_[i] = wall_clock64(); } while (0)
+#define MI_ELBO_FLUSH() do { if (threadIdx.x == 0) { unsigned long long* o = mi_elbo_tbuf + (int64_t)blockIdx.x * 8; \
+    for (int q = 0; q < 8; ++q) o[q] = ets_[q]; } } while (0)
+#else
+#define MI_ELBO_STAMP(i) do { } while (0)
+#define MI_ELBO_FLUSH() do { } while (0)
+#endif
+
 // ---- forward --------------------------------------------------------------------------------
 // HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
 // of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
@@ -732,6 +724,10 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                                                float* __restrict__ loss) {
   __shared__ double red[kElboThreads][2];
   __shared__ bool last;
+#if MI_ELBO_TIMING
+  unsigned long long ets_[8] = {};
+#endif
+  MI_ELBO_STAMP(0);
   const int nred = R.first[R.num];
   const int nloss = P.lead_blocks;
   const int nshare = nred + nloss;   // blocks that write a loss share
@@ -811,8 +807,40 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       }
     }
   }
-  if (!ABSORB && R.tails > 0) tail_partials(R, (int)blockIdx.x, nshare, c, red, work);
-  const double s = block_sum(share, rsum);
+  MI_ELBO_STAMP(1);
+  // the block's share and its tail partials in one pass: wave sums, then the waves in order
+  // through LDS, one barrier (thread 0 stores the tail partials and returns the share)
+  double s;
+  {
+    constexpr int kWaves = kElboThreads / kWave;
+    constexpr int kVals = 1 + 2 * kMaxTails;
+    __shared__ double wsum[kVals][kWaves];
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const double v0 = wave_sum(share);
+    if (lane == 0) wsum[0][wave] = v0;
+    const int tails = ABSORB ? 0 : R.tails;
+#pragma unroll
+    for (int t = 0; t < kMaxTails; ++t)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (t < tails) {
+          const double v = wave_sum(c[t][q]);
+          if (lane == 0) wsum[1 + 2 * t + q][wave] = v;
+        }
+    __syncthreads();
+    s = 0.0;
+    if (threadIdx.x == 0) {
+      for (int w = 0; w < kWaves; ++w) s += wsum[0][w];
+      for (int t = 0; t < tails; ++t)
+        for (int q = 0; q < 2; ++q) {
+          double v = 0.0;
+          for (int w = 0; w < kWaves; ++w) v += wsum[1 + 2 * t + q][w];
+          __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + blockIdx.x) * 2 + q], v,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+  }
+  MI_ELBO_STAMP(2);
   if (threadIdx.x == 0) {
     // The shares (and the slot gradients the tail reads) are device-coherent stores, complete
     // (s_waitcnt) before the barrier / the counter update: no per-block L2 write-back fence,
@@ -831,15 +859,44 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     }
     last = done && atomicAdd(counters, 1u) == (unsigned)(ngroups > 1 ? ngroups : nshare) - 1u;
   }
+  MI_ELBO_STAMP(3);
   __syncthreads();
-  if (!last) return;
+  if (!last) {
+    MI_ELBO_FLUSH();
+    return;
+  }
   // the last block adds the shares: each thread a fixed strided subset, then a fixed-order block
-  // sum -- deterministic, and no serial chain of dependent loads
+  // sum -- deterministic, and no serial chain of dependent loads. Every load of this phase (shares,
+  // the tails' partials and concentrations, the validation words, the generator step) is issued
+  // before the first sum: one memory round trip instead of one per stage.
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double t = 0.0;
-  for (int b = threadIdx.x; b < nshare; b += kElboThreads)
+  double acc[kMaxTails][2] = {};
+  for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
     t += __hip_atomic_load(&work[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ABSORB) {
+#pragma unroll
+      for (int q = 0; q < kMaxTails; ++q) {
+        if (q >= R.tails) break;
+        const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
+        acc[q][0] += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[q][1] += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  float tc1[kMaxTails] = {}, tc0[kMaxTails] = {};
+  if (!ABSORB) {
+#pragma unroll
+    for (int q = 0; q < kMaxTails; ++q)
+      if (q < R.tails) {
+        tc1[q] = *R.tail_c1[q];
+        tc0[q] = *R.tail_c0[q];
+      }
+  }
+  const uint32_t fw0 = (int64_t)threadIdx.x < E.nflags ? E.flags[threadIdx.x] : 0u;
+  const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
   const double total = block_sum(t, rsum + kElboThreads / kWave);
+  MI_ELBO_STAMP(4);
   if (threadIdx.x == 0) {
     *loss = (float)total;
     *counters = 0u;
@@ -850,35 +907,32 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       if (q >= R.tails) break;
       // both sums through one fixed-order tree (red[][0] and red[][1]); the three trigammas of the
       // entropy derivatives on lanes 0-2 meanwhile
-      double acc0 = 0.0, acc1 = 0.0;
-      for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
-        const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
-        acc0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      const float a = *R.tail_c1[q], b = *R.tail_c0[q];
+      const float a = tc1[q], b = tc0[q];
       const float tsum = a + b;
       const float tg = threadIdx.x == 0 ? trigammaf(tsum)
                        : threadIdx.x == 1 ? trigammaf(a)
                        : threadIdx.x == 2 ? trigammaf(b) : 0.0f;
-      __syncthreads();
-      red[threadIdx.x][0] = acc0;
-      red[threadIdx.x][1] = acc1;
+      // wave sums, then the waves in order (fixed order, one barrier)
+      const double w0 = wave_sum(acc[q][0]), w1 = wave_sum(acc[q][1]);
+      __shared__ double tws[2][kElboThreads / kWave];
       __shared__ float tgs[3];
+      const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+      if (lane == 0) {
+        tws[0][wave] = w0;
+        tws[1][wave] = w1;
+      }
       if (threadIdx.x < 3) tgs[threadIdx.x] = tg;
       __syncthreads();
-      for (int half = kElboThreads >> 1; half > 0; half >>= 1) {
-        if ((int)threadIdx.x < half) {
-          red[threadIdx.x][0] += red[threadIdx.x + half][0];
-          red[threadIdx.x][1] += red[threadIdx.x + half][1];
-        }
-        __syncthreads();
-      }
       if (threadIdx.x == 0) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
+        double s0 = 0.0, s1 = 0.0;
+        for (int w = 0; w < kElboThreads / kWave; ++w) {
+          s0 += tws[0][w];
+          s1 += tws[1][w];
+        }
         const float tt = (tsum - 2.0f) * tgs[0];
         double* pre = R.tail_saved[q];
-        pre[0] = red[0][0];
-        pre[1] = red[0][1];
+        pre[0] = s0;
+        pre[1] = s1;
         pre[2] = (double)(tt - (a - 1.0f) * tgs[1]);
         pre[3] = (double)(tt - (b - 1.0f) * tgs[2]);
       }
@@ -887,12 +941,15 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   }
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=
                     MI_ELBO_COUNTER_BYTES / sizeof(unsigned), "counter area");
-  for (int64_t i = threadIdx.x; i < E.nflags; i += kElboThreads) E.flags_mirror[i] = E.flags[i];
+  if ((int64_t)threadIdx.x < E.nflags) E.flags_mirror[threadIdx.x] = fw0;
+  for (int64_t i = threadIdx.x + kElboThreads; i < E.nflags; i += kElboThreads)
+    E.flags_mirror[i] = E.flags[i];
   if (threadIdx.x == 0 && E.step_counter != nullptr) {
-    const uint64_t c = *E.step_counter;
-    *E.step_snapshot = c;
-    *E.step_counter = c + 1;
+    *E.step_snapshot = step0;
+    *E.step_counter = step0 + 1;
   }
+  MI_ELBO_STAMP(5);
+  MI_ELBO_FLUSH();
 }
 
 // ---- backward -------------------------------------------------------------------------------
@@ -1217,7 +1274,20 @@ int to_code(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 }  // namespace
 
+#if MI_ELBO_TIMING
+static unsigned long long* mi_elbo_timing_last = nullptr;
+#endif
+
 extern "C" {
+
+#if MI_ELBO_TIMING
+// Copy the stamps of the last k_elbo_forward (8 per block) to the host (timing builds only).
+int mi_elbo_timing_read(void* host, size_t bytes) {
+  if (mi_elbo_timing_last == nullptr) return MI_EINVAL;
+  return hipMemcpy(host, mi_elbo_timing_last, bytes < (8u << 20) ? bytes : (8u << 20),
+                   hipMemcpyDeviceToHost) == hipSuccess ? 0 : MI_EINVAL;
+}
+#endif
 
 int mi_elbo_struct_sizes(size_t* factor, size_t* elbo) {
   if (factor == nullptr || elbo == nullptr) return MI_EINVAL;
@@ -1258,6 +1328,15 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
   for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family != MI_NORMAL;
   const dim3 grid((unsigned)(L.red.first[L.red.num] + L.fwd.lead_blocks + L.fwd.first[L.fwd.num]));
   hipStream_t s = static_cast<hipStream_t>(stream);
+#if MI_ELBO_TIMING
+  {
+    static unsigned long long* tb = nullptr;
+    if (tb == nullptr && hipMalloc(&tb, 8 << 20) != hipSuccess) return MI_EWORKSPACE;
+    hipMemsetAsync(tb, 0, 8 << 20, s);
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(mi::mi_elbo_tbuf), &tb, sizeof(tb), 0, hipMemcpyHostToDevice, s);
+    mi_elbo_timing_last = tb;
+  }
+#endif
   const dim3 block(mi::kElboThreads);
   if (L.fwd.num > 0)
     hipLaunchKernelGGL((mi::k_elbo_forward<true, true>), grid, block, 0, s, *elbo, L.fwd, L.red,
