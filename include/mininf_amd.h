@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 10
+#define MI_ABI_VERSION 11
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -515,6 +515,15 @@ typedef struct mi_linear {
                              regression's `theta ~ Normal(0, 1)`, examples/minibatch.md:45-50)
                              evaluated by this launch: its log density joins the site's total,
                              d log p / d theta joins dslots (mi_linear_prior_supported) */
+  mi_draw draw;           /* draw.operand != 0: theta is the guide's Normal draw, made by this launch
+                             instead of a mi_normal_rsample launch before it (FactorizedDistribution
+                             .rsample, nn.py:133-145): theta[k, j] = loc[j] + eps * scale[j] with the
+                             eps of mi_normal_rsample (same seed, step, stream, particle_offset + k,
+                             element_offset + j; bit-identical values), scale = expf(scale_exp[j])
+                             when scale_exp is non-NULL (then also written to scale, as
+                             mi_normal_rsample_exp). `theta` is not read; every element of it is
+                             written by the launch. dloc / dscale unused. Matrix-core kernel only,
+                             P % 4 == 0 (else MI_EUNSUPPORTED: launch mi_normal_rsample first). */
 } mi_linear;
 
 /* *supported = 1 when mi_linear_forward evaluates `site`'s folded prior (the matrix-core kernel). */

@@ -37,7 +37,7 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 10   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 11   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -112,7 +112,7 @@ class Linear(ctypes.Structure):
         ("scale_constant", ctypes.c_float), ("grad_scale", ctypes.c_float),
         ("site_scale", ctypes.c_double),
         ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
-        ("row_index", c_vp), ("rows", Rows), ("prior", Prior),
+        ("row_index", c_vp), ("rows", Rows), ("prior", Prior), ("draw", Draw),
     ]
 
 

@@ -56,14 +56,35 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(path) <= built for path in SOURCES + HEADERS)
 
 
+OBJ = os.path.join(HERE, "_obj")   # per-source objects (git- and gpurun-ignored)
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
     """
-    Compile the HIP sources into ``mininf_amd/libmininf_amd.so`` unless it is up to date.
+    Compile the HIP sources into ``mininf_amd/libmininf_amd.so`` unless it is up to date: one
+    object per source, compiled in parallel (a source is recompiled when it or any header is newer
+    than its object), then linked.
     """
     write_embedded()
     if not force and up_to_date():
         return TARGET
-    command = [HIPCC, *FLAGS, "-o", TARGET, *SOURCES, *LIBS]
+    os.makedirs(OBJ, exist_ok=True)
+    headers = max(os.path.getmtime(path) for path in HEADERS)
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    jobs, objects = [], []
+    for source in SOURCES:
+        obj = os.path.join(OBJ, os.path.basename(source) + ".o")
+        objects.append(obj)
+        if force or not os.path.exists(obj) or \
+                os.path.getmtime(obj) < max(headers, os.path.getmtime(source)):
+            command = [HIPCC, *compile_flags, "-c", "-o", obj, source]
+            if verbose:
+                print(" ".join(command), file=sys.stderr)
+            jobs.append(subprocess.Popen(command))
+    failed = [job.args[-1] for job in jobs if job.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc {' '.join(failed)}")
+    command = [HIPCC, *FLAGS, "-o", TARGET, *objects, *LIBS]
     if verbose:
         print(" ".join(command), file=sys.stderr)
     subprocess.run(command, check=True)

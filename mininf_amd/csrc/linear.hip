@@ -208,6 +208,37 @@ struct MfShape {
   static constexpr int QPT = CH * PM / 4 / NT;   // float4 loads per thread per stage
 };
 
+// theta drawn by the launch (mi_linear.draw): the block's particles [kbase, kbase + nk) into LDS rows
+// dst[(k - kbase) * dstr + j], one work item per (particle, feature quad) -- the normals of
+// k_normal_rsample for the same (particle, element quad) and the same fmaf, so the values are
+// bit-identical to the separate draw. The first row block also writes them to theta (every
+// particle group its own particles) and, for an exp-transformed scale, group 0 writes the scale.
+template <int NT>
+__device__ __forceinline__ void draw_theta(const mi_linear& L, int64_t kbase, int nk, float* dst,
+                                           int dstr, bool write_theta, bool write_scale) {
+  const mi_draw& D = L.draw;
+  const uint64_t step = D.step + (D.step_device != nullptr ? *D.step_device : 0ull);
+  const int nq = (int)L.P / 4;
+  const bool exp_scale = D.scale_exp != nullptr;
+  for (int item = threadIdx.x; item < nk * nq; item += NT) {
+    const int kl = item / nq, q = item - kl * nq;
+    const int64_t kk = kbase + kl;
+    float e[4];
+    guide_normals(D.seed, step, D.stream_id, (uint64_t)(D.element_offset / 4 + q),
+                  (uint64_t)(D.particle_offset + kk), e);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = 4 * q + j;
+      const float m = D.loc[i * D.loc_stride];
+      const float sd = exp_scale ? expf(D.scale_exp[i * D.scale_stride]) : D.scale[i * D.scale_stride];
+      const float z = fmaf(e[j], sd, m);
+      dst[kl * dstr + i] = z;
+      if (write_theta) const_cast<float*>(L.theta)[kk * L.theta_stride_k + i * L.theta_stride_j] = z;
+      if (write_scale && exp_scale && kl == 0) const_cast<float*>(D.scale)[i * D.scale_stride] = sd;
+    }
+  }
+}
+
 // Grid: one dimension of gx * gy blocks, gx (row blocks) a multiple of 8. Blocks are dealt to the
 // 8 XCDs round-robin, so block b's row block is chosen such that the gy particle groups of one row
 // block run on one XCD (b, b + 8, ...) and share its L2 copy of the X rows.
@@ -254,7 +285,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   // clamped (valid) address, zeroed after -- guarded loads compile to one branch and one exec mask
   // per load, and a one-stage launch is a single pass through this code.
   float thf[S::HS];
-  {
+  // theta drawn here (mi_linear.draw): into the X staging buffer after the first stage's loads are
+  // issued, then into thf (draw_here below)
+  const bool drawn = L.draw.operand != 0;
+  if (!drawn) {
     const int64_t kk = k0 + c;
     const int64_t kc = kk < K ? kk : K - 1;
 #pragma unroll
@@ -344,6 +378,24 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     if (tid < S::CH) yms[tid] = ymr;
   };
 
+  // The block's particles' draws through the (still unused) X staging buffer into thf: called by
+  // every thread after the first stage's loads are issued and before they are stored.
+  constexpr int kDrawStride = S::PM + 1;   // odd row stride: lanes c read distinct banks
+  auto draw_here = [&]() {
+    const int64_t kbase = group * wt * 32;
+    const int nk = (int)min((int64_t)wt * 32, K - kbase);
+    draw_theta<kMfThreads>(L, kbase, nk, xs, kDrawStride, row_block == 0, row_block == 0 && group == 0);
+    __syncthreads();
+    const int kl = pt * 32 + c;
+    const int klc = kl < nk ? kl : nk - 1;
+#pragma unroll
+    for (int s = 0; s < S::HS; ++s) {
+      const int p = 2 * s + h;
+      thf[s] = keep_if(xs[klc * kDrawStride + (p < P ? p : P - 1)], kl < nk && p < P);
+    }
+    __syncthreads();
+  };
+
   // MU = X theta^T for the tile's 32 rows and this wave's 32 particles
   auto gemm1 = [&](int tile) -> f32x16 {
     f32x16 mu = f32x16{};
@@ -414,10 +466,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       __syncthreads();
     }
     MI_LIN_STAMP(1);
-    if (st0 < st1) {
-      load_stage(st0);
-      store_stage();
-    }
+    if (st0 < st1) load_stage(st0);
+    if (drawn) draw_here();
+    if (st0 < st1) store_stage();
     MI_LIN_STAMP(2);
     __syncthreads();
     MI_LIN_STAMP(3);
@@ -443,10 +494,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     MI_LIN_STAMP(4);
     __syncthreads();
   }
-  if (!ONESTAGE && st0 < st1) {
-    load_stage(st0);
-    store_stage();
-  }
+  if (!ONESTAGE && st0 < st1) load_stage(st0);
+  if (!ONESTAGE && drawn) draw_here();
+  if (!ONESTAGE && st0 < st1) store_stage();
   if (!ONESTAGE) __syncthreads();
   for (int64_t st = st0; !ONESTAGE && st < st1; ++st) {
     if (st + 1 < st1) load_stage(st + 1);   // in flight during this stage's MFMAs
@@ -836,6 +886,17 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
   if (site->prior.present != 0 && !g.mfma) return MI_EUNSUPPORTED;   // (the VALU kernel has none)
   if (site->rows.counter != nullptr && (!g.mfma || g.stages_per_block != 1))
     return MI_EUNSUPPORTED;   // rows drawn only by one-stage matrix-core launches
+  if (site->draw.operand != 0) {
+    const mi_draw& D = site->draw;
+    if (D.loc == nullptr || D.scale == nullptr || D.element_offset < 0 || (D.element_offset & 3) != 0 ||
+        D.stream_id > 0xFFFFFFu)
+      return MI_EINVAL;
+    // theta drawn only by the matrix-core kernel, through its X staging buffer
+    const int threads = g.mfma ? kMfVariants[g.variant].threads : 0;
+    const int64_t lds_floats = (int64_t)((threads >= 512 ? 256 : 128) / std::max(1, g.pt)) * (32 * g.pt + 4);
+    if (!g.mfma || site->P % 4 != 0 || (int64_t)g.wt * 32 * (32 * g.pt + 1) > lds_floats)
+      return MI_EUNSUPPORTED;
+  }
   float* part = static_cast<float*>(workspace);
 #if MI_LINEAR_TIMING
   {

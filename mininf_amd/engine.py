@@ -566,6 +566,8 @@ class _LinearLauncher:
         # a prior site over theta itself folded into this launch (mi_linear.prior,
         # fold_linear_priors): (site, family code, (constant, constant))
         self.prior: Optional[Tuple[SiteRecord, int, Tuple[float, float]]] = None
+        # theta is a guide draw this launch makes itself (mi_linear.draw, guide.PendingDraw)
+        self.draw: Optional[guide.PendingDraw] = None
         # decided here, outside the autograd Function (whose forward runs with grad disabled)
         grad_on = torch.is_grad_enabled()
         self.theta_grad = grad_on and theta.requires_grad
@@ -583,7 +585,7 @@ class _LinearLauncher:
         return [self.theta, self.sigma_input]
 
     def describe(self, compute_grads: bool, draw_rows: bool = True,
-                 query: bool = False) -> nat.Linear:
+                 query: bool = False, draw: bool = True) -> nat.Linear:
         """
         The ``mi_linear`` descriptor. ``query``: for a support query only -- a minibatch's rows
         are neither drawn nor taken (the descriptor reads the dataset's first rows).
@@ -630,6 +632,8 @@ class _LinearLauncher:
             pr.present, pr.family = 1, self.prior[1]
             pr.constant[0], pr.constant[1] = self.prior[2]
             pr.scale = self.prior[0].scale
+        if draw and self.draw is not None and not self.draw.done:
+            self.draw.describe(L.draw)
         return L
 
     def run(self, compute_grads: bool, flags: Optional[torch.Tensor] = None,
@@ -663,6 +667,19 @@ class _LinearLauncher:
                 None if stop is None else stop.cuda_event, nat.stream_handle(device),
                 ctypes.byref(reduce) if defer else None)
         code = launch(L)
+        if L.draw.operand and code == nat.MI_EUNSUPPORTED:
+            # this launch shape does not draw theta: the guide's own draw first
+            self.draw.launch()
+            guide.take_draw(self.draw)
+            zeroed, prior_flags, rows = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags, L.rows
+            L = self.describe(compute_grads, draw_rows=False, draw=False)
+            L.options |= zeroed
+            L.prior.flags = prior_flags
+            if rows.counter:
+                L.rows, L.row_index = rows, None
+            code = launch(L)
+        elif L.draw.operand and code == 0:
+            guide.take_draw(self.draw)
         if L.rows.counter:
             if code == nat.MI_EUNSUPPORTED:   # this launch shape does not draw rows: draw first
                 zeroed, prior_flags = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags
@@ -708,7 +725,73 @@ class _LinearSiteFn(torch.autograd.Function):
         return (None, None, *launcher.grads(dslots))
 
 
-def plan_linear(trace: ParticleTrace, g0: float, device: torch.device) -> List[_LinearLauncher]:
+def _storage(t: torch.Tensor) -> Optional[int]:
+    return guide._storage_of(t)
+
+
+def claim_linear_draws(trace: ParticleTrace) -> Dict[int, guide.PendingDraw]:
+    """
+    Deferred guide draws (:class:`guide.PendingDraw`) a linear site kernel makes itself
+    (``mi_linear.draw``), by ``id`` of that site: the draw is the theta of exactly one linear site,
+    and every other site tensor reading it is the [K, P] draw itself (e.g. the value of a prior
+    over theta, which the linear launch evaluates too). Every other deferred draw is launched now,
+    before planning reads anything.
+    """
+    if not guide._PENDING_DRAWS:
+        return {}
+    thetas: Dict[guide.PendingDraw, list] = collections.defaultdict(list)
+    others: Dict[guide.PendingDraw, list] = collections.defaultdict(list)
+    for site in trace.sites:
+        if site.linear_X is not None and site.linear_theta is not None:
+            rec = guide.pending_draw(site.linear_theta)
+            if rec is not None:
+                thetas[rec].append(site)
+        for t in site.tensors:
+            rec = guide.pending_draw(t)
+            if rec is not None:
+                others[rec].append(t)
+    claims = {}
+    for rec, sites in thetas.items():
+        z = rec.z
+        if len(sites) == 1 and all(
+                isinstance(t, torch.Tensor) and t.data_ptr() == z.data_ptr() and
+                tuple(t.shape) == tuple(z.shape) and tuple(t.stride()) == tuple(z.stride())
+                for t in others.get(rec, [])):
+            claims[id(sites[0])] = rec
+            rec.claimed = True
+    claimed = set(map(id, claims.values()))
+    for key, rec in list(guide._PENDING_DRAWS.items()):
+        if id(rec) not in claimed:
+            del guide._PENDING_DRAWS[key]
+            rec.launch()
+    return claims
+
+
+def release_unsafe_claims(linears: List["_LinearLauncher"], launchers: List["_GroupLauncher"],
+                          categorical) -> None:
+    """
+    Launch the claimed draws that a group or categorical launch also reads (a prior over theta
+    that was not folded into the linear launch): those run before the linear sites.
+    """
+    drawn = {_storage(l.draw.z): l for l in linears if l.draw is not None}
+    if not drawn:
+        return
+    read = set()
+    for launcher in launchers:
+        for op in launcher.operands:
+            if op.view.tensor is not None:
+                read.add(_storage(op.view.tensor))
+    for site, lg, val, _ in categorical:
+        read.update(_storage(t) for t in (lg, val) if isinstance(t, torch.Tensor))
+    for key in read & set(drawn):
+        linear = drawn[key]
+        linear.draw.launch()
+        guide.take_draw(linear.draw)
+        linear.draw = None
+
+
+def plan_linear(trace: ParticleTrace, g0: float, device: torch.device,
+                claims: Optional[Dict[int, guide.PendingDraw]] = None) -> List[_LinearLauncher]:
     """
     Launchers for the fused linear-predictor sites of a trace. A site whose operands the kernel
     cannot take (per-element sigma, particle-dependent values, non-float32) gets its predictor
@@ -751,9 +834,11 @@ def plan_linear(trace: ParticleTrace, g0: float, device: torch.device) -> List[_
                     launcher.value_src = batch.loader.columns[vb[1]]
         if launcher is None:
             # materialise the predictor as the model would have: [K, N] = theta @ X^T
+            guide.flush_draws(claimed=True)
             site.tensors[0] = theta @ site.linear_X.t()
             site.linear_X = None
             continue
+        launcher.draw = (claims or {}).get(id(site))
         out.append(launcher)
     return out
 
@@ -1695,7 +1780,8 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     _, bad = _lazy_uses(trace)
     if bad:
         _materialize_draws(trace, bad)
-    linears = plan_linear(trace, g0, device)
+    claims = claim_linear_draws(trace)
+    linears = plan_linear(trace, g0, device, claims)
     while True:
         launchers, categorical = plan_groups(trace, g0, device)
         bad = {l.draw for l in launchers if l.draw is not None and not l.draw_supported()}
@@ -1703,6 +1789,8 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
             break
         _materialize_draws(trace, bad)
     launchers = fold_linear_priors(fold_priors(launchers), linears)
+    release_unsafe_claims(linears, launchers, categorical)
+    guide.flush_draws()   # draws made while planning (materialised lazy draws)
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,

@@ -38,6 +38,9 @@ class DrawConfig:
     step_snapshot: Optional[torch.Tensor] = None
     # global index of element 0 (data-sharded factors, mininf_amd.distributed.DataShard)
     element_offset: int = 0
+    # small Normal factors: leave the launch to the loss's planning (PendingDraw), which may hand
+    # the draw to the linear site kernel that reads it (mi_linear.draw)
+    defer: bool = False
 
 
 def backward_step(cfg: DrawConfig) -> Optional[torch.Tensor]:
@@ -78,24 +81,12 @@ class _NormalRsampleFn(torch.autograd.Function):
         N = loc.shape[0]
         K = cfg.K
         z = torch.empty((K, N), dtype=torch.float32, device=loc.device)
-        seed, step = _philox_key(cfg)
-        eps = cfg.noise
-        source = exp_source(scale)
-        if source is not None:
-            # the guide's exp transform and the draw in one launch
-            pending, u_ptr = source
-            nat.check(nat.lib().mi_normal_rsample_exp(
-                loc.data_ptr(), loc_s, u_ptr, scale_s, scale.data_ptr(), K, N, seed, step,
-                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
-                nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)), "mi_normal_rsample_exp")
-            pending.filled = True
+        draw = PendingDraw(cfg, z, loc, loc_s, scale, scale_s, exp_source(scale))
+        if cfg.defer and cfg.noise is None and N % 4 == 0 and N <= DEFER_MAX_N and \
+                os.environ.get("MININF_AMD_DRAW_IN_LINEAR", "1") != "0":
+            _PENDING_DRAWS[_storage_of(z)] = draw   # launched by flush_draws, or taken
         else:
-            fill_exp(scale)
-            nat.check(nat.lib().mi_normal_rsample(
-                loc.data_ptr(), loc_s, scale.data_ptr(), scale_s, K, N, seed, step,
-                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
-                nat.ptr(eps), z.data_ptr(), nat.stream_handle(loc.device)),
-                "mi_normal_rsample")
+            draw.launch()
         ctx.cfg = cfg
         ctx.N = N
         ctx.save_for_backward(scale)
@@ -387,6 +378,98 @@ class _GammaRsampleFn(torch.autograd.Function):
         return None, dconc, None, drate, None
 
 
+# ---- deferred small Normal draws ---------------------------------------------------------------
+# A small Normal factor's [K, N] draw (the regression's theta, N = P features) is made by the loss's
+# planning instead of when the guide is drawn: when the only kernel that reads it is one linear
+# site, that launch draws it (mi_linear.draw, one launch less per step); otherwise flush_draws
+# launches mi_normal_rsample before anything reads it (the particle trace's torch operations flush
+# through mininf_amd.linear.DeferredMatmul).
+DEFER_MAX_N = 64   # MI_LINEAR_MAX_P
+
+@dataclasses.dataclass(eq=False)
+class PendingDraw:
+    cfg: DrawConfig
+    z: torch.Tensor
+    loc: torch.Tensor
+    loc_s: int
+    scale: torch.Tensor
+    scale_s: int
+    source: Optional[Tuple["_PendingExp", int]]   # exp_source(scale) at draw time
+    done: bool = False
+    claimed: bool = False   # a planned linear launch will make it (engine.claim_linear_draws)
+
+    def launch(self) -> None:
+        """mi_normal_rsample (or _exp with the guide's pending exp transform) into z."""
+        if self.done:
+            return
+        self.done = True
+        cfg, loc, scale, z = self.cfg, self.loc, self.scale, self.z
+        K, N = z.shape
+        seed, step = _philox_key(cfg)
+        if self.source is not None:
+            # the guide's exp transform and the draw in one launch
+            pending, u_ptr = self.source
+            nat.check(nat.lib().mi_normal_rsample_exp(
+                loc.data_ptr(), self.loc_s, u_ptr, self.scale_s, scale.data_ptr(), K, N, seed,
+                step, nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset,
+                cfg.element_offset, nat.ptr(cfg.noise), z.data_ptr(),
+                nat.stream_handle(loc.device)), "mi_normal_rsample_exp")
+            pending.filled = True
+        else:
+            fill_exp(scale)
+            nat.check(nat.lib().mi_normal_rsample(
+                loc.data_ptr(), self.loc_s, scale.data_ptr(), self.scale_s, K, N, seed, step,
+                nat.ptr(cfg.step_device), cfg.stream_id, cfg.particle_offset, cfg.element_offset,
+                nat.ptr(cfg.noise), z.data_ptr(), nat.stream_handle(loc.device)),
+                "mi_normal_rsample")
+
+    def describe(self, D) -> None:
+        """Fill an mi_draw descriptor for the linear site kernel that takes this draw over."""
+        cfg = self.cfg
+        seed, step = _philox_key(cfg)
+        D.operand, D.stream_id = 1, cfg.stream_id
+        D.loc, D.loc_stride = self.loc.data_ptr(), self.loc_s
+        D.scale, D.scale_stride = self.scale.data_ptr(), self.scale_s
+        D.scale_exp = self.source[1] if self.source is not None else None
+        D.seed, D.step, D.step_device = seed, step, nat.ptr(cfg.step_device)
+        D.particle_offset, D.element_offset = cfg.particle_offset, cfg.element_offset
+
+    def taken(self) -> None:
+        """The linear launch made the draw (and the pending exp transform of its scale)."""
+        self.done = True
+        if self.source is not None:
+            self.source[0].filled = True
+
+
+_PENDING_DRAWS: Dict[Optional[int], PendingDraw] = {}
+
+
+def pending_draw(tensor) -> Optional[PendingDraw]:
+    """The not yet launched draw whose storage `tensor` (or a batched view of it) reads, or None."""
+    if not _PENDING_DRAWS or not isinstance(tensor, torch.Tensor):
+        return None
+    functorch = torch._C._functorch
+    base = tensor
+    while functorch.is_batchedtensor(base):
+        base = functorch.get_unwrapped(base)
+    rec = _PENDING_DRAWS.get(_storage_of(base))
+    return rec if rec is not None and not rec.done else None
+
+
+def flush_draws(claimed: bool = False) -> None:
+    """Launch every deferred draw no linear launch has claimed (with ``claimed``, those too)
+    before anything reads them."""
+    for key, rec in list(_PENDING_DRAWS.items()):
+        if claimed or not rec.claimed:
+            del _PENDING_DRAWS[key]
+            rec.launch()
+
+
+def take_draw(rec: PendingDraw) -> None:
+    rec.taken()
+    _PENDING_DRAWS.pop(_storage_of(rec.z), None)
+
+
 @dataclasses.dataclass(eq=False)   # identity semantics: used in sets
 class LazyDraw:
     r"""
@@ -497,6 +580,7 @@ def release_lazy() -> None:
     """
     _LAZY.clear()
     _DRAWN.clear()
+    flush_draws(claimed=True)
 
 
 def drawn_of(tensor) -> Optional[Drawn]:
@@ -602,12 +686,13 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
     """
     _LAZY.clear()
     _DRAWN.clear()
+    flush_draws(claimed=True)
     samples = {}
     for stream_id, (name, factor) in enumerate(approximation.items()):
         cfg = DrawConfig(K=K, seed=seed, step=step, stream_id=stream_id,
                          particle_offset=particle_offset,
                          noise=None if noise is None else noise.get(name),
                          step_device=step_device, step_snapshot=step_snapshot,
-                         element_offset=(element_offsets or {}).get(name, 0))
+                         element_offset=(element_offsets or {}).get(name, 0), defer=lazy)
         samples[name] = draw(factor, cfg, lazy)
     return samples

@@ -137,6 +137,7 @@ class DeferredMatmul(TorchFunctionMode):
             return tensor
         root = info.root or info
         if root.real is None:
+            _guide.flush_draws()   # theta may be a guide draw not launched yet
             self._bypass = True
             try:
                 root.real = torch.matmul(root.X, root.theta)
@@ -161,7 +162,7 @@ class DeferredMatmul(TorchFunctionMode):
             X, theta = args
             info = Deferred(X=X, theta=theta, shape=torch.Size([X.shape[0]]))
             return self._placeholder(theta, info.shape, info)
-        if not self.deferred and not _guide._LAZY:
+        if not self.deferred and not _guide._LAZY and not _guide._PENDING_DRAWS:
             return func(*args, **kwargs)   # no placeholder exists: nothing to look for
         touched = []
         lazy = []
@@ -171,6 +172,10 @@ class DeferredMatmul(TorchFunctionMode):
                 touched.append(info)
             elif lazy_of(x) is not None:
                 lazy.append(x)
+            elif func not in _METADATA and func not in _BROADCASTS and \
+                    _guide.pending_draw(x) is not None:
+                # the model reads a guide draw whose launch was left to the loss's planning
+                _guide.flush_draws()
         if not touched and not lazy:
             return func(*args, **kwargs)
         if func in _METADATA:

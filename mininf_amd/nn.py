@@ -117,7 +117,7 @@ class ParameterizedDistribution(nn.Module):
                     arguments[name] = forward(unconstrained)
                 if isinstance(forward, distributions.ExpTransform):
                     sources[name] = (unconstrained, "exp")
-        distribution = self.distribution_cls(**arguments, **self.distribution_constants)
+        distribution = _construct(self.distribution_cls, arguments, self.distribution_constants)
         # How each parameter derives from this module's nn.Parameters: the fused ELBO can then
         # write the guide's gradients directly (mi_factor transforms, engine.elbo).
         distribution._mininf_amd_sources = sources  # type: ignore[attr-defined]
@@ -144,13 +144,53 @@ class ParameterizedDistribution(nn.Module):
             return None
         conc = _ExpStackFn.apply(u1, u0)
         validate = self.distribution_constants.get("validate_args")
+        if validate is None:
+            validate = distributions.Distribution._validate_args
         beta = distributions.Beta.__new__(distributions.Beta)
-        beta._dirichlet = distributions.Dirichlet(conc, validate_args=validate)
+        beta._dirichlet = distributions.Dirichlet(conc, validate_args=False)
         distributions.Distribution.__init__(beta, beta._dirichlet._batch_shape,
-                                            validate_args=validate)
+                                            validate_args=False)
+        if validate:
+            # Dirichlet's and Beta's three argument checks are all `conc > 0` elementwise: one
+            # host synchronisation instead of three; torch raises its own error on failure
+            if not torch._is_all_true((conc > 0).all()):
+                distributions.Beta(conc[..., 0], conc[..., 1], validate_args=True)
+            beta._validate_args = beta._dirichlet._validate_args = True
         beta._mininf_amd_sources = {  # type: ignore[attr-defined]
             "concentration1": (u1, "exp"), "concentration0": (u0, "exp")}
         return beta
+
+
+# Guide families whose constructor builds no inner distribution: their argument validation can
+# be taken over by _construct.
+_ONE_SYNC = (distributions.Normal, distributions.Gamma)
+
+
+def _construct(cls, arguments: Dict, constants: Dict) -> distributions.Distribution:
+    """
+    ``cls(**arguments, **constants)`` with torch's argument validation (``Distribution.__init__``,
+    torch distribution.py:68-80) evaluated with ONE host synchronisation for all parameters
+    instead of one per parameter. When a check fails the distribution is constructed again with
+    validation, so torch raises its own error for the first failing parameter.
+    """
+    validate = constants.get("validate_args")
+    if validate is None:
+        validate = distributions.Distribution._validate_args
+    if cls not in _ONE_SYNC or not validate:
+        return cls(**arguments, **constants)
+    plain = {k: v for k, v in constants.items() if k != "validate_args"}
+    distribution = cls(**arguments, **plain, validate_args=False)
+    checks = []
+    for param, constraint in distribution.arg_constraints.items():
+        if distributions.constraints.is_dependent(constraint) or param not in distribution.__dict__:
+            continue
+        checks.append(constraint.check(getattr(distribution, param)).all())
+    if checks:
+        ok = checks[0] if len(checks) == 1 else torch.stack(checks).all()
+        if not torch._is_all_true(ok):
+            cls(**arguments, **plain, validate_args=True)   # raises torch's error
+    distribution._validate_args = True
+    return distribution
 
 
 def _defer_exp() -> bool:

@@ -549,8 +549,10 @@ def _trace(model: Callable, samples: Dict[str, torch.Tensor], K: int, validate: 
     names = list(samples)
     tracer = ParticleTracer(validate=validate)
 
-    from .guide import _LAZY
+    from .guide import _LAZY, flush_draws
     use_mode = defer_matmul or bool(_LAZY)
+    if not use_mode:
+        flush_draws()   # no mode watches the model's reads of deferred guide draws
 
     def per_particle(*values):
         mode = DeferredMatmul(K, defer_matmul) if use_mode else None
