@@ -65,6 +65,29 @@ class EventTimer:
         return sum(times) / len(times) if times else float("nan"), len(times)
 
 
+class _GcClock:
+    """Host time spent in Python's cyclic garbage collector while active (gc.callbacks): part of
+    an eager step's cost, reported beside it."""
+    def __init__(self):
+        self.seconds, self._t0 = 0.0, None
+
+    def _callback(self, phase, info):
+        if phase == "start":
+            self._t0 = time.perf_counter()
+        elif self._t0 is not None:
+            self.seconds += time.perf_counter() - self._t0
+            self._t0 = None
+
+    def __enter__(self):
+        import gc
+        gc.callbacks.append(self._callback)
+        return self
+
+    def __exit__(self, *exc):
+        import gc
+        gc.callbacks.remove(self._callback)
+
+
 # ------------------------------------------------------------------------------------------------
 # Workloads (restated from the reference's README / examples, SURVEY.md 8(d)).
 # ------------------------------------------------------------------------------------------------
@@ -400,7 +423,9 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         eager_step()
     timer.active = True
     eager_steps = max(3, steps // 3) if args.graph else steps
-    eager_elapsed, loss = timed(eager_step, eager_steps)
+    gc_clock = _GcClock()
+    with gc_clock:
+        eager_elapsed, loss = timed(eager_step, eager_steps)
     timer.active = False
     eager_ms = 1e3 * eager_elapsed / eager_steps
     torch.cuda.synchronize()
@@ -503,6 +528,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                         f" + {args.dist_backend} grad all-reduce") if sharded else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms,
+                   "eager_gc_ms_per_step": gc_clock.seconds * 1e3 / eager_steps,
                    **({"reducible_floor_ms_per_step": floor_ms,
                        "reducible_floor_note": "the same step with the site kernel evaluating "
                        "sum_i x_i l_k as l_k sum_i x_i (MININF_AMD_BCAST_SUFFSTAT=1); value and "

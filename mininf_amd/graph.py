@@ -29,6 +29,7 @@ optimizer must be created with ``capturable=True`` when its step is part of the 
 from __future__ import annotations
 
 import contextlib
+import gc
 import ctypes
 import sys
 import threading
@@ -244,6 +245,13 @@ class StepGraph:
         mirror = None
         capture_stream = torch.cuda.Stream()
         capture_stream.wait_stream(torch.cuda.current_stream())
+        # Garbage from earlier steps or graphs (pinned buffers, events, graph executables held in
+        # reference cycles) is freed now: a collection during the capture would run their
+        # finalizers on a capturing stream, which aborts the process. The collector stays off until
+        # the capture ends (torch.cuda.graph collects before its capture too).
+        gc.collect()
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
         with torch.cuda.stream(capture_stream):
             self.graph.capture_begin(capture_error_mode=capture_error_mode)
             try:
@@ -253,6 +261,7 @@ class StepGraph:
                         # AccumulateGrad nodes (and their capture stream) alive past the capture
                         self.output = _detached(step())
                     mirror = self._record_validation(count)
+                self.graph.capture_end()
             except BaseException as error:
                 self._joints = []
                 _abandon_capture(self.graph, capture_stream)
@@ -260,7 +269,9 @@ class StepGraph:
                 raise CaptureError("the step cannot be captured into a hipGraph, "
                                    f"{_failing_op(error)}: {type(error).__name__}: {error}") \
                     from error
-            self.graph.capture_end()
+            finally:
+                if gc_was_enabled:
+                    gc.enable()
         torch.cuda.current_stream().wait_stream(capture_stream)
         # The ELBO forward of a sticky step writes its words to pinned host memory itself (the
         # mirror); otherwise the copy is enqueued after each replay (one small asynchronous D2H
