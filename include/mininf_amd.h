@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 11
+#define MI_ABI_VERSION 12
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -679,7 +679,7 @@ typedef struct mi_elbo {
   int32_t num_buffers;
   int32_t num_reduce;
   float g0;
-  float pad1;
+  int32_t options;       /* MI_ELBO_* bits */
   double entropy_scale;
   const float* terms[MI_MAX_TERMS];
   mi_factor factors[MI_MAX_FACTORS];
@@ -702,6 +702,17 @@ typedef struct mi_elbo {
   int64_t nflags;
 } mi_elbo;
 
+
+/* mi_elbo.options: the forward's last block also writes the final gradients (`grad` of every
+ * factor) for an upstream gradient of exactly 1 -- loss.backward() of the training loop,
+ * README.md:66-69 -- when mi_elbo_final_grads reports the forward complete; the caller then need not
+ * launch mi_elbo_backward for that upstream (any other upstream: launch it, it rewrites them). */
+#define MI_ELBO_FINAL_GRADS 1
+
+/* *complete = 1 when mi_elbo_forward with MI_ELBO_FINAL_GRADS leaves nothing for mi_elbo_backward
+ * at an upstream of 1: every factor is a one-element forward-absorbed Beta factor whose sums the
+ * forward finishes (the README model's theta, with deferred site reductions). */
+int mi_elbo_final_grads(const mi_elbo* elbo, int* complete);
 
 /* sizeof(mi_factor), sizeof(mi_elbo) as compiled. */
 int mi_elbo_struct_sizes(size_t* factor, size_t* elbo);

@@ -37,7 +37,8 @@ MAX_SOURCES = 4
 MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
-ABI_VERSION = 11   # MI_ABI_VERSION of include/mininf_amd.h
+ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
+ABI_VERSION = 12   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM = 1, 2
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -156,7 +157,7 @@ class Elbo(ctypes.Structure):
     _fields_ = [
         ("K", c_i64), ("num_terms", ctypes.c_int32), ("num_factors", ctypes.c_int32),
         ("num_buffers", ctypes.c_int32), ("num_reduce", ctypes.c_int32),
-        ("g0", ctypes.c_float), ("pad1", ctypes.c_float), ("entropy_scale", ctypes.c_double),
+        ("g0", ctypes.c_float), ("options", ctypes.c_int32), ("entropy_scale", ctypes.c_double),
         ("terms", c_vp * MAX_TERMS), ("factors", Factor * MAX_FACTORS),
         ("buffers", c_vp * MAX_BUFFERS), ("buffer_len", c_i64 * MAX_BUFFERS),
         ("reduce", Reduce * MAX_REDUCE),
@@ -276,6 +277,7 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
     "mi_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "mi_elbo_final_grads": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
                                         c_vp]),
 }

@@ -575,6 +575,7 @@ struct ReducePlan {
   const float* tail_c1[kMaxTails];       // concentrations (n = 1)
   const float* tail_c0[kMaxTails];
   double* tail_saved[kMaxTails];
+  int tail_factor[kMaxTails];            // factor index of each tail (MI_ELBO_FINAL_GRADS)
 };
 
 // Fixed-order tree sum over the first `n` (a power of two) entries of lds; result in lds[0].
@@ -931,10 +932,20 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         }
         const float tt = (tsum - 2.0f) * tgs[0];
         double* pre = R.tail_saved[q];
+        const double h0 = (double)(tt - (a - 1.0f) * tgs[1]);
+        const double h1 = (double)(tt - (b - 1.0f) * tgs[2]);
         pre[0] = s0;
         pre[1] = s1;
-        pre[2] = (double)(tt - (a - 1.0f) * tgs[1]);
-        pre[3] = (double)(tt - (b - 1.0f) * tgs[2]);
+        pre[2] = h0;
+        pre[3] = h1;
+        if (E.options & MI_ELBO_FINAL_GRADS) {
+          // the gradients k_elbo_backward writes from `pre` for an upstream of 1 (same
+          // arithmetic: u * pre + w * dH with u = 1, w = -entropy_scale * weight)
+          const mi_factor F = factor_at(E, pick(R.tail_factor, q));
+          const double w = -(double)1.0f * E.entropy_scale * F.weight;
+          write_grad(F, 0, 0, (double)1.0f * s0 + w * h0);
+          write_grad(F, 1, 0, (double)1.0f * s1 + w * h1);
+        }
       }
       __syncthreads();
     }
@@ -1225,6 +1236,7 @@ Layout make_layout(const mi_elbo* e) {
       L.red.tail_c1[t] = F.param[0];
       L.red.tail_c0[t] = F.param[1];
       L.red.tail_saved[t] = F.saved;
+      L.red.tail_factor[t] = f;
       for (int src = 0; src < F.num_sources; ++src) {
         const mi_source& S = F.source[src];
         bool matched = false;
@@ -1293,6 +1305,13 @@ int mi_elbo_struct_sizes(size_t* factor, size_t* elbo) {
   if (factor == nullptr || elbo == nullptr) return MI_EINVAL;
   *factor = sizeof(mi_factor);
   *elbo = sizeof(mi_elbo);
+  return 0;
+}
+
+int mi_elbo_final_grads(const mi_elbo* elbo, int* complete) {
+  if (!valid(elbo) || complete == nullptr) return MI_EINVAL;
+  const Layout L = make_layout(elbo);
+  *complete = (elbo->num_factors > 0 && L.red.tails == elbo->num_factors && !L.red.external) ? 1 : 0;
   return 0;
 }
 

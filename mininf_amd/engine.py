@@ -1587,6 +1587,18 @@ class _ElboPlan:
             E.flags = self.flags.data_ptr()
             E.flags_mirror = self.mirror.data_ptr()
             E.nflags = min(self.flags.numel(), self.mirror.numel())
+        # The guide gradients of an upstream of exactly 1 (loss.backward() through nn._Loss's unit
+        # seed) written by the forward when that leaves the backward nothing to do: the backward
+        # then returns them without a launch (MI_ELBO_FINAL_GRADS).
+        self.final = None
+        if not self.recompute and not self.fallback and not extra and \
+                os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0":
+            complete = ctypes.c_int(0)
+            nat.check(lib.mi_elbo_final_grads(ctypes.byref(E), ctypes.byref(complete)),
+                      "mi_elbo_final_grads")
+            if complete.value:
+                self.final = self._factor_grads(E)
+                E.options |= nat.ELBO_FINAL_GRADS
         size = ctypes.c_size_t()
         nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
                   "mi_elbo_workspace_bytes")
@@ -1623,9 +1635,29 @@ class _ElboPlan:
             self.forward()
         E, results, cat_results, lin_results, extra, _ = self.state
         self.state = None
+        final, self.final = getattr(self, "final", None), None
+        if final is not None and _is_unit_seed(u):
+            # the forward wrote the gradients of exactly this upstream (MI_ELBO_FINAL_GRADS)
+            return self._outputs(results, cat_results, lin_results, None, final)
         device = self.device
         u = u.to(torch.float32).contiguous()
         dterm = torch.empty(1, dtype=torch.float32, device=device)
+        fgrads = self._factor_grads(E)
+        size = ctypes.c_size_t()
+        lib = nat.lib()
+        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
+                  "mi_elbo_workspace_bytes")
+        ws = _elbo_workspace(device, size.value)
+        nat.check(lib.mi_elbo_backward(ctypes.byref(E), u.data_ptr(), dterm.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), nat.stream_handle(device)),
+                  "mi_elbo_backward")
+        for buffer in extra:
+            buffer.mul_(u)
+        return self._outputs(results, cat_results, lin_results, dterm, fgrads)
+
+    def _factor_grads(self, E) -> List[List[Optional[torch.Tensor]]]:
+        """The guide factors' gradient outputs, their addresses written into E's factors."""
+        device = self.device
         fgrads: List[List[Optional[torch.Tensor]]] = []
         for j, f in enumerate(self.factors):
             d = E.factors[j]
@@ -1652,16 +1684,11 @@ class _ElboPlan:
                 d.grad[1] = base
                 d.grad_stride[1] = grad.stride(0) if f.n > 1 else 1
             fgrads.append([grad])
-        size = ctypes.c_size_t()
-        lib = nat.lib()
-        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(size)),
-                  "mi_elbo_workspace_bytes")
-        ws = _elbo_workspace(device, size.value)
-        nat.check(lib.mi_elbo_backward(ctypes.byref(E), u.data_ptr(), dterm.data_ptr(),
-                                       ws.data_ptr(), ws.numel(), nat.stream_handle(device)),
-                  "mi_elbo_backward")
-        for buffer in extra:
-            buffer.mul_(u)
+        return fgrads
+
+    def _outputs(self, results, cat_results, lin_results, dterm, fgrads
+                 ) -> List[Optional[torch.Tensor]]:
+        """The backward's gradients in the order of the autograd node's inputs."""
         out: List[Optional[torch.Tensor]] = []
         for li, (launcher, (grads, slot_grad, _)) in enumerate(zip(self.launchers, results)):
             skip = self.skip_ops.get(li, ())
@@ -1686,6 +1713,14 @@ class _ElboPlan:
         for grads_j in fgrads:
             out.extend(grads_j)
         return out
+
+
+def _is_unit_seed(u: torch.Tensor) -> bool:
+    """Whether the upstream gradient is nn._Loss's cached device 1.0 (never written)."""
+    from .nn import _UNIT
+    seed = _UNIT.get(u.device)
+    return seed is not None and u.dtype == torch.float32 and u.numel() == 1 and \
+        u.data_ptr() == seed.data_ptr()
 
 
 class _ElboFn(torch.autograd.Function):

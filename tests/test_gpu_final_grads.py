@@ -1,0 +1,126 @@
+"""
+Final guide gradients written by the ELBO forward (``MI_ELBO_FINAL_GRADS``): for the README model
+(``theta ~ Beta`` guide over a Bernoulli likelihood, README.md:43-69) the forward's last block
+finishes the Beta factor's particle sums, so for ``loss.backward()`` -- an upstream of exactly 1,
+nn._Loss's unit seed -- it also writes the gradients and ``mi_elbo_backward`` is not launched.
+
+* the gradients equal those of the backward launch (MININF_AMD_FINAL_GRADS=0), eager and over
+  several steps;
+* the backward kernel is skipped for loss.backward() and launched for any other upstream
+  (``torch.autograd.grad`` with a non-unit gradient), whose gradients scale accordingly;
+* a captured step (StepGraph) replays without the backward kernel and matches eager steps.
+"""
+import pytest
+import torch
+from torch.distributions import Bernoulli, Beta
+
+import mininf_amd
+from mininf_amd import _native as nat
+from mininf_amd.graph import StepGraph
+from mininf_amd.nn import EvidenceLowerBoundLoss, ParameterizedDistribution
+
+pytestmark = pytest.mark.gpu
+
+N, K = 50_000, 1024
+
+
+def _setup(device, seed=3):
+    gen = torch.Generator().manual_seed(seed)
+    x = (torch.rand(N, generator=gen) < 0.3).float().to(device)
+
+    def model():
+        theta = mininf_amd.sample("theta", Beta(2.0, 2.0))
+        mininf_amd.sample("x", Bernoulli(theta), sample_shape=[N])
+
+    guide = ParameterizedDistribution(Beta, concentration1=3.0, concentration0=5.0).to(device)
+    return mininf_amd.condition(model, x=x), guide, EvidenceLowerBoundLoss(num_particles=K, seed=7)
+
+
+def _spy_backward(monkeypatch):
+    lib = nat.lib()
+    real = lib.mi_elbo_backward
+    calls = []
+
+    def spy(*args):
+        calls.append(1)
+        return real(*args)
+    monkeypatch.setattr(lib, "mi_elbo_backward", spy)
+    return calls
+
+
+def _steps(device, monkeypatch, final, steps=3):
+    monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1" if final else "0")
+    model, guide, loss_fn = _setup(device)
+    out = []
+    for _ in range(steps):
+        loss = loss_fn(model, {"theta": guide()})
+        loss.backward()
+        out.append((float(loss), [p.grad.clone() for p in guide.parameters()]))
+        for p in guide.parameters():
+            p.grad = None
+    torch.cuda.synchronize()
+    return out
+
+
+def test_final_grads_match_the_backward_launch(device, monkeypatch):
+    calls = _spy_backward(monkeypatch)
+    fused = _steps(device, monkeypatch, True)
+    assert calls == []            # no mi_elbo_backward for loss.backward()
+    plain = _steps(device, monkeypatch, False)
+    assert len(calls) == 3
+    for (lf, gf), (lp, gp) in zip(fused, plain):
+        assert lf == lp
+        for a, b in zip(gf, gp):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
+
+
+def test_other_upstream_launches_the_backward(device, monkeypatch):
+    monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1")
+    calls = _spy_backward(monkeypatch)
+    model, guide, loss_fn = _setup(device)
+    params = list(guide.parameters())
+    torch.manual_seed(0)
+    loss = loss_fn(model, {"theta": guide()})
+    g2 = torch.autograd.grad(loss, params, torch.tensor(2.0, device=device))
+    assert calls == [1]
+    model, guide, loss_fn = _setup(device)
+    loss = loss_fn(model, {"theta": guide()})
+    loss.backward()
+    assert calls == [1]
+    for a, b in zip(g2, guide.parameters()):
+        torch.testing.assert_close(a, 2 * b.grad, rtol=1e-6, atol=0)
+
+
+def test_captured_final_grads_match_eager(device, monkeypatch):
+    monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1")
+
+    def run(captured):
+        model, guide, loss_fn = _setup(device)
+        optimizer = mininf_amd.optim.Adam(guide.parameters(), lr=0.02)
+
+        def step():
+            optimizer.zero_grad(set_to_none=False)
+            loss = loss_fn(model, {"theta": guide()})
+            loss.backward()
+            optimizer.step()
+            return loss
+
+        losses = []
+        if captured:
+            graph = StepGraph(step, warmup=2, repeat=2)
+            for _ in range(3):
+                losses.append(float(graph()))
+            graph.check()
+        else:
+            for i in range(8):
+                loss = step()
+                if i >= 2 and i % 2 == 1:
+                    losses.append(float(loss))
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in guide.parameters()]
+
+    le, pe = run(False)
+    lc, pc = run(True)
+    assert le == pytest.approx(lc, rel=1e-6)
+    for a, b in zip(pe, pc):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
