@@ -576,6 +576,15 @@ struct ReducePlan {
   const float* tail_c0[kMaxTails];
   double* tail_saved[kMaxTails];
   int tail_factor[kMaxTails];            // factor index of each tail (MI_ELBO_FINAL_GRADS)
+  // One small Normal factor whose draw's only source is consecutive slot rows of one split
+  // reduction (the regression's theta under a linear site, mi_linear.draw): with
+  // MI_ELBO_FINAL_GRADS the blocks writing those rows also sum dz and dz * eps over their
+  // particles, and the last block finishes the factor's gradients.
+  int nt_job;                            // -1: none
+  int nt_j0;                             // slot of element 0
+  int nt_factor;
+  int nt_nkb;                            // particle blocks of the job
+  int64_t nt_part;                       // offset (doubles) of the [n][nt_nkb][2] partials
 };
 
 // Fixed-order tree sum over the first `n` (a power of two) entries of lds; result in lds[0].
@@ -589,13 +598,21 @@ MI_DEV void lds_tree(double* lds, int n) {
 // Writes job J's outputs for one block's particles (local block `local` of the job) and returns
 // g0 * the sum of its (fp32) totals (0 from blocks that do not write totals): the block's share of
 // the loss.
-MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kRedK,
-                         const ReducePlan& R, int a, double (&c)[kMaxTails][2],
-                         double (*red)[2]) {
+MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int local, int vb,
+                         int kRedK, const ReducePlan& R, int a, double (&c)[kMaxTails][2],
+                         double (*red)[2], double (&nt)[2], int& nt_slot) {
   const int kRedG = kElboThreads / kRedK;
   const int nv = J.num_sites + J.num_slots;
   const int64_t kb = local / vb;
   const int v0 = vb > 1 ? local % vb : 0, v1 = vb > 1 ? v0 + 1 : nv;
+  // this block's element of the Normal tail (split jobs: one value per block), or -1
+  const bool nt_on = (E.options & MI_ELBO_FINAL_GRADS) && a == R.nt_job && vb > 1;
+  nt_slot = -1;
+  if (nt_on) {
+    const int j = v0 - J.num_sites;
+    const int i = j - R.nt_j0;
+    if (j >= 0 && i >= 0 && i < (int)factor_at(E, R.nt_factor).n) nt_slot = i;
+  }
   const int kl = threadIdx.x % kRedK, gl = threadIdx.x / kRedK;
   const int64_t K = J.K;
   const int64_t k = kb * kRedK + kl;
@@ -656,6 +673,20 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
         const int j = v - J.num_sites;
         const float gv = (float)(s * J.slot_scale);
         J.slot_grad[(int64_t)j * K + k] = gv;
+        if (nt_slot >= 0) {   // d z[k, i] for the Normal tail, against its regenerated eps
+          const mi_factor F = factor_at(E, R.nt_factor);
+          // the forward runs before it advances the step counter: the backward's snapshot word
+          // still holds the previous evaluation's step, the counter this one's
+          const uint64_t* sd = (E.step_counter != nullptr && F.step_device == E.step_snapshot)
+                                   ? E.step_counter : F.step_device;
+          const uint64_t step = F.step + (sd != nullptr ? *sd : 0ull);
+          const int64_t i = nt_slot;
+          float q[4];
+          guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
+                        (uint64_t)(F.particle_offset + k), q);
+          nt[0] += (double)gv;
+          nt[1] += (double)gv * (double)q[i & 3];
+        }
         const int mask = j < MI_MAX_SLOTS ? pick(R.tail_slot, a * MI_MAX_SLOTS + j) : 0;
 #pragma unroll
         for (int q = 0; q < kMaxTails; ++q)
@@ -676,7 +707,8 @@ MI_DEV double reduce_job(float g0, const mi_reduce& J, int local, int vb, int kR
 }
 
 MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
-                           double (&c)[kMaxTails][2], double (*red)[2]) {
+                           double (&c)[kMaxTails][2], double (*red)[2], double (&nt)[2],
+                           int& nt_slot, int& nt_kb) {
   int a = 0;
 #pragma unroll
   for (int q = 1; q < MI_MAX_REDUCE; ++q)
@@ -687,11 +719,12 @@ MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
   double share;
   // constant descriptor indices (a run-time index into the by-value kernel argument would copy
   // it to scratch memory)
+  nt_kb = local / vb;
   switch (a) {
-    case 1: share = reduce_job(E.g0, E.reduce[1], local, vb, kred, R, 1, c, red); break;
-    case 2: share = reduce_job(E.g0, E.reduce[2], local, vb, kred, R, 2, c, red); break;
-    case 3: share = reduce_job(E.g0, E.reduce[3], local, vb, kred, R, 3, c, red); break;
-    default: share = reduce_job(E.g0, E.reduce[0], local, vb, kred, R, 0, c, red); break;
+    case 1: share = reduce_job(E, E.g0, E.reduce[1], local, vb, kred, R, 1, c, red, nt, nt_slot); break;
+    case 2: share = reduce_job(E, E.g0, E.reduce[2], local, vb, kred, R, 2, c, red, nt, nt_slot); break;
+    case 3: share = reduce_job(E, E.g0, E.reduce[3], local, vb, kred, R, 3, c, red, nt, nt_slot); break;
+    default: share = reduce_job(E, E.g0, E.reduce[0], local, vb, kred, R, 0, c, red, nt, nt_slot); break;
   }
   return share;
 }
@@ -739,8 +772,10 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   double* rsum = &red[0][0];
   double share;
   double c[kMaxTails][2] = {};   // this lane's tail contributions
+  double nt[2] = {0.0, 0.0};     // this lane's Normal-tail sums (R.nt_job), element nt_slot
+  int nt_slot = -1, nt_kb = 0;
   if (!ABSORB && (int)blockIdx.x < nred) {   // (ABSORB launches have no deferred reductions)
-    share = reduce_block(E, R, (int)blockIdx.x, c, red);
+    share = reduce_block(E, R, (int)blockIdx.x, c, red, nt, nt_slot, nt_kb);
     __syncthreads();
   } else {
     const int64_t lead = (int64_t)blockIdx.x - nred;
@@ -820,6 +855,12 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     const double v0 = wave_sum(share);
     if (lane == 0) wsum[0][wave] = v0;
     const int tails = ABSORB ? 0 : R.tails;
+    // the Normal tail's sums live on the particle lanes (the first kRedK <= 64 threads: wave 0)
+    double nts0 = 0.0, nts1 = 0.0;
+    if (!ABSORB && nt_slot >= 0 && wave == 0) {
+      nts0 = wave_sum(nt[0]);
+      nts1 = wave_sum(nt[1]);
+    }
 #pragma unroll
     for (int t = 0; t < kMaxTails; ++t)
 #pragma unroll
@@ -839,6 +880,11 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
           __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + blockIdx.x) * 2 + q], v,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+      if (!ABSORB && nt_slot >= 0) {
+        double* w2 = &work[R.nt_part + ((int64_t)nt_slot * R.nt_nkb + nt_kb) * 2];
+        __hip_atomic_store(w2, nts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w2 + 1, nts1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   MI_ELBO_STAMP(2);
@@ -948,6 +994,26 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         }
       }
       __syncthreads();
+    }
+  }
+  if (!ABSORB && R.nt_job >= 0 && (E.options & MI_ELBO_FINAL_GRADS)) {
+    // the Normal tail's gradients for an upstream of 1: its blocks' sums in a fixed order, then
+    // what k_elbo_backward's absorbed blocks write (u * s + w * dH, the exp chain rule)
+    const mi_factor F = factor_at(E, R.nt_factor);
+    const int64_t i = threadIdx.x;
+    if (i < F.n) {
+      const Params2 q = load_params(F, i);
+      double s0 = 0.0, s1 = 0.0;
+      for (int kb = 0; kb < R.nt_nkb; ++kb) {
+        const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
+        s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      double d0, d1;
+      entropy_grad_of(F, q, d0, d1);
+      const double w = -(double)1.0f * E.entropy_scale * F.weight;
+      write_grad_of(F, 0, i, (double)1.0f * s0 + w * d0, q);
+      write_grad_of(F, 1, i, (double)1.0f * s1 + w * d1, q);
     }
   }
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=
@@ -1255,10 +1321,33 @@ Layout make_layout(const mi_elbo* e) {
         }
       }
     }
+  L.red.nt_job = -1;
+  if (deferred && !L.red.external)
+    for (int f = 0; f < e->num_factors && L.red.nt_job < 0; ++f) {
+      const mi_factor& F = e->factors[f];
+      if (tail[f] || F.family != MI_NORMAL || F.draw_kind != MI_DRAW_SOURCES ||
+          F.num_sources != 1 || F.n > mi::kElboThreads || F.eps != nullptr)
+        continue;
+      const mi_source& S = F.source[0];
+      for (int r = 0; r < e->num_reduce; ++r) {
+        const mi_reduce& J = e->reduce[r];
+        if (J.num_sites != 1 || J.num_slots < 1 || S.stride_k != 1 || S.stride_i != J.K) continue;
+        const int64_t off = S.ptr - J.slot_grad;
+        if (off < 0 || off % J.K != 0 || off / J.K + F.n > J.num_slots) continue;
+        L.red.nt_job = r;
+        L.red.nt_j0 = (int)(off / J.K);
+        L.red.nt_factor = f;
+        L.red.nt_nkb = (int)ceil_div(J.K, L.red.kred[r]);
+        tail[f] = true;
+        break;
+      }
+    }
   int64_t counters = kCounterFirst;
   int64_t doubles = (nshare + 31) / 32 * 32;
   L.red.tail_part = doubles;
   doubles += (int64_t)L.red.tails * nshare * 2;
+  L.red.nt_part = doubles;
+  if (L.red.nt_job >= 0) doubles += e->factors[L.red.nt_factor].n * (int64_t)L.red.nt_nkb * 2;
   int blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
     if (forward_absorbed(e->factors[f]) && !deferred)
@@ -1270,7 +1359,8 @@ Layout make_layout(const mi_elbo* e) {
     if (e->factors[f].draw_kind != MI_DRAW_NONE) {
       // the forward left the sums in F.saved: its absorbed blocks (no deferred reductions) or
       // its tail partials
-      const bool finish = forward_absorbed(e->factors[f]) && (!deferred || tail[f]);
+      const bool finish = forward_absorbed(e->factors[f]) && (!deferred || tail[f]) &&
+                          e->factors[f].family == MI_BETA;
       add_absorbed(e, f, false, finish, L.bwd, counters, doubles, blocks);
     }
   L.bwd.first[L.bwd.num] = blocks;
@@ -1311,7 +1401,8 @@ int mi_elbo_struct_sizes(size_t* factor, size_t* elbo) {
 int mi_elbo_final_grads(const mi_elbo* elbo, int* complete) {
   if (!valid(elbo) || complete == nullptr) return MI_EINVAL;
   const Layout L = make_layout(elbo);
-  *complete = (elbo->num_factors > 0 && L.red.tails == elbo->num_factors && !L.red.external) ? 1 : 0;
+  const int finished = L.red.tails + (L.red.nt_job >= 0 ? 1 : 0);
+  *complete = (elbo->num_factors > 0 && finished == elbo->num_factors && !L.red.external) ? 1 : 0;
   return 0;
 }
 

@@ -12,7 +12,7 @@ nn._Loss's unit seed -- it also writes the gradients and ``mi_elbo_backward`` is
 """
 import pytest
 import torch
-from torch.distributions import Bernoulli, Beta
+from torch.distributions import Bernoulli, Beta, Normal
 
 import mininf_amd
 from mininf_amd import _native as nat
@@ -124,3 +124,50 @@ def test_captured_final_grads_match_eager(device, monkeypatch):
     assert le == pytest.approx(lc, rel=1e-6)
     for a, b in zip(pe, pc):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+
+
+def _regression_steps(device, monkeypatch, final, K, minibatch, steps=3):
+    """C3 / C4-shaped regression (examples/minibatch.md): the theta factor's gradients finished by
+    the ELBO forward from the linear site's slot rows (the Normal tail)."""
+    monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1" if final else "0")
+    gen = torch.Generator().manual_seed(5)
+    n, p = 8192, 32
+    X = torch.randn(n, p, generator=gen)
+    y = X @ torch.randn(p, generator=gen) + torch.randn(n, generator=gen)
+    X, y = X.to(device), y.to(device)
+
+    def model():
+        theta = mininf_amd.sample("theta", Normal(0, 1), sample_shape=p)
+        with mininf_amd.batch(n):
+            with mininf_amd.no_log_prob():
+                Xs = mininf_amd.sample("X", Normal(0, 1), sample_shape=(n, p))
+            mininf_amd.sample("y", Normal(Xs @ theta, 1))
+
+    guide = ParameterizedDistribution(Normal, loc=0.1 * torch.randn(p, generator=gen),
+                                      scale=torch.rand(p, generator=gen) + 0.5).to(device)
+    loss_fn = EvidenceLowerBoundLoss(num_particles=K, seed=2)
+    loader = mininf_amd.DeviceDataLoader(X, y, batch_size=1024, shuffle=True, drop_last=True,
+                                         seed=7) if minibatch else None
+    out = []
+    for _ in range(steps):
+        Xb, yb = loader.next() if loader is not None else (X, y)
+        loss = loss_fn(mininf_amd.condition(model, X=Xb, y=yb), {"theta": guide()})
+        loss.backward()
+        out.append((float(loss), [q.grad.clone() for q in guide.parameters()]))
+        for q in guide.parameters():
+            q.grad = None
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("K, minibatch", [(64, False), (256, False), (40, True)])
+def test_regression_final_grads_match_the_backward_launch(device, monkeypatch, K, minibatch):
+    calls = _spy_backward(monkeypatch)
+    fused = _regression_steps(device, monkeypatch, True, K, minibatch)
+    assert calls == []
+    plain = _regression_steps(device, monkeypatch, False, K, minibatch)
+    assert len(calls) == 3
+    for (lf, gf), (lp, gp) in zip(fused, plain):
+        assert lf == lp
+        for a, b in zip(gf, gp):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
