@@ -575,17 +575,52 @@ struct ReducePlan {
   const float* tail_c1[kMaxTails];       // concentrations (n = 1)
   const float* tail_c0[kMaxTails];
   double* tail_saved[kMaxTails];
-  int tail_factor[kMaxTails];            // factor index of each tail (MI_ELBO_FINAL_GRADS)
-  // One small Normal factor whose draw's only source is consecutive slot rows of one split
-  // reduction (the regression's theta under a linear site, mi_linear.draw): with
-  // MI_ELBO_FINAL_GRADS the blocks writing those rows also sum dz and dz * eps over their
-  // particles, and the last block finishes the factor's gradients.
+  // MI_ELBO_FINAL_GRADS: the factor of each tail; its fields are read through factor_field-style
+  // selects (a whole mi_factor selected by a run-time index would be copied to scratch memory,
+  // and the kernel arguments must stay within 4 KiB)
+  int tail_factor[kMaxTails];
+  // One small Normal factor -- factor 0 of the launch -- whose draw's only source is consecutive
+  // slot rows of one split reduction (the regression's theta under a linear site,
+  // mi_linear.draw): with MI_ELBO_FINAL_GRADS the blocks writing those rows also sum dz and
+  // dz * eps over their particles, and the last block finishes the factor's gradients.
   int nt_job;                            // -1: none
   int nt_j0;                             // slot of element 0
-  int nt_factor;
   int nt_nkb;                            // particle blocks of the job
   int64_t nt_part;                       // offset (doubles) of the [n][nt_nkb][2] partials
 };
+
+// Fields of factor f of the launch, by constant-index selects (see ReducePlan.tail_factor).
+MI_DEV float* factor_grad(const mi_elbo& E, int f, int j) {
+  float* g = E.factors[0].grad[j];
+#pragma unroll
+  for (int c = 1; c < MI_MAX_FACTORS; ++c)
+    if (f == c) g = E.factors[c].grad[j];
+  return g;
+}
+MI_DEV bool factor_exp(const mi_elbo& E, int f, int j) {
+  int t = E.factors[0].transform[j];
+#pragma unroll
+  for (int c = 1; c < MI_MAX_FACTORS; ++c)
+    if (f == c) t = E.factors[c].transform[j];
+  return t == MI_TRANSFORM_EXP;
+}
+MI_DEV double factor_weight(const mi_elbo& E, int f) {
+  double w = E.factors[0].weight;
+#pragma unroll
+  for (int c = 1; c < MI_MAX_FACTORS; ++c)
+    if (f == c) w = E.factors[c].weight;
+  return w;
+}
+
+// The forward's generator step word of factor 0 (the Normal tail): the forward runs before it
+// advances the step counter, so the backward's snapshot word still holds the previous
+// evaluation's step and the counter this one's.
+MI_DEV uint64_t forward_step0(const mi_elbo& E) {
+  const mi_factor& F = E.factors[0];
+  const uint64_t* sd = (E.step_counter != nullptr && F.step_device == E.step_snapshot)
+                           ? E.step_counter : F.step_device;
+  return F.step + (sd != nullptr ? *sd : 0ull);
+}
 
 // Fixed-order tree sum over the first `n` (a power of two) entries of lds; result in lds[0].
 MI_DEV void lds_tree(double* lds, int n) {
@@ -611,7 +646,7 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
   if (nt_on) {
     const int j = v0 - J.num_sites;
     const int i = j - R.nt_j0;
-    if (j >= 0 && i >= 0 && i < (int)factor_at(E, R.nt_factor).n) nt_slot = i;
+    if (j >= 0 && i >= 0 && i < E.factors[0].n) nt_slot = i;
   }
   const int kl = threadIdx.x % kRedK, gl = threadIdx.x / kRedK;
   const int64_t K = J.K;
@@ -674,12 +709,8 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
         const float gv = (float)(s * J.slot_scale);
         J.slot_grad[(int64_t)j * K + k] = gv;
         if (nt_slot >= 0) {   // d z[k, i] for the Normal tail, against its regenerated eps
-          const mi_factor F = factor_at(E, R.nt_factor);
-          // the forward runs before it advances the step counter: the backward's snapshot word
-          // still holds the previous evaluation's step, the counter this one's
-          const uint64_t* sd = (E.step_counter != nullptr && F.step_device == E.step_snapshot)
-                                   ? E.step_counter : F.step_device;
-          const uint64_t step = F.step + (sd != nullptr ? *sd : 0ull);
+          const mi_factor& F = E.factors[0];
+          const uint64_t step = forward_step0(E);
           const int64_t i = nt_slot;
           float q[4];
           guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
@@ -986,11 +1017,19 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         pre[3] = h1;
         if (E.options & MI_ELBO_FINAL_GRADS) {
           // the gradients k_elbo_backward writes from `pre` for an upstream of 1 (same
-          // arithmetic: u * pre + w * dH with u = 1, w = -entropy_scale * weight)
-          const mi_factor F = factor_at(E, pick(R.tail_factor, q));
-          const double w = -(double)1.0f * E.entropy_scale * F.weight;
-          write_grad(F, 0, 0, (double)1.0f * s0 + w * h0);
-          write_grad(F, 1, 0, (double)1.0f * s1 + w * h1);
+          // arithmetic as write_grad: u * pre + w * dH with u = 1, w = -entropy_scale * weight,
+          // times the parameter under an exp transform)
+          const int f = R.tail_factor[q];
+          const double w = -(double)1.0f * E.entropy_scale * factor_weight(E, f);
+          double g[2] = {(double)1.0f * s0 + w * h0, (double)1.0f * s1 + w * h1};
+          const float pv[2] = {a, b};
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float* out = factor_grad(E, f, j);
+            if (out == nullptr) continue;
+            if (factor_exp(E, f, j)) g[j] *= (double)pv[j];
+            out[0] = (float)g[j];
+          }
         }
       }
       __syncthreads();
@@ -999,23 +1038,31 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   if (!ABSORB && R.nt_job >= 0 && (E.options & MI_ELBO_FINAL_GRADS)) {
     // the Normal tail's gradients for an upstream of 1: its blocks' sums in a fixed order, then
     // what k_elbo_backward's absorbed blocks write (u * s + w * dH, the exp chain rule)
-    const mi_factor F = factor_at(E, R.nt_factor);
+    const mi_factor& F = E.factors[0];
     const int64_t i = threadIdx.x;
     if (i < F.n) {
-      const Params2 q = load_params(F, i);
+      const float p0 = F.param[0][i * F.stride[0]], p1 = F.param[1][i * F.stride[1]];
       double s0 = 0.0, s1 = 0.0;
       for (int kb = 0; kb < R.nt_nkb; ++kb) {
         const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
         s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      double d0, d1;
-      entropy_grad_of(F, q, d0, d1);
+      // entropy_grad_of / write_grad_of of a Normal factor: dH = (0, 1 / scale)
+      const double d0 = 0.0, d1 = (double)(1.0f / p1);
       const double w = -(double)1.0f * E.entropy_scale * F.weight;
-      write_grad_of(F, 0, i, (double)1.0f * s0 + w * d0, q);
-      write_grad_of(F, 1, i, (double)1.0f * s1 + w * d1, q);
+      double g[2] = {(double)1.0f * s0 + w * d0, (double)1.0f * s1 + w * d1};
+      const float pv[2] = {p0, p1};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (F.grad[j] == nullptr) continue;
+        if (F.transform[j] == MI_TRANSFORM_EXP) g[j] *= (double)pv[j];
+        F.grad[j][i * F.grad_stride[j]] = (float)g[j];
+      }
     }
   }
+  static_assert(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan) + 3 * sizeof(void*) <= 4096,
+                "k_elbo_forward's arguments exceed 4 KiB");
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=
                     MI_ELBO_COUNTER_BYTES / sizeof(unsigned), "counter area");
   if ((int64_t)threadIdx.x < E.nflags) E.flags_mirror[threadIdx.x] = fw0;
@@ -1323,7 +1370,7 @@ Layout make_layout(const mi_elbo* e) {
     }
   L.red.nt_job = -1;
   if (deferred && !L.red.external)
-    for (int f = 0; f < e->num_factors && L.red.nt_job < 0; ++f) {
+    for (int f = 0; f < 1 && f < e->num_factors; ++f) {   // factor 0 only (ReducePlan.nt_job)
       const mi_factor& F = e->factors[f];
       if (tail[f] || F.family != MI_NORMAL || F.draw_kind != MI_DRAW_SOURCES ||
           F.num_sources != 1 || F.n > mi::kElboThreads || F.eps != nullptr)
@@ -1336,7 +1383,6 @@ Layout make_layout(const mi_elbo* e) {
         if (off < 0 || off % J.K != 0 || off / J.K + F.n > J.num_slots) continue;
         L.red.nt_job = r;
         L.red.nt_j0 = (int)(off / J.K);
-        L.red.nt_factor = f;
         L.red.nt_nkb = (int)ceil_div(J.K, L.red.kred[r]);
         tail[f] = true;
         break;
@@ -1347,7 +1393,7 @@ Layout make_layout(const mi_elbo* e) {
   L.red.tail_part = doubles;
   doubles += (int64_t)L.red.tails * nshare * 2;
   L.red.nt_part = doubles;
-  if (L.red.nt_job >= 0) doubles += e->factors[L.red.nt_factor].n * (int64_t)L.red.nt_nkb * 2;
+  if (L.red.nt_job >= 0) doubles += e->factors[0].n * (int64_t)L.red.nt_nkb * 2;
   int blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
     if (forward_absorbed(e->factors[f]) && !deferred)

@@ -74,6 +74,24 @@ def main():
     import warnings
     from mininf_amd.graph import StepGraph
     warnings.filterwarnings("error", message=".*AccumulateGrad node's stream.*")
+    real_begin = torch.cuda.CUDAGraph.capture_begin
+
+    def begin(self, *args, **kwargs):   # what the warm-up left alive, just before the capture
+        gc.collect()
+        nodes = [o for o in gc.get_objects()
+                 if isinstance(o, torch.autograd.function.BackwardCFunction)]
+        tensors = [o for o in gc.get_objects()
+                   if isinstance(o, torch.Tensor) and getattr(o, "grad_fn", None) is not None]
+        print(f"before capture: {len(nodes)} custom-Function nodes, {len(tensors)} tensors with "
+              "grad_fn", flush=True)
+        for o in (nodes + tensors)[:6]:
+            print(" ", describe(o))
+            for r in gc.get_referrers(o)[:5]:
+                print("    <-", describe(r))
+                for r2 in gc.get_referrers(r)[:3]:
+                    print("       <-", describe(r2))
+        return real_begin(self, *args, **kwargs)
+    torch.cuda.CUDAGraph.capture_begin = begin
     try:
         graph = StepGraph(step, warmup=2)
         graph()
