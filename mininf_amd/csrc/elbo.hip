@@ -971,6 +971,22 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         tc0[q] = *R.tail_c0[q];
       }
   }
+  // the Normal tail's partial sums and parameters, fetched with the shares (one round trip)
+  const bool nt_fin = !ABSORB && R.nt_job >= 0 && (E.options & MI_ELBO_FINAL_GRADS) &&
+                      (int64_t)threadIdx.x < E.factors[0].n;
+  double nt_s0 = 0.0, nt_s1 = 0.0;
+  float nt_p0 = 1.0f, nt_p1 = 1.0f;
+  if (nt_fin) {
+    const mi_factor& F = E.factors[0];
+    const int64_t i = threadIdx.x;
+    nt_p0 = F.param[0][i * F.stride[0]];
+    nt_p1 = F.param[1][i * F.stride[1]];
+    for (int kb = 0; kb < R.nt_nkb; ++kb) {
+      const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
+      nt_s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nt_s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   const uint32_t fw0 = (int64_t)threadIdx.x < E.nflags ? E.flags[threadIdx.x] : 0u;
   const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
   const double total = block_sum(t, rsum + kElboThreads / kWave);
@@ -1040,14 +1056,9 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     // what k_elbo_backward's absorbed blocks write (u * s + w * dH, the exp chain rule)
     const mi_factor& F = E.factors[0];
     const int64_t i = threadIdx.x;
-    if (i < F.n) {
-      const float p0 = F.param[0][i * F.stride[0]], p1 = F.param[1][i * F.stride[1]];
-      double s0 = 0.0, s1 = 0.0;
-      for (int kb = 0; kb < R.nt_nkb; ++kb) {
-        const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
-        s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    if (nt_fin) {
+      const float p0 = nt_p0, p1 = nt_p1;
+      const double s0 = nt_s0, s1 = nt_s1;
       // entropy_grad_of / write_grad_of of a Normal factor: dH = (0, 1 / scale)
       const double d0 = 0.0, d1 = (double)(1.0f / p1);
       const double w = -(double)1.0f * E.entropy_scale * F.weight;
