@@ -213,25 +213,55 @@ struct MfShape {
 // k_normal_rsample for the same (particle, element quad) and the same fmaf, so the values are
 // bit-identical to the separate draw. The first row block also writes them to theta (every
 // particle group its own particles) and, for an exp-transformed scale, group 0 writes the scale.
+// Two phases: the items' parameters and the generator step are loaded before the stage's X rows
+// (a wait for them then does not wait for the X loads, vector-memory counts being in order), the
+// normals are computed while the X loads are in flight.
+constexpr int kDrawItems = 4;   // items per thread: nk * P / 4 <= 4 * threads (host-checked)
+struct DrawRegs {
+  float loc[kDrawItems][4], sd[kDrawItems][4];
+  uint64_t step;
+};
 template <int NT>
-__device__ __forceinline__ void draw_theta(const mi_linear& L, int64_t kbase, int nk, float* dst,
-                                           int dstr, bool write_theta, bool write_scale) {
+__device__ __forceinline__ void draw_theta_load(const mi_linear& L, int nk, DrawRegs& R) {
   const mi_draw& D = L.draw;
-  const uint64_t step = D.step + (D.step_device != nullptr ? *D.step_device : 0ull);
+  R.step = D.step + (D.step_device != nullptr ? *D.step_device : 0ull);
   const int nq = (int)L.P / 4;
   const bool exp_scale = D.scale_exp != nullptr;
-  for (int item = threadIdx.x; item < nk * nq; item += NT) {
+  const float* sp = exp_scale ? D.scale_exp : D.scale;
+#pragma unroll
+  for (int t = 0; t < kDrawItems; ++t) {
+    const int item = (int)threadIdx.x + t * NT;
+    const int ic = item < nk * nq ? item : 0;   // clamped: every load from a valid address
+    const int q = ic % nq;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = 4 * q + j;
+      R.loc[t][j] = D.loc[i * D.loc_stride];
+      R.sd[t][j] = sp[i * D.scale_stride];
+    }
+  }
+}
+template <int NT>
+__device__ __forceinline__ void draw_theta(const mi_linear& L, int64_t kbase, int nk, float* dst,
+                                           int dstr, bool write_theta, bool write_scale,
+                                           const DrawRegs& R) {
+  const mi_draw& D = L.draw;
+  const int nq = (int)L.P / 4;
+  const bool exp_scale = D.scale_exp != nullptr;
+#pragma unroll
+  for (int t = 0; t < kDrawItems; ++t) {
+    const int item = (int)threadIdx.x + t * NT;
+    if (item >= nk * nq) break;
     const int kl = item / nq, q = item - kl * nq;
     const int64_t kk = kbase + kl;
     float e[4];
-    guide_normals(D.seed, step, D.stream_id, (uint64_t)(D.element_offset / 4 + q),
+    guide_normals(D.seed, R.step, D.stream_id, (uint64_t)(D.element_offset / 4 + q),
                   (uint64_t)(D.particle_offset + kk), e);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t i = 4 * q + j;
-      const float m = D.loc[i * D.loc_stride];
-      const float sd = exp_scale ? expf(D.scale_exp[i * D.scale_stride]) : D.scale[i * D.scale_stride];
-      const float z = fmaf(e[j], sd, m);
+      const float sd = exp_scale ? expf(R.sd[t][j]) : R.sd[t][j];
+      const float z = fmaf(e[j], sd, R.loc[t][j]);
       dst[kl * dstr + i] = z;
       if (write_theta) const_cast<float*>(L.theta)[kk * L.theta_stride_k + i * L.theta_stride_j] = z;
       if (write_scale && exp_scale && kl == 0) const_cast<float*>(D.scale)[i * D.scale_stride] = sd;
@@ -381,10 +411,14 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   // The block's particles' draws through the (still unused) X staging buffer into thf: called by
   // every thread after the first stage's loads are issued and before they are stored.
   constexpr int kDrawStride = S::PM + 1;   // odd row stride: lanes c read distinct banks
+  const int64_t draw_kbase = group * wt * 32;
+  const int draw_nk = (int)min((int64_t)wt * 32, K - draw_kbase);
+  DrawRegs dregs;
   auto draw_here = [&]() {
-    const int64_t kbase = group * wt * 32;
-    const int nk = (int)min((int64_t)wt * 32, K - kbase);
-    draw_theta<kMfThreads>(L, kbase, nk, xs, kDrawStride, row_block == 0, row_block == 0 && group == 0);
+    const int64_t kbase = draw_kbase;
+    const int nk = draw_nk;
+    draw_theta<kMfThreads>(L, kbase, nk, xs, kDrawStride, row_block == 0, row_block == 0 && group == 0,
+                           dregs);
     __syncthreads();
     const int kl = pt * 32 + c;
     const int klc = kl < nk ? kl : nk - 1;
@@ -466,6 +500,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       __syncthreads();
     }
     MI_LIN_STAMP(1);
+    if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
     if (drawn) draw_here();
     if (st0 < st1) store_stage();
@@ -494,6 +529,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     MI_LIN_STAMP(4);
     __syncthreads();
   }
+  if (!ONESTAGE && drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
   if (!ONESTAGE && st0 < st1) load_stage(st0);
   if (!ONESTAGE && drawn) draw_here();
   if (!ONESTAGE && st0 < st1) store_stage();
@@ -894,7 +930,8 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
     // theta drawn only by the matrix-core kernel, through its X staging buffer
     const int threads = g.mfma ? kMfVariants[g.variant].threads : 0;
     const int64_t lds_floats = (int64_t)((threads >= 512 ? 256 : 128) / std::max(1, g.pt)) * (32 * g.pt + 4);
-    if (!g.mfma || site->P % 4 != 0 || (int64_t)g.wt * 32 * (32 * g.pt + 1) > lds_floats)
+    if (!g.mfma || site->P % 4 != 0 || (int64_t)g.wt * 32 * (32 * g.pt + 1) > lds_floats ||
+        (int64_t)g.wt * 32 * (site->P / 4) > (int64_t)mi::kDrawItems * threads)
       return MI_EUNSUPPORTED;
   }
   float* part = static_cast<float*>(workspace);
