@@ -1305,6 +1305,17 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
 }
 
 // particles per reducing block for long segment lists (MININF_AMD_ELBO_KRED: 16, 32 or 64)
+// particles per reducing block for very long segment lists over few particles
+// (MININF_AMD_ELBO_KRED_LONG: 8 or 16)
+int env_kred_long() {
+  static const int v = [] {
+    const char* e = getenv("MININF_AMD_ELBO_KRED_LONG");
+    const int n = e != nullptr ? atoi(e) : 16;
+    return (n == 8 || n == 16) ? n : 16;
+  }();
+  return v;
+}
+
 int env_kred() {
   static const int v = [] {
     const char* e = getenv("MININF_AMD_ELBO_KRED");
@@ -1330,7 +1341,7 @@ Layout make_layout(const mi_elbo* e) {
     L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
     // long lists over few particles (a fused draw's block rows: ~1000 segments, K = 128): 16
     // particles x 16 segment groups per block, for more blocks and fewer serial loads per lane
-    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? 16
+    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? env_kred_long()
                     : (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred()
                                                                      : mi::kRedKWide;
     nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
