@@ -126,6 +126,14 @@ def graph_safe(collector: list):
         Distribution.set_default_validate_args(previous)
 
 
+def _check_warmup(collector: list) -> int:
+    """Raise a warm-up step's validation errors; the number of its validation words. (A function
+    of its own: no loop variable outlives it holding a joint, and with it the step's graph.)"""
+    for joint in collector:
+        joint.raise_on_violation()
+    return sum(joint.flag_count() for joint in collector)
+
+
 def _detached(out):
     if isinstance(out, torch.Tensor):
         return out.detach()
@@ -224,11 +232,11 @@ class StepGraph:
                 collector: List = []
                 with graph_safe(collector), _capture_safe_distributions():
                     (warmup_step or step)()
-                for joint in collector:
-                    joint.raise_on_violation()
-                count = sum(joint.flag_count() for joint in collector)
+                count = _check_warmup(collector)
                 # the joints hold the step's loss: drop them, or the warm-up's autograd graph
-                # (its AccumulateGrad nodes on this side stream) stays alive into the capture
+                # (its AccumulateGrad nodes on this side stream) stays alive into the capture --
+                # a loop variable bound to the last joint did exactly that (the AccumulateGrad
+                # stream warning of the first captured backward)
                 del collector
         torch.cuda.current_stream().wait_stream(side)
         # Validation results must survive replays the host does not inspect: the step's words are
