@@ -126,6 +126,24 @@ def graph_safe(collector: list):
         Distribution.set_default_validate_args(previous)
 
 
+def _release_graph_refs(joints: list) -> None:
+    """
+    After a capture only the validation words (and the sites' names and order, for the messages)
+    are read from the joints: drop their loss and the sites' particle tensors, which reach the
+    captured step's autograd graph (the guide draws' nodes and the parameters' AccumulateGrad
+    nodes, created on the capture stream -- kept alive, a later capture's warm-up on another
+    stream warns about them).
+    """
+    for joint in joints:
+        if hasattr(joint, "total"):
+            joint.total = None
+        for _, _, sites in getattr(joint, "pending", ()):
+            for site in sites:
+                site.tensors = []
+                site.linear_theta = None
+                site.linear_X = None
+
+
 def _check_warmup(collector: list) -> int:
     """Raise a warm-up step's validation errors; the number of its validation words. (A function
     of its own: no loop variable outlives it holding a joint, and with it the step's graph.)"""
@@ -338,9 +356,7 @@ class StepGraph:
                 self._flags_device = None
                 self._accumulator = None
         self._joints = steps[0]
-        for joint in self._joints:
-            if hasattr(joint, "total"):
-                joint.total = None   # only the validation words are read after the capture
+        _release_graph_refs(self._joints)
         return mirror
 
     def __call__(self):

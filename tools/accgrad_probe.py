@@ -84,7 +84,7 @@ def main():
                    if isinstance(o, torch.Tensor) and getattr(o, "grad_fn", None) is not None]
         print(f"before capture: {len(nodes)} custom-Function nodes, {len(tensors)} tensors with "
               "grad_fn", flush=True)
-        for o in (nodes + tensors)[:6]:
+        for o in (nodes + tensors)[:10]:
             print(" ", describe(o))
             for r in gc.get_referrers(o)[:5]:
                 print("    <-", describe(r))
@@ -97,6 +97,10 @@ def main():
         graph()
         torch.cuda.synchronize()
         print("StepGraph: no warning", flush=True)
+        graph2 = StepGraph(step, warmup=2)   # a second capture after the first (bench: C2 floor)
+        graph2()
+        torch.cuda.synchronize()
+        print("second StepGraph: no warning", flush=True)
     except Exception:
         traceback.print_exc()
 
