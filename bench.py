@@ -88,6 +88,71 @@ class _GcClock:
         gc.callbacks.remove(self._callback)
 
 
+class Watchdog:
+    """
+    Host deadline for every phase of a run ("Next round" 2): a rank whose phase --
+    rendezvous, warm-up, capture, a timed loop of replays -- has not finished within its limit
+    prints which config and phase it was in (one JSON line on stdout, also on stderr) and ends with
+    exit status 3. A collective that never completes (a peer lost inside a captured RCCL
+    all-reduce) then fails the run bounded, naming the config, instead of blocking until the
+    driver kills it. The exit is os._exit from this thread: the main thread may be blocked inside a
+    HIP or RCCL call that cannot be unwound; nothing is re-executed.
+    """
+    def __init__(self, rank: int, limit_s: float) -> None:
+        import threading
+        self.rank, self.limit_s = rank, limit_s
+        self._cond = threading.Condition()
+        self._phase, self._deadline = None, None
+        self._thread = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
+        self._thread.start()
+
+    def arm(self, phase: str, seconds: float | None = None) -> None:
+        with self._cond:
+            self._phase = phase
+            self._deadline = time.monotonic() + (seconds or self.limit_s)
+            self._cond.notify()
+
+    def disarm(self) -> None:
+        with self._cond:
+            self._phase, self._deadline = None, None
+            self._cond.notify()
+
+    def _run(self) -> None:
+        while True:
+            with self._cond:
+                if self._deadline is None:
+                    self._cond.wait()
+                    continue
+                left = self._deadline - time.monotonic()
+                if left > 0:
+                    self._cond.wait(left)
+                    continue
+                phase = self._phase
+            line = json.dumps({"metric": METRIC, "error": "deadline", "rank": self.rank,
+                               "phase": phase, "limit_s": self.limit_s})
+            print(line, flush=True)
+            print(f"bench.py rank {self.rank}: {phase} did not finish within {self.limit_s:.0f} s",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
+
+
+WATCHDOG: Watchdog | None = None
+
+
+def arm(phase: str) -> None:
+    if WATCHDOG is not None:
+        WATCHDOG.arm(phase)
+
+
+def wait_device(device) -> None:
+    """torch.cuda.synchronize() as an event poll: the host keeps running Python (and the
+    watchdog its deadline) while the device drains."""
+    event = torch.cuda.Event()
+    event.record(torch.cuda.current_stream(device))
+    while not event.query():
+        time.sleep(20e-6)
+
+
 # ------------------------------------------------------------------------------------------------
 # Workloads (restated from the reference's README / examples, SURVEY.md 8(d)).
 # ------------------------------------------------------------------------------------------------
@@ -339,8 +404,21 @@ def check_launch(args, world, rank):
     return 0
 
 
+_COMMUNICATOR = None
+
+
+def communicator(group, device):
+    """The run's one RCCL communicator (mininf_amd.rccl), shared by every config: graphs of an
+    earlier config may still hold its captured collective."""
+    global _COMMUNICATOR
+    if _COMMUNICATOR is None:
+        _COMMUNICATOR = rccl.Communicator(group, device)
+    return _COMMUNICATOR
+
+
 def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budget):
     """Measure one workload (all ranks); rank 0 gets the bench line's dict."""
+    arm(f"{config}: set-up")
     w = workload(config, device, world, rank)
     if args.particles_per_gpu:
         w["evals"] = w["evals"] // w["k_local"] * args.particles_per_gpu
@@ -366,7 +444,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     collective_in_graph = sharded and args.dist_backend == "nccl"
     # over RCCL the all-reduce runs on a communicator of our own (mininf_amd.rccl: RCCL called
     # directly, no process-group watchdog polling events of the captured collective)
-    comm = rccl.Communicator(group, device) if collective_in_graph else None
+    comm = communicator(group, device) if collective_in_graph else None
     # data sharding reduces only the replicated (shared) parameters' gradients; every rank
     # updates its own slice of the rest
     bucket = GradientBucket(w.get("reduce_params") or module.parameters(), group, with_loss=True,
@@ -398,7 +476,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
-        torch.cuda.synchronize()
+        wait_device(device)
 
     def timed(run, steps):
         barrier()
@@ -419,8 +497,11 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         return full_step().detach()
 
     # Eager steps: every kernel launched from Python (the kernel timing comes from these).
+    arm(f"{config}: eager warm-up")
     for _ in range(warmup):
         eager_step()
+    wait_device(device)
+    arm(f"{config}: timed eager steps")
     timer.active = True
     eager_steps = max(3, steps // 3) if args.graph else steps
     gc_clock = _GcClock()
@@ -428,7 +509,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         eager_elapsed, loss = timed(eager_step, eager_steps)
     timer.active = False
     eager_ms = 1e3 * eager_elapsed / eager_steps
-    torch.cuda.synchronize()
+    wait_device(device)
     elapsed, mode = eager_elapsed * steps / eager_steps, "eager"
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
@@ -439,6 +520,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
             repeat = args.graph_repeat or next(r for r in (8, 6, 5, 4, 3, 2, 1) if steps % r == 0)
             if steps % repeat:
                 raise SystemExit(f"--graph-repeat {repeat} does not divide --steps {steps}")
+        arm(f"{config}: graph capture")
         if not sharded or collective_in_graph:
             # RCCL's watchdog thread polls events during the capture: thread-local capture mode
             graph_step = StepGraph(full_step, warmup=2, repeat=repeat,
@@ -456,8 +538,11 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 update()
                 return bucket.loss()
 
+        arm(f"{config}: graph warm-up replays")
         for _ in range(max(1, warmup // repeat)):
             graph_step()
+        wait_device(device)
+        arm(f"{config}: timed graph replays ({steps // repeat} replays of {repeat} steps)")
         elapsed, loss = timed(graph_step, steps // repeat)
         captured.check()
         mode = "hipGraph replay" + (f" ({repeat} steps per replay)" if repeat > 1 else "")
@@ -469,6 +554,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
             # C2's per-eval sum over x_i l_k is reducible to l_k sum_i x_i:
             # the same step with the site kernel's closed form, reported beside the per-eval number
             os.environ["MININF_AMD_BCAST_SUFFSTAT"] = "1"
+            arm(f"{config}: reducible-floor graph")
             try:
                 floor_graph = StepGraph(forward_backward, warmup=2, repeat=repeat)
                 for _ in range(max(1, warmup // repeat)):
@@ -492,7 +578,13 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         pstats.Stats(profiler, stream=sys.stderr).sort_stats("cumulative").print_stats(45)
 
     ms = 1e3 * elapsed / steps
-    value = w["evals"] * world * steps / elapsed
+    evals_all = w["evals"] * world
+    if world > 1:   # data-sharded slices differ by an element or an observation: count them all
+        import torch.distributed as dist
+        t = torch.tensor([float(w["evals"])], device=device, dtype=torch.float64)
+        dist.all_reduce(t)
+        evals_all = float(t)
+    value = evals_all * steps / elapsed
     kernel_ms, launches = timer.mean_ms(w["dominant_N"])
     kernel_s = kernel_ms * 1e-3
     if w["bound"] in ("valu", "mfma"):
@@ -538,6 +630,10 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                                  else "torch.optim.Adam(fused=True)")},
         "roofline": roof,
     }
+    out["config"]["ranks"] = world
+    out["scaling"] = "weak" if shard is None else "strong"
+    if WATCHDOG is not None:
+        WATCHDOG.disarm()
     if rank == 0 and world == 1 and cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline(config, cpu_budget)
     return out
@@ -580,6 +676,9 @@ def main():
                          "at N = 1: measures the N > 1 step's own overhead on one GPU")
     ap.add_argument("--profile-host", action="store_true",
                     help="cProfile 20 extra steps and print the hottest host functions to stderr")
+    ap.add_argument("--deadline", type=float, default=120.0,
+                    help="seconds any phase (rendezvous, warm-up, capture, a timed loop) may take "
+                         "before the rank prints the config and phase and exits with status 3")
     ap.add_argument("--check-launch", action="store_true",
                     help="rendezvous and one all-reduce only, no GPU work: prints the line's "
                          "n_gpus (tests the --gpus launch path on a CPU host)")
@@ -596,22 +695,27 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
     if args.check_launch:
         raise SystemExit(check_launch(args, world, rank))
+    global WATCHDOG
+    WATCHDOG = Watchdog(rank, args.deadline)
     global DATA_SHARD, DATA_SHARD_WORLD, DATA_SHARD_RANK
-    DATA_SHARD = args.shard == "data" or (args.shard == "auto" and args.config == "c5" and
+    # (the layout applies to C5 only, also when C5 runs after the default C2 line)
+    DATA_SHARD = args.shard == "data" or (args.shard == "auto" and
                                           (world > 1 or args.shard_world > 1))
     DATA_SHARD_WORLD, DATA_SHARD_RANK = args.shard_world, args.shard_rank
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     group = None
     if world > 1 or args.process_group:
+        import datetime
         import torch.distributed as dist
-        init = {}
+        arm("process-group rendezvous")
+        init = {"timeout": datetime.timedelta(seconds=args.deadline)}
         if "MASTER_ADDR" not in os.environ:   # --process-group without a launcher: one rank
             import socket
             with socket.socket() as sock:
                 sock.bind(("127.0.0.1", 0))
                 port = sock.getsockname()[1]
-            init = dict(init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+            init.update(init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device, **init)
         else:
@@ -620,21 +724,28 @@ def main():
 
     out = run_config(args.config, args, world, rank, device, group, args.steps, args.warmup,
                      0.0 if args.no_cpu_baseline else 12.0)
-    if world == 1 and group is None and args.config == "c2" and not args.no_other_configs:
-        # the other single-GPU configurations of BASELINE.json, measured in the same run
-        # (shorter: 10 graph-replayed steps each; CPU baseline only for C3)
+    others = ()
+    if args.config == "c2" and not args.no_other_configs:
+        # the other configurations of BASELINE.json, measured in the same run (shorter: 10
+        # graph-replayed steps each; CPU baseline only for C3 at N = 1): C3 is a one-GPU config;
+        # C4 (particle-sharded, 32 particles per GPU: 256 at N = 8) and C5 (data-sharded, all
+        # 1024 particles on each rank's element slice) are the multi-GPU ones
+        others = ("c3", "c4", "c5") if world == 1 and group is None else ("c4", "c5")
+    if others:
         out["other_configs"] = {}
-        for name in ("c3", "c4", "c5"):
+        for name in others:
             sub = run_config(name, args, world, rank, device, group, min(args.steps, 10), 3,
                              0.0 if (args.no_cpu_baseline or name != "c3") else 8.0)
             out["other_configs"][name] = {key: sub[key] for key in (
-                "value", "unit", "ms_per_step", "config", "roofline", "cpu_baseline")
+                "value", "unit", "ms_per_step", "scaling", "config", "roofline", "cpu_baseline")
                 if key in sub}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:
         import torch.distributed as dist
+        arm("process-group teardown")
         dist.destroy_process_group()
+    WATCHDOG.disarm()
 
 
 if __name__ == "__main__":

@@ -262,12 +262,14 @@ class _GroupLauncher:
                 return False
         return True
 
-    def describe(self, compute_grads: bool, fuse_exp: bool = False):
+    def describe(self, compute_grads: bool, fuse_exp: bool = False, query: bool = False):
         """
         The ctypes ``mi_group`` descriptor of this group plus freshly allocated dense gradient
         buffers (one per DENSE operand, None otherwise). ``fuse_exp``: a fused draw whose guide
         scale still waits for its exp transform reads the unconstrained parameter instead
-        (``mi_draw.scale_exp``); otherwise the transform is launched first.
+        (``mi_draw.scale_exp``); otherwise the transform is launched first. ``query``: for a plan
+        query only (``mi_group_prior_supported``): nothing is launched or allocated -- no pending
+        transform or gather runs, and dense gradients get a placeholder address.
         """
         device = self.device
         K, N = self.K, self.N
@@ -299,7 +301,7 @@ class _GroupLauncher:
                     # the guide's deferred exp transform runs inside the site program, which
                     # writes the scale for the autograd of the transform (run() marks it filled)
                     self.exp_pending, dw.scale_exp = source
-                else:
+                elif not query:
                     guide.fill_exp(d.scale)   # a deferred transform runs before the kernel reads it
                 dw.seed, dw.step = guide._philox_key(d.cfg)
                 dw.step_device = nat.ptr(d.cfg.step_device)
@@ -307,6 +309,8 @@ class _GroupLauncher:
                 dw.element_offset = d.cfg.element_offset
                 if mode == nat.GRAD_DENSE and self.draw_partials:
                     group.options |= nat.GROUP_DRAW_PARTIALS
+                elif mode == nat.GRAD_DENSE and query:
+                    dw.dloc = dw.dscale = _QUERY_ADDRESS
                 elif mode == nat.GRAD_DENSE:
                     dloc = torch.empty(N, dtype=torch.float32, device=device)
                     dscale = torch.empty(N, dtype=torch.float32, device=device)
@@ -314,10 +318,14 @@ class _GroupLauncher:
                     grad = (dloc, dscale)
                 grads.append(grad)
                 continue
-            data.ensure_filled(view.tensor)   # a minibatch read directly: gather its rows
+            if not query:
+                data.ensure_filled(view.tensor)   # a minibatch read directly: gather its rows
             desc.data = view.tensor.data_ptr()
             desc.stride_k, desc.stride_i = view.sk, view.si
-            if mode == nat.GRAD_DENSE:
+            if mode == nat.GRAD_DENSE and query:
+                desc.grad = _QUERY_ADDRESS
+                desc.grad_stride_k, desc.grad_stride_i = view.sk, view.si
+            elif mode == nat.GRAD_DENSE:
                 sk, si = view.sk, view.si
                 if (sk, si) in ((N, 1), (1, K)):
                     grad = torch.empty_strided((K, N), (sk, si), dtype=torch.float32, device=device)
@@ -337,7 +345,8 @@ class _GroupLauncher:
                 desc.operand[q] = roles[q][0]
                 desc.constant[q] = roles[q][1]
             if mask is not None:
-                data.ensure_filled(mask.tensor)
+                if not query:
+                    data.ensure_filled(mask.tensor)
                 desc.mask = mask.tensor.data_ptr()
                 desc.mask_stride_k, desc.mask_stride_i = mask.sk, mask.si
             desc.scale = site.scale
@@ -671,12 +680,13 @@ class _LinearLauncher:
             # this launch shape does not draw theta: the guide's own draw first
             self.draw.launch()
             guide.take_draw(self.draw)
-            zeroed, prior_flags, rows = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags, L.rows
-            L = self.describe(compute_grads, draw_rows=False, draw=False)
+            zeroed, prior_flags = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags
+            # the batch is still pending (take_rows changes nothing), so this descriptor draws
+            # the rows in the launch again; reading batch.rows here would launch the rows kernel
+            # AND leave them to this launch: the loader counter would advance twice
+            L = self.describe(compute_grads, draw=False)
             L.options |= zeroed
             L.prior.flags = prior_flags
-            if rows.counter:
-                L.rows, L.row_index = rows, None
             code = launch(L)
         elif L.draw.operand and code == 0:
             guide.take_draw(self.draw)
@@ -983,6 +993,10 @@ def plan_groups(trace: ParticleTrace, g0: float, device: torch.device):
 _PRIOR_FAMILIES = ("beta", "normal", "gamma")
 
 
+# a non-null address for descriptors that are only queried (never dereferenced)
+_QUERY_ADDRESS = 1 << 20
+
+
 def fold_priors(launchers: List[_GroupLauncher]) -> List[_GroupLauncher]:
     """
     Fold one-element-per-particle prior sites into the launch of the site that reads the same
@@ -1014,8 +1028,8 @@ def fold_priors(launchers: List[_GroupLauncher]) -> List[_GroupLauncher]:
             if param.view.key != value.view.key or param.mode != value.mode:
                 continue
             host.prior = (site, FAMILY_CODES[site.family], (roles[0][1], roles[1][1]))
-            group, _ = host.describe(True)
-            group.prior.flags = 1 << 20   # (any non-null word: only the plan is queried)
+            group, _ = host.describe(True, query=True)
+            group.prior.flags = _QUERY_ADDRESS
             supported = ctypes.c_int(0)
             nat.check(lib.mi_group_prior_supported(ctypes.byref(group), ctypes.byref(supported)),
                       "mi_group_prior_supported")

@@ -278,10 +278,14 @@ class StepGraph:
         gc.collect()
         gc_was_enabled = gc.isenabled()
         gc.disable()
+        from . import particles
         with torch.cuda.stream(capture_stream):
             self.graph.capture_begin(capture_error_mode=capture_error_mode)
             try:
-                with graph_safe(self._joints), _capture_safe_distributions():
+                # the cached device copies of host constants the captured step reads live as long
+                # as the graph (particles.device_copy's cache may evict them)
+                with graph_safe(self._joints), _capture_safe_distributions(), \
+                        particles.pin_device_copies() as self._pinned:
                     for _ in range(repeat):
                         # detached: holding the captured step's autograd graph would keep its
                         # AccumulateGrad nodes (and their capture stream) alive past the capture

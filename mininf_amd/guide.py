@@ -38,6 +38,9 @@ class DrawConfig:
     step_snapshot: Optional[torch.Tensor] = None
     # global index of element 0 (data-sharded factors, mininf_amd.distributed.DataShard)
     element_offset: int = 0
+    # the factor is data-sharded (every rank draws its slice), also on the rank whose slice
+    # starts at element 0
+    sharded: bool = False
     # small Normal factors: leave the launch to the loss's planning (PendingDraw), which may hand
     # the draw to the linear site kernel that reads it (mi_linear.draw)
     defer: bool = False
@@ -621,7 +624,7 @@ def draw(distribution: Distribution, cfg: DrawConfig, lazy: bool = False) -> tor
     K reparameterised draws of one guide factor: shape [K, *batch_shape, *event_shape].
     """
     cls = type(distribution)
-    if cfg.element_offset and cls is not Normal:
+    if (cfg.sharded or cfg.element_offset) and cls is not Normal:
         raise nat.NativeError(f"a data-sharded guide factor must be a Normal (got {cls.__name__}): "
                               "only the Normal sampler draws element slices of a global draw")
     if cfg.element_offset % 4:
@@ -693,6 +696,8 @@ def draw_all(approximation: Dict[str, Distribution], K: int, seed: int, step: in
                          particle_offset=particle_offset,
                          noise=None if noise is None else noise.get(name),
                          step_device=step_device, step_snapshot=step_snapshot,
-                         element_offset=(element_offsets or {}).get(name, 0), defer=lazy)
+                         element_offset=(element_offsets or {}).get(name, 0),
+                         sharded=element_offsets is not None and name in element_offsets,
+                         defer=lazy)
         samples[name] = draw(factor, cfg, lazy)
     return samples

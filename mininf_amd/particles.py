@@ -145,30 +145,63 @@ _HOST_COPIES: "collections.OrderedDict[Tuple, Tuple[torch.Tensor, torch.Tensor]]
     collections.OrderedDict()
 
 
+# device copies read by the step being captured (StepGraph keeps them for the graph's lifetime:
+# the LRU below may evict an entry while a graph still reads its copy)
+_PINS: Optional[List[torch.Tensor]] = None
+
+
+@contextlib.contextmanager
+def pin_device_copies():
+    """Collect every device copy ``device_copy`` hands out inside the block (a capture)."""
+    global _PINS
+    saved, _PINS = _PINS, []
+    try:
+        yield _PINS
+    finally:
+        _PINS = saved
+
+
+def _content_digest(t: torch.Tensor) -> Optional[bytes]:
+    """blake2b of a host tensor's values (None when numpy cannot view them)."""
+    data = t.detach().resolve_conj().resolve_neg().contiguous()
+    if data.dtype == torch.bfloat16:
+        data = data.view(torch.int16)
+    try:
+        return hashlib.blake2b(data.numpy().tobytes(), digest_size=16).digest()
+    except (TypeError, RuntimeError):
+        return None
+
+
 def device_copy(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     """
     A cached device copy of an unbatched host tensor (keyed on storage, layout and version), so a
     constant such as the 2.0 of ``Gamma(2.0, 2.0)`` is copied once, not on every step (and not
     inside a captured graph).
     """
+    out = _device_copy(t, device)
+    if _PINS is not None:
+        _PINS.append(out)
+    return out
+
+
+def _device_copy(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t._version, str(device))
     hit = _HOST_COPIES.get(key)
+    digest = None
     if hit is None and t.numel() * t.element_size() <= _CONTENT_KEY_BYTES:
+        digest = _content_digest(t)
+    if digest is not None:
         # A small host intermediate the model computes afresh on every call (the GP example's
         # `x[:, None] - x`, examples/missing-observations.md:40) is a new tensor each time: key it
         # by its contents, so a captured step finds the copy its warm-up made instead of a
         # host-to-device copy, which a capturing stream refuses.
-        data = t.detach().contiguous()
-        content = ("content", tuple(t.shape), t.dtype, str(device),
-                   hashlib.blake2b(data.numpy().tobytes() if data.dtype != torch.bfloat16 else
-                                   data.view(torch.int16).numpy().tobytes(),
-                                   digest_size=16).digest())
+        content = ("content", tuple(t.shape), t.dtype, str(device), digest)
         hit = _HOST_COPIES.get(content)
         if hit is not None:
             _HOST_COPIES.move_to_end(content)
             return hit[1]
         key = content
-        t = data
+        t = t.detach().resolve_conj().resolve_neg().contiguous()
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError(

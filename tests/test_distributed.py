@@ -163,3 +163,14 @@ def test_data_shard_validation():
     # every rank evaluates every particle; the loss knows the world from the shard
     assert loss._shard() == (4, 0, 16, 0)
     assert loss._element_offsets({"mu": None, "z": None}) == {"z": 0}
+
+
+@pytest.mark.parametrize("offset", [0, 500])
+def test_sharded_non_normal_factor_is_rejected_on_every_rank(offset):
+    """A data-sharded Beta factor is rejected by the rank whose slice starts at element 0 as well
+    (rank 0 accepted it and went on to the collective while the others raised)."""
+    from torch.distributions import Beta
+    from mininf_amd import _native as nat, guide
+    factor = Beta(torch.full((1000,), 2.0), torch.full((1000,), 3.0))
+    with pytest.raises(nat.NativeError, match="must be a Normal"):
+        guide.draw_all({"p": factor}, 4, 0, 0, 0, element_offsets={"p": offset})

@@ -58,3 +58,34 @@ def test_bench_two_gloo_ranks_match_one_rank(device):
     assert one["n_gpus"] == 1 and one["config"]["global_particles"] == 64
     assert "gloo all-reduce" in two["config"]["step_mode"]
     assert two["config"]["final_loss"] == pytest.approx(one["config"]["final_loss"], rel=1e-5)
+
+
+def test_bench_two_gloo_ranks_match_one_rank_c5_data_sharded(device):
+    """C5 data-sharded (DataShard: each rank all 1024 particles on half the elements, mu's
+    gradients and the loss all-reduced) against one rank over all elements: the same final loss
+    within 1e-5 after the same steps ("Next round" 2)."""
+    common = ["--config", "c5", "--shard", "data", "--steps", "4", "--warmup", "2",
+              "--graph-repeat", "1", "--no-other-configs", "--no-cpu-baseline"]
+    two = _last_json(_bench("--gpus", "2", "--dist-backend", "gloo", *common))
+    one = _last_json(_bench(*common))
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["global_particles"] == one["config"]["global_particles"] == 1024
+    assert "data-sharded x2" in two["config"]["parallelism"]
+    assert two["scaling"] == "strong"
+    assert two["config"]["final_loss"] == pytest.approx(one["config"]["final_loss"], rel=1e-5)
+
+
+def test_bench_n2_default_run_measures_c4_and_c5(device):
+    """`bench.py --gpus 2` (default C2 line) also measures C4 and C5 under other_configs, each
+    entry carrying its rank count and layout."""
+    line = _last_json(_bench("--gpus", "2", "--dist-backend", "gloo", "--steps", "4", "--warmup",
+                             "2", "--graph-repeat", "1", "--no-cpu-baseline"))
+    assert line["n_gpus"] == 2 and line["config"]["ranks"] == 2
+    others = line["other_configs"]
+    assert sorted(others) == ["c4", "c5"]
+    assert others["c4"]["config"]["ranks"] == 2 and others["c4"]["scaling"] == "weak"
+    assert others["c4"]["config"]["global_particles"] == 64
+    assert others["c5"]["config"]["ranks"] == 2 and others["c5"]["scaling"] == "strong"
+    assert "data-sharded x2" in others["c5"]["config"]["parallelism"]
+    for entry in others.values():
+        assert entry["value"] > 0 and entry["ms_per_step"] > 0

@@ -133,3 +133,87 @@ def test_c5_fused_draw_full_size_against_oracle(device):
     _close(float(mu_p["scale"].grad), ref["grad_mu_scale"], "grad mu log-scale")
     _close(z_p["loc"].grad.cpu(), ref["grad_z_loc"], "grad z loc")
     _close(z_p["scale"].grad.cpu(), ref["grad_z_scale"], "grad z log-scale")
+
+
+def test_c4_full_size_bench_configuration(device, monkeypatch):
+    """
+    C4 exactly as bench.py runs it (BASELINE.json configs[3] per GPU: X[1e7, 32] resident,
+    DeviceDataLoader(batch_size=65536, shuffle=True), K = 32): the batch's rows drawn inside the
+    linear launch (mi_linear.rows), theta drawn by the same launch (mi_linear.draw), the prior
+    folded into it (mi_linear.prior) and the final gradients written by the ELBO forward -- with
+    nothing injected. Two consecutive training steps (Adam between them) against the Gram-form
+    oracle on the rows of oracle/minibatch.py and the eps of liboracle (stream 0, steps 0 and 1),
+    batch scale 1e7 / 65536 (/root/reference/examples/minibatch.md:76-88). 1e-5 relative.
+    """
+    from mininf_amd import _native as nat, guide as guide_mod
+    from mininf_amd.data import DeviceDataLoader
+    from mininf_amd.optim import Adam
+    from oracle import minibatch as mb_oracle
+    n_total, p, B, K, seed, loader_seed = 10_000_000, 32, 65536, 32, 1, 0
+    gen = torch.Generator(device=device).manual_seed(0)
+    X = torch.randn(n_total, p, generator=gen, device=device)
+    y = X @ torch.randn(p, generator=gen, device=device) + \
+        torch.randn(n_total, generator=gen, device=device)
+
+    def model():
+        theta = mi.sample("theta", Normal(0, 1), sample_shape=p)
+        with mi.batch(n_total):
+            with mi.no_log_prob():
+                Xs = mi.sample("X", Normal(0, 1), sample_shape=(n_total, p))
+            mi.sample("y", Normal(Xs @ theta, 1))
+
+    hgen = torch.Generator().manual_seed(3)
+    module = mi.nn.ParameterizedDistribution(
+        Normal, loc=1e-3 * torch.randn(p, generator=hgen),
+        scale=(1e-3 * torch.randn(p, generator=hgen)).exp()).to(device)
+    optimizer = Adam(module.parameters(), lr=0.01)
+    loader = DeviceDataLoader(X, y, batch_size=B, shuffle=True, drop_last=True, seed=loader_seed)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed)
+
+    separate_draws, backward_calls = [], []
+    real_launch = guide_mod.PendingDraw.launch
+
+    def spy_launch(self):
+        if not self.done:
+            separate_draws.append(tuple(self.z.shape))
+        return real_launch(self)
+    monkeypatch.setattr(guide_mod.PendingDraw, "launch", spy_launch)
+    lib = nat.lib()
+    real_backward = lib.mi_elbo_backward
+
+    def spy_backward(*args):
+        backward_calls.append(1)
+        return real_backward(*args)
+    monkeypatch.setattr(lib, "mi_elbo_backward", spy_backward)
+
+    lib_o = oracle_build.load()
+    batches = n_total // B
+    for step in range(2):
+        optimizer.zero_grad(set_to_none=True)
+        Xb, yb = loader.next()
+        batch = Xb._mininf_batch
+        q = module()
+        loss = loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": q})
+        loss.backward()
+        assert not batch.pending, "the linear launch should draw the batch's rows"
+        loc = q.loc.detach().cpu().numpy().astype(np.float32)
+        scale = q.scale.detach().cpu().numpy().astype(np.float32)
+        grads = {name: prm.grad.detach().cpu().numpy().copy()
+                 for name, prm in module.distribution_parameters.items()}
+        value = float(loss)
+        optimizer.step()
+
+        rows = mb_oracle.batch_rows(step, n_total, B, batches, True, loader_seed, B)
+        idx = torch.as_tensor(rows, device=device)
+        Xr = X[idx].double().cpu().numpy()
+        yr = y[idx].double().cpu().numpy()
+        eps = np.empty((K, p), np.float32)
+        lib_o.oracle_guide_normals(K, p, seed, step, 0, 0, eps.ctypes.data)
+        ref = oracle.regression_elbo_gram(Xr.T @ Xr, Xr.T @ yr, float(yr @ yr), B, loc, scale,
+                                          eps, batch_scale=n_total / B)
+        assert abs(value - ref["loss"]) <= 1e-5 * abs(ref["loss"]), (step, value, ref["loss"])
+        _close(grads["loc"], ref["grad_loc"], f"step {step} grad loc")
+        _close(grads["scale"], ref["grad_u_scale"], f"step {step} grad log-scale")
+    assert separate_draws == [], "theta should be drawn inside the linear launch"
+    assert backward_calls == [], "the ELBO forward should write the final gradients"
+    assert int(loader.counter[0]) == 2

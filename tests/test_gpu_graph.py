@@ -257,3 +257,96 @@ def test_graph_never_loses_a_transient_violation(device, family, host_looks):
         captured.check()
     captured()                             # cleared after raising: valid windows pass again
     captured.check()
+
+
+def test_captured_step_keeps_its_host_constant_copies(device):
+    """
+    A torch-evaluated site with host constants (StudentT(3., 0., 1.)) reads cached device copies
+    of them (particles.device_copy). StepGraph pins the copies its capture read, so evicting them
+    from the cache (more than 64 other copies) and reusing the freed memory leaves the replays
+    unchanged (a replay could read memory the caching allocator had handed out again).
+    """
+    from torch.distributions import StudentT
+    from mininf_amd import particles
+    x = torch.linspace(-2, 2, 100, device=device)
+
+    def model():
+        theta = mi.sample("theta", StudentT(3.0, 0.0, 1.0))
+        mi.sample("x", Normal(theta, 1.0), sample_shape=[100])
+
+    module = mi.nn.ParameterizedDistribution(Normal, loc=0.1, scale=0.8).to(device)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=64, seed=3)
+    cond = mi.condition(model, x=x)
+
+    def step():
+        for p in module.parameters():
+            p.grad = None
+        loss = loss_fn(cond, {"theta": module()})
+        loss.backward()
+        return loss
+
+    captured = StepGraph(step, warmup=2)
+    assert captured._pinned, "the capture should have read device copies of the constants"
+    loss_fn._counter.zero_()
+    before = float(captured())
+    for i in range(200):   # evict every cached copy, then reuse the freed blocks
+        particles.device_copy(torch.full((5,), float(i) + 0.5), device)
+    particles._HOST_COPIES.clear()
+    import gc
+    gc.collect()
+    junk = [torch.full((64,), 1e30, device=device) for _ in range(256)]
+    loss_fn._counter.zero_()
+    after = float(captured())
+    captured.check()
+    del junk
+    assert after == before
+
+
+def test_capture_survives_garbage_with_device_finalizers(device):
+    """
+    Garbage whose finalizers touch the device -- an earlier StepGraph (its hipGraph executable and
+    memory pool), a pinned host buffer written by a non-blocking copy, HIP events -- left in
+    reference cycles right before a StepGraph is built, with the collector set to run at every
+    allocation (commit 1bb8d71: a collection inside a capture ran such finalizers on the capturing
+    stream and aborted a bench run; StepGraph now collects before the capture and keeps the
+    collector off during it). Capture and replays succeed and match eager steps, and the
+    collector's state is restored afterwards.
+    """
+    import gc
+
+    class Cycle:
+        def __init__(self, payload):
+            self.payload = payload
+            self.me = self
+
+    eager_step, _, _ = coin_setup(device, n=2000, K=64)
+    eager = [float(eager_step()) for _ in range(5)]
+
+    body, _, _ = coin_setup(device, n=2000, K=64)
+    old_body, _, _ = coin_setup(device, n=2000, K=64)
+    old = StepGraph(old_body, warmup=1)
+    old()
+    old.check()
+    thresholds = gc.get_threshold()
+    gc.disable()   # the garbage survives until the StepGraph is built
+    try:
+        pinned = torch.empty(1024, pin_memory=True)
+        pinned.copy_(torch.ones(1024, device=device), non_blocking=True)
+        events = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+        for e in events:
+            e.record()
+        torch.cuda.synchronize()
+        Cycle(old)
+        Cycle(pinned)
+        Cycle(events)
+        del old, pinned, events
+        gc.set_threshold(1, 1, 1)
+        gc.enable()
+        captured = StepGraph(body, warmup=3)
+        assert gc.isenabled()
+    finally:
+        gc.set_threshold(*thresholds)
+        gc.enable()
+    losses = [float(captured()) for _ in range(2)]
+    captured.check()
+    torch.testing.assert_close(torch.tensor(losses), torch.tensor(eager[3:5]), rtol=1e-6, atol=0)

@@ -227,3 +227,47 @@ def test_linear_kernel_draws_the_batch_rows(device, monkeypatch):
         assert l0 == l1
         for a, b in zip(g0, g1):
             torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_unsupported_linear_draw_takes_the_batch_rows_once(device, monkeypatch):
+    """
+    The linear launch cannot draw theta for P = 64 features and K = 128 particles (its staging
+    buffer is too small for four particle tiles of two feature tiles) but can draw the batch's
+    rows: the draw falls back to the guide's own launch, and the rows are still drawn exactly once
+    per step -- the loader counter advances by one and every batch is the oracle's (ADVICE r03,
+    high: the fallback drew them twice, skipping every other batch).
+    """
+    from mininf_amd import guide as guide_mod
+    n, p, batch, K = 8192, 64, 1024, 128
+    X, y = regression(device, n=n, p=p)[1:]
+    launches = []
+    real = guide_mod.PendingDraw.launch
+
+    def spy(self):
+        if not self.done:
+            launches.append(tuple(self.z.shape))
+        return real(self)
+    monkeypatch.setattr(guide_mod.PendingDraw, "launch", spy)
+
+    def model():
+        theta = mi.sample("theta", Normal(0, 1), sample_shape=p)
+        with mi.batch(n):
+            with mi.no_log_prob():
+                Xs = mi.sample("X", Normal(0, 1), sample_shape=(n, p))
+            mi.sample("y", Normal(Xs @ theta, 1))
+
+    loader = DeviceDataLoader(X, y, batch_size=batch, shuffle=True, drop_last=True, seed=9)
+    module = mi.nn.ParameterizedDistribution(Normal, loc=torch.zeros(p),
+                                             scale=torch.ones(p)).to(device)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=2)
+    for step in range(3):
+        Xb, yb = loader.next()
+        b = Xb._mininf_batch
+        loss = loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": module()})
+        loss.backward()
+        assert int(loader.counter[0]) == step + 1
+        assert b.rows.cpu().tolist() == oracle.batch_rows(step, n, batch, n // batch, True, 9,
+                                                          batch)
+        for q in module.parameters():
+            q.grad = None
+    assert launches == [(K, p)] * 3, launches   # the guide's own draw, once per step
