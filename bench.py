@@ -620,6 +620,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                         f" + {args.dist_backend} grad all-reduce") if sharded else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms,
+                   "fusions": loss_fn.last_fusions,
                    "eager_gc_ms_per_step": gc_clock.seconds * 1e3 / eager_steps,
                    **({"reducible_floor_ms_per_step": floor_ms,
                        "reducible_floor_note": "the same step with the site kernel evaluating "

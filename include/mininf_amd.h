@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 12
+#define MI_ABI_VERSION 13
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -72,6 +72,7 @@ enum mi_grad_mode {
 
 #define MI_FLAG_SUPPORT 1u  /* a (non-masked) value lies outside the family's support */
 #define MI_FLAG_PARAM 2u    /* a parameter violates its constraint (e.g. scale <= 0) */
+#define MI_FLAG_INTERNAL 0x40000000u  /* an in-kernel completion wait gave up (never expected) */
 
 typedef struct mi_operand {
   const float* data;
@@ -542,6 +543,27 @@ int mi_linear_struct_size(size_t* bytes);
 int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
                                float* total, float* dslots, uint32_t* flags, void* start_event,
                                void* stop_event, void* stream, mi_reduce* reduce);
+
+/* The whole ELBO forward in the linear site's launch (ABI 13). For a step whose ELBO is this one
+ * site (with its folded prior) and one small Normal guide factor drawn by the same launch
+ * (mi_linear.draw) -- the minibatch regression of examples/minibatch.md:76-88 -- the launch's last
+ * blocks reduce its partials and run mi_elbo_forward's tail: `total` and `dslots` as the deferred
+ * reduction writes them, *loss as mi_elbo_forward (elbo: the step's descriptor with num_terms 0
+ * and num_reduce 0 -- the site's totals are not a term -- and factor 0 that Normal factor, its one
+ * source dslots), the factor's gradients for an upstream of 1 (as with MI_ELBO_FINAL_GRADS), the
+ * generator step advance and the flag mirror. One kernel instead of two (mi_linear_forward_deferred
+ * + mi_elbo_forward). The completion counters and fp64 sums live in `elbo_workspace` (an
+ * mi_elbo_forward workspace: zeroed counters, left zero). mi_linear_elbo_supported reports whether
+ * the pair qualifies (one-stage matrix-core launch with gradients whose whole grid is resident,
+ * K <= the block size, a short partial slab) and the elbo workspace it needs; otherwise
+ * mi_linear_elbo_forward returns MI_EUNSUPPORTED without launching. Replaces nn.py:224-228 for
+ * that step together with the site (core.py:241-273). */
+int mi_linear_elbo_supported(const mi_linear* site, const struct mi_elbo* elbo, int* supported,
+                             size_t* elbo_workspace_bytes);
+int mi_linear_elbo_forward(const mi_linear* site, const struct mi_elbo* elbo, void* workspace,
+                           size_t workspace_bytes, float* total, float* dslots, uint32_t* flags,
+                           void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
+                           void* start_event, void* stop_event, void* stream);
 
 /* ---- device-resident minibatches (replaces examples/minibatch.md:78-88, the host DataLoader) ---- */
 

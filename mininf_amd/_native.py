@@ -38,8 +38,8 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 12   # MI_ABI_VERSION of include/mininf_amd.h
-FLAG_SUPPORT, FLAG_PARAM = 1, 2
+ABI_VERSION = 13   # MI_ABI_VERSION of include/mininf_amd.h
+FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
 c_i64 = ctypes.c_int64
@@ -277,6 +277,12 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
     "mi_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "mi_linear_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo),
+                                                ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_linear_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo), c_vp,
+                                              ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
+                                              ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp]),
     "mi_elbo_final_grads": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
                                         c_vp]),

@@ -587,6 +587,11 @@ struct ReducePlan {
   int nt_j0;                             // slot of element 0
   int nt_nkb;                            // particle blocks of the job
   int64_t nt_part;                       // offset (doubles) of the [n][nt_nkb][2] partials
+  // A one-element Normal factor (the masked hierarchical model's mu) whose sources are slots of
+  // any jobs (nt_mask[a] bit j: job a's slot j): every reducing block adds its slots' share, by
+  // linearity, into its own partial (nt_nkb = the reducing blocks, indexed by block).
+  int nt_single;
+  int nt_mask[MI_MAX_REDUCE];
 };
 
 // Fields of factor f of the launch, by constant-index selects (see ReducePlan.tail_factor).
@@ -641,13 +646,16 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
   const int64_t kb = local / vb;
   const int v0 = vb > 1 ? local % vb : 0, v1 = vb > 1 ? v0 + 1 : nv;
   // this block's element of the Normal tail (split jobs: one value per block), or -1
-  const bool nt_on = (E.options & MI_ELBO_FINAL_GRADS) && a == R.nt_job && vb > 1;
+  const bool nt_fin = (E.options & MI_ELBO_FINAL_GRADS) && R.nt_job >= 0;
   nt_slot = -1;
-  if (nt_on) {
+  if (nt_fin && R.nt_single) {
+    nt_slot = 0;   // every reducing block writes its (possibly zero) share
+  } else if (nt_fin && a == R.nt_job && vb > 1) {
     const int j = v0 - J.num_sites;
     const int i = j - R.nt_j0;
     if (j >= 0 && i >= 0 && i < E.factors[0].n) nt_slot = i;
   }
+  const int nt_mask = nt_fin && R.nt_single ? pick(R.nt_mask, a) : 0;
   const int kl = threadIdx.x % kRedK, gl = threadIdx.x / kRedK;
   const int64_t K = J.K;
   const int64_t k = kb * kRedK + kl;
@@ -708,7 +716,8 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
         const int j = v - J.num_sites;
         const float gv = (float)(s * J.slot_scale);
         J.slot_grad[(int64_t)j * K + k] = gv;
-        if (nt_slot >= 0) {   // d z[k, i] for the Normal tail, against its regenerated eps
+        if (nt_slot >= 0 && (!R.nt_single || ((nt_mask >> j) & 1))) {
+          // d z[k, i] for the Normal tail, against its regenerated eps
           const mi_factor& F = E.factors[0];
           const uint64_t step = forward_step0(E);
           const int64_t i = nt_slot;
@@ -750,7 +759,7 @@ MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
   double share;
   // constant descriptor indices (a run-time index into the by-value kernel argument would copy
   // it to scratch memory)
-  nt_kb = local / vb;
+  nt_kb = R.nt_single ? bid : local / vb;
   switch (a) {
     case 1: share = reduce_job(E, E.g0, E.reduce[1], local, vb, kred, R, 1, c, red, nt, nt_slot); break;
     case 2: share = reduce_job(E, E.g0, E.reduce[2], local, vb, kred, R, 2, c, red, nt, nt_slot); break;
@@ -798,6 +807,13 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   const int nshare = nred + nloss;   // blocks that write a loss share
   if (ABSORB && (int)blockIdx.x >= nshare) {
     absorbed_block<true>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
+    return;
+  }
+  if (!ABSORB && (int)blockIdx.x >= nshare) {
+    // MI_ELBO_FINAL_GRADS: the gradients of the fused-draw factors (MI_DRAW_PARTIALS) for an
+    // upstream of 1 -- k_elbo_backward's absorbed blocks, run here (P: their plan); they read only
+    // the site launches' partial rows, so they run beside the reductions
+    absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
     return;
   }
   double* rsum = &red[0][0];
@@ -1209,13 +1225,17 @@ int64_t longest_factor(const mi_elbo* e) {
 // from kCounterFirst on; the forward's group counters (kGroupCounters words, 64 bytes apart) in
 // between.
 constexpr int64_t kCounterFirst = mi::kGroupCounterWord + mi::kGroupCounters * mi::kGroupCounterStride;
-constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned);
+// (the last 32 words belong to mi_linear_elbo_forward, linear.hip kLinFinishCounterWord)
+constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 32;
 
 // Launch plans of both kernels and the layout of the fp64 work area that follows the counters:
 // [loss partials | forward absorbed partials | backward absorbed partials]. All of it is scratch
 // of one launch; what the backward needs from the forward lives in the caller's mi_factor.saved.
 struct Layout {
   mi::AbsorbPlan fwd, bwd;
+  // MI_ELBO_FINAL_GRADS: the fused-draw factors' backward blocks, run by the forward launch
+  // (lead_blocks: the forward's)
+  mi::AbsorbPlan fin;
   mi::ReducePlan red;
   int64_t doubles;
 };
@@ -1395,8 +1415,36 @@ Layout make_layout(const mi_elbo* e) {
     for (int f = 0; f < 1 && f < e->num_factors; ++f) {   // factor 0 only (ReducePlan.nt_job)
       const mi_factor& F = e->factors[f];
       if (tail[f] || F.family != MI_NORMAL || F.draw_kind != MI_DRAW_SOURCES ||
-          F.num_sources != 1 || F.n > mi::kElboThreads || F.eps != nullptr)
+          F.n > mi::kElboThreads || F.eps != nullptr)
         continue;
+      if (F.n == 1 && F.num_sources >= 1) {
+        // one element, sources anywhere among the jobs' slots
+        int mask[MI_MAX_REDUCE] = {};
+        int matched = 0;
+        for (int src = 0; src < F.num_sources; ++src) {
+          const mi_source& S = F.source[src];
+          for (int r = 0; r < e->num_reduce && S.stride_k == 1; ++r) {
+            const mi_reduce& J = e->reduce[r];
+            const int64_t off = S.ptr - J.slot_grad;
+            if (J.slot_grad == nullptr || off < 0 || off % J.K != 0 || off / J.K >= J.num_slots ||
+                off / J.K >= 31)
+              continue;
+            mask[r] |= 1 << (int)(off / J.K);
+            ++matched;
+            break;
+          }
+        }
+        if (matched == F.num_sources) {
+          L.red.nt_single = 1;
+          for (int r = 0; r < MI_MAX_REDUCE; ++r) L.red.nt_mask[r] = mask[r];
+          L.red.nt_job = 0;
+          L.red.nt_j0 = 0;
+          L.red.nt_nkb = nred;
+          tail[f] = true;
+        }
+        continue;
+      }
+      if (F.num_sources != 1) continue;
       const mi_source& S = F.source[0];
       for (int r = 0; r < e->num_reduce; ++r) {
         const mi_reduce& J = e->reduce[r];
@@ -1432,8 +1480,23 @@ Layout make_layout(const mi_elbo* e) {
       add_absorbed(e, f, false, finish, L.bwd, counters, doubles, blocks);
     }
   L.bwd.first[L.bwd.num] = blocks;
+  L.fin.lead_blocks = L.fwd.lead_blocks;
+  blocks = 0;
+  if (!L.red.external)
+    for (int f = 0; f < e->num_factors; ++f)
+      if (e->factors[f].draw_kind == MI_DRAW_PARTIALS)
+        add_absorbed(e, f, false, false, L.fin, counters, doubles, blocks);
+  L.fin.first[L.fin.num] = blocks;
   L.doubles = doubles;
   return L;
+}
+
+// With MI_ELBO_FINAL_GRADS the forward finishes every factor: one-element Beta tails, the Normal
+// tail (nt_job) and the fused-draw factors (Layout.fin) -- nothing left for the backward at an
+// upstream of 1.
+bool final_complete(const mi_elbo* e, const Layout& L) {
+  const int finished = L.red.tails + (L.red.nt_job >= 0 ? 1 : 0) + L.fin.num;
+  return e->num_factors > 0 && finished == e->num_factors && !L.red.external && L.fwd.num == 0;
 }
 
 size_t workspace_need(const mi_elbo* e) {
@@ -1469,8 +1532,7 @@ int mi_elbo_struct_sizes(size_t* factor, size_t* elbo) {
 int mi_elbo_final_grads(const mi_elbo* elbo, int* complete) {
   if (!valid(elbo) || complete == nullptr) return MI_EINVAL;
   const Layout L = make_layout(elbo);
-  const int finished = L.red.tails + (L.red.nt_job >= 0 ? 1 : 0);
-  *complete = (elbo->num_factors > 0 && finished == elbo->num_factors && !L.red.external) ? 1 : 0;
+  *complete = final_complete(elbo, L) ? 1 : 0;
   return 0;
 }
 
@@ -1504,7 +1566,13 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
     }
   bool has_beta = false;
   for (int f = 0; f < elbo->num_factors; ++f) has_beta |= elbo->factors[f].family != MI_NORMAL;
-  const dim3 grid((unsigned)(L.red.first[L.red.num] + L.fwd.lead_blocks + L.fwd.first[L.fwd.num]));
+  // the fused-draw factors' final gradients (blocks after the share-writing ones; only launches
+  // without forward-absorbed Beta blocks, which use that range)
+  const bool fin = (elbo->options & MI_ELBO_FINAL_GRADS) && L.fin.num > 0 && L.fwd.num == 0 &&
+                   final_complete(elbo, L);
+  const int extra = L.fwd.num > 0 ? L.fwd.first[L.fwd.num] : fin ? L.fin.first[L.fin.num] : 0;
+  const dim3 grid((unsigned)(L.red.first[L.red.num] + L.fwd.lead_blocks + extra));
+  const mi::AbsorbPlan& plan = fin ? L.fin : L.fwd;
   hipStream_t s = static_cast<hipStream_t>(stream);
 #if MI_ELBO_TIMING
   {
@@ -1520,10 +1588,10 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
     hipLaunchKernelGGL((mi::k_elbo_forward<true, true>), grid, block, 0, s, *elbo, L.fwd, L.red,
                        work, counters, loss);
   else if (has_beta)
-    hipLaunchKernelGGL((mi::k_elbo_forward<true, false>), grid, block, 0, s, *elbo, L.fwd, L.red,
+    hipLaunchKernelGGL((mi::k_elbo_forward<true, false>), grid, block, 0, s, *elbo, plan, L.red,
                        work, counters, loss);
   else
-    hipLaunchKernelGGL((mi::k_elbo_forward<false, false>), grid, block, 0, s, *elbo, L.fwd,
+    hipLaunchKernelGGL((mi::k_elbo_forward<false, false>), grid, block, 0, s, *elbo, plan,
                        L.red, work, counters, loss);
   return to_code(hipGetLastError());
 }

@@ -577,6 +577,7 @@ class _LinearLauncher:
         self.prior: Optional[Tuple[SiteRecord, int, Tuple[float, float]]] = None
         # theta is a guide draw this launch makes itself (mi_linear.draw, guide.PendingDraw)
         self.draw: Optional[guide.PendingDraw] = None
+        self.drew_theta = self.drew_rows = False   # what the last launch made itself
         # decided here, outside the autograd Function (whose forward runs with grad disabled)
         grad_on = torch.is_grad_enabled()
         self.theta_grad = grad_on and theta.requires_grad
@@ -690,6 +691,7 @@ class _LinearLauncher:
             code = launch(L)
         elif L.draw.operand and code == 0:
             guide.take_draw(self.draw)
+            self.drew_theta = True
         if L.rows.counter:
             if code == nat.MI_EUNSUPPORTED:   # this launch shape does not draw rows: draw first
                 zeroed, prior_flags = L.options & nat.GROUP_FLAGS_ZEROED, L.prior.flags
@@ -699,6 +701,7 @@ class _LinearLauncher:
                 code = launch(L)
             elif code == 0:
                 self.batch.rows_taken()
+                self.drew_rows = True
         nat.check(code, "mi_linear_forward_deferred")
         self.reduce = reduce if defer and reduce.part else None
         self.workspace = workspace   # holds the deferred partials
@@ -902,6 +905,9 @@ class LogJoint:
             for site in sites:
                 bits = int(values[cursor])
                 cursor += 1
+                if bits & nat.FLAG_INTERNAL:
+                    raise RuntimeError(f"site '{site.name}': an in-kernel completion wait of its "
+                                       "launch timed out (results of this step are invalid)")
                 if bits & nat.FLAG_PARAM:
                     found.append((site.order, len(found), (
                         f"Expected parameters of distribution {site.description} for site "
@@ -1361,6 +1367,8 @@ class _ElboPlan:
         self.cat_holders = [dict() for _ in categorical]
         self.flags: Optional[torch.Tensor] = None
         self.state = None
+        self.fused_linear = False   # the linear launch ran the ELBO forward (mi_linear_elbo_forward)
+        self.deferred_count = 0
         self.absorbed = absorbed or {}
         # operands / linear inputs whose gradient an absorbed factor consumes
         self.skip_ops: Dict[int, set] = collections.defaultdict(set)
@@ -1393,7 +1401,8 @@ class _ElboPlan:
                 out.extend(p[0] if p is not None else None for p in plan.params)
         return out
 
-    def _describe(self, terms: List[torch.Tensor], buffers: List[torch.Tensor]) -> nat.Elbo:
+    def _describe(self, terms: List[torch.Tensor], buffers: List[torch.Tensor],
+                  fill: bool = True) -> nat.Elbo:
         E = nat.Elbo()
         E.K = self.K
         E.g0 = self.g0
@@ -1407,8 +1416,10 @@ class _ElboPlan:
             d.family, d.n = f.family, f.n
             d.weight = f.weight
             # the entropy kernels read the parameters directly: a deferred exp transform no draw
-            # kernel has written yet runs first (a no-op once a draw kernel wrote it)
-            guide.fill_exp(f.tensor)
+            # kernel has written yet runs first (a no-op once a draw kernel wrote it; `fill`
+            # False: the launch being described writes it)
+            if fill:
+                guide.fill_exp(f.tensor)
             base = f.tensor.data_ptr()
             if f.family in (nat.BETA, nat.GAMMA):
                 d.param[0], d.param[1] = base, base + 4
@@ -1492,6 +1503,10 @@ class _ElboPlan:
             self.flags = zeroed[:words]
         else:
             self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
+        if self._linear_elbo_candidate():
+            loss = self._forward_linear_elbo()
+            if loss is not None:
+                return loss
         cursor = len(self.categorical) + sum(len(l.flag_sites) for l in self.linears)
         # absorbed Beta draws whose implicit-gradient factors a site launch can carry (mi_side)
         side_jobs = [plan for plan in self.absorbed.values()
@@ -1576,6 +1591,7 @@ class _ElboPlan:
         fused = self._reduce_ok() and len(deferred) <= nat.MAX_REDUCE and \
             os.environ.get("MININF_AMD_FUSE_REDUCE", "1") != "0"
         lib = nat.lib()
+        self.deferred_count = len(deferred) if fused else 0
         if fused:
             reduced = {id(t) for _, t in deferred}
             terms = [t for t in terms if id(t) not in reduced]
@@ -1623,6 +1639,112 @@ class _ElboPlan:
                                       nat.stream_handle(self.device)), "mi_elbo_forward")
         self.state = (E, results, cat_results, lin_results, extra, terms)
         return loss
+
+    def _linear_elbo_candidate(self) -> bool:
+        """
+        The step is one linear site over the guide's one Normal factor that its launch draws
+        (examples/minibatch.md:76-88): the launch may run the whole ELBO forward
+        (mi_linear_elbo_forward; the library decides, MININF_AMD_LINEAR_ELBO=0 disables it).
+        """
+        if len(self.linears) != 1 or self.launchers or self.categorical or self.fallback or \
+                self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
+            return False
+        linear = self.linears[0]
+        return (linear.draw is not None and not linear.draw.done and linear.needs_grads() and
+                ("lin_theta", 0) in self.skip_lin and
+                os.environ.get("MININF_AMD_LINEAR_ELBO", "1") != "0" and
+                os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
+
+    def _forward_linear_elbo(self) -> Optional[torch.Tensor]:
+        """
+        The linear site's launch with the ELBO forward finished by its last blocks: one kernel
+        for the whole forward (and, with the final gradients, the whole backward). None (nothing
+        launched) when the library does not take this step.
+        """
+        device, lib = self.device, nat.lib()
+        linear, holder = self.linears[0], self.lin_holders[0]
+        flags = self.flags[:len(linear.flag_sites)]
+        L = linear.describe(True)
+        L.options |= nat.GROUP_FLAGS_ZEROED
+        if linear.prior is not None:   # its word after the site's
+            L.prior.flags = flags.data_ptr() + 4
+        size = ctypes.c_size_t()
+        nat.check(lib.mi_linear_workspace_bytes(ctypes.byref(L), ctypes.byref(size)),
+                  "mi_linear_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        total = torch.empty(self.K, dtype=torch.float32, device=device)
+        nslots = linear.P + (1 if L.scale else 0)
+        dslots = torch.empty((nslots, self.K), dtype=torch.float32, device=device)
+        buffers = []
+        if nslots > linear.P and ("lin_sigma", 0) not in self.skip_lin:
+            buffers.append(dslots[linear.P:])
+        E = self._describe([], buffers, fill=False)   # (the launch writes the factor's scale)
+        self._describe_absorbed(E, [], [dslots])
+        if self.step_words is not None:
+            E.step_counter = self.step_words[0].data_ptr()
+            E.step_snapshot = self.step_words[1].data_ptr()
+        if self.mirror is not None:
+            E.flags = self.flags.data_ptr()
+            E.flags_mirror = self.mirror.data_ptr()
+            E.nflags = min(self.flags.numel(), self.mirror.numel())
+        final = self._factor_grads(E)
+        E.options |= nat.ELBO_FINAL_GRADS
+        supported, need = ctypes.c_int(0), ctypes.c_size_t()
+        nat.check(lib.mi_linear_elbo_supported(ctypes.byref(L), ctypes.byref(E),
+                                               ctypes.byref(supported), ctypes.byref(need)),
+                  "mi_linear_elbo_supported")
+        if not supported.value:
+            return None
+        elbo_need = ctypes.c_size_t()
+        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(elbo_need)),
+                  "mi_elbo_workspace_bytes")   # (the backward of a non-unit upstream uses it)
+        ws = _elbo_workspace(device, max(need.value, elbo_need.value))
+        loss = torch.empty((), dtype=torch.float32, device=device)
+        start = stop = None
+        if KERNEL_TIMER is not None:
+            start, stop = KERNEL_TIMER.pair(linear)
+        code = lib.mi_linear_elbo_forward(
+            ctypes.byref(L), ctypes.byref(E), workspace.data_ptr(), size.value, total.data_ptr(),
+            dslots.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(), loss.data_ptr(),
+            None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
+            nat.stream_handle(device))
+        if code == nat.MI_EUNSUPPORTED:
+            return None
+        nat.check(code, "mi_linear_elbo_forward")
+        guide.take_draw(linear.draw)
+        linear.drew_theta = True
+        if L.rows.counter:
+            linear.batch.rows_taken()
+            linear.drew_rows = True
+        linear.reduce, linear.workspace = None, workspace
+        holder["flags"] = flags
+        self.final = final
+        self.fused_linear = True
+        self.state = (E, [], [], [dslots], [], [])
+        return loss
+
+    def fusions(self) -> Dict[str, int]:
+        """
+        Which fast paths this evaluation took (structural patterns the planner recognised; a model
+        slightly off a pattern takes the general path, and this says so):
+        folded_priors: prior sites evaluated by the launch of the site that reads their value
+        (mi_prior); linear_theta_draws / linear_rows: linear launches that drew the guide's theta
+        (mi_linear.draw) / their minibatch rows (mi_rows) themselves; fused_draws: Normal guide
+        factors drawn in registers by the site programs (mi_draw); deferred_reductions: site
+        reductions finished by the ELBO forward; final_grads: the forward wrote the guide
+        gradients (no backward launch for loss.backward()); linear_elbo: the linear launch ran the
+        whole ELBO forward (mi_linear_elbo_forward).
+        """
+        return {
+            "folded_priors": sum(l.prior is not None for l in self.launchers) +
+            sum(l.prior is not None for l in self.linears),
+            "linear_theta_draws": sum(l.drew_theta for l in self.linears),
+            "linear_rows": sum(l.drew_rows for l in self.linears),
+            "fused_draws": sum(p.kind == nat.DRAW_PARTIALS for p in self.absorbed.values()),
+            "deferred_reductions": self.deferred_count,
+            "final_grads": int(getattr(self, "final", None) is not None),
+            "linear_elbo": int(self.fused_linear),
+        }
 
     def _reduce_ok(self) -> bool:
         """
@@ -1812,6 +1934,10 @@ def entropy_factors(approximation) -> Tuple[List[EntropyFactor], list]:
     return fused, rest
 
 
+# _ElboPlan.fusions() of the last ELBO evaluation (EvidenceLowerBoundLoss.last_fusions)
+LAST_FUSIONS: Dict[str, int] = {}
+
+
 def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[EntropyFactor],
          entropy_scale: float, samples: Optional[Dict[str, torch.Tensor]] = None,
          flags: Optional[torch.Tensor] = None,
@@ -1845,6 +1971,8 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
                      entropy_scale, linears, absorbed, flags, step_words, mirror)
     loss = _ElboFn.apply(plan, *plan.inputs())
+    global LAST_FUSIONS
+    LAST_FUSIONS = plan.fusions()
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []
     for (site, _, _, _), holder in zip(categorical, plan.cat_holders):
         pending.append(("categorical", holder, [site]))

@@ -368,6 +368,8 @@ class EvidenceLowerBoundLoss(nn.Module):
         if data_shard is not None and process_group is None and data_shard.world is None:
             raise ValueError("data_shard needs the process_group it shards over (or its world)")
         self._counter: Optional[torch.Tensor] = None   # device step counter of the guide RNG
+        # the fast paths the last evaluation took (engine._ElboPlan.fusions)
+        self.last_fusions: Dict[str, int] = {}
         self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
         self._mirror: Optional[torch.Tensor] = None   # their pinned host copy
 
@@ -487,6 +489,7 @@ class EvidenceLowerBoundLoss(nn.Module):
             try:
                 loss, joint = engine.elbo(trace, g0, device, factors, entropy_scale, samples,
                                           flags=flags, step_words=step_words, mirror=mirror)
+                self.last_fusions = dict(engine.LAST_FUSIONS)
                 joint.sticky = sticky and joint.flags is not None and not joint.checks and \
                     joint.flags.data_ptr() == flags.data_ptr()
             finally:

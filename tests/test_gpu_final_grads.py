@@ -130,6 +130,9 @@ def _regression_steps(device, monkeypatch, final, K, minibatch, steps=3):
     """C3 / C4-shaped regression (examples/minibatch.md): the theta factor's gradients finished by
     the ELBO forward from the linear site's slot rows (the Normal tail)."""
     monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1" if final else "0")
+    # the ELBO forward's own Normal tail (the linear launch finishing the whole ELBO is
+    # test_gpu_linear_elbo.py's subject)
+    monkeypatch.setenv("MININF_AMD_LINEAR_ELBO", "0")
     gen = torch.Generator().manual_seed(5)
     n, p = 8192, 32
     X = torch.randn(n, p, generator=gen)
@@ -171,3 +174,52 @@ def test_regression_final_grads_match_the_backward_launch(device, monkeypatch, K
         assert lf == lp
         for a, b in zip(gf, gp):
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+
+
+def _masked_steps(device, monkeypatch, final, n=20000, K=64, steps=3, shard=None):
+    """The masked hierarchical model (examples/missing-observations.md restated, C5): z drawn in
+    registers by the site program (MI_DRAW_PARTIALS), mu a one-element Normal factor whose sources
+    are the program's slot and the prior site's slot."""
+    monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1" if final else "0")
+    import numpy as np
+    rng = np.random.default_rng(0)
+    mask = torch.as_tensor(rng.random(n) > 0.2, device=device)
+    y = torch.as_tensor(rng.normal(size=n).astype(np.float32), device=device)
+    b = torch.as_tensor((rng.random(n) < 0.5).astype(np.float32), device=device)
+
+    def model():
+        mu = mininf_amd.sample("mu", Normal(0.0, 1.0))
+        z = mininf_amd.sample("z", Normal(mu, 1.0), sample_shape=[n])
+        mininf_amd.sample("y", Normal(z, 0.5))
+        mininf_amd.sample("b", Bernoulli(logits=z))
+
+    guide = mininf_amd.nn.ParameterizedFactorizedDistribution(
+        mu=ParameterizedDistribution(Normal, loc=0.3, scale=0.8),
+        z=ParameterizedDistribution(Normal, loc=torch.linspace(-1, 1, n),
+                                    scale=torch.linspace(0.5, 1.5, n))).to(device)
+    loss_fn = EvidenceLowerBoundLoss(num_particles=K, seed=4)
+    cond = mininf_amd.condition(model, y=torch.masked.as_masked_tensor(y, mask),
+                                b=torch.masked.as_masked_tensor(b, mask))
+    out = []
+    for _ in range(steps):
+        loss = loss_fn(cond, guide())
+        loss.backward()
+        out.append((float(loss), [q.grad.clone() for q in guide.parameters()]))
+        for q in guide.parameters():
+            q.grad = None
+    torch.cuda.synchronize()
+    return out, loss_fn.last_fusions
+
+
+def test_masked_model_final_grads_match_the_backward_launch(device, monkeypatch):
+    """The forward finishes the fused-draw factor (its backward blocks run inside the forward
+    launch) and the one-element mu (the Normal tail over every job's slot): no backward launch."""
+    calls = _spy_backward(monkeypatch)
+    fused, fusions = _masked_steps(device, monkeypatch, True)
+    assert calls == [] and fusions["final_grads"] == 1 and fusions["fused_draws"] == 1
+    plain, _ = _masked_steps(device, monkeypatch, False)
+    assert len(calls) == 3
+    for (lf, gf), (lp, gp) in zip(fused, plain):
+        assert lf == lp
+        for a, b in zip(gf, gp):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6 * float(b.abs().max()))
