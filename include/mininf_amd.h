@@ -565,6 +565,24 @@ int mi_linear_elbo_forward(const mi_linear* site, const struct mi_elbo* elbo, vo
                            void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
                            void* start_event, void* stop_event, void* stream);
 
+/* The whole ELBO forward in a site group's launch (ABI 13), for the README model's step
+ * (README.md:40-69): one Bernoulli BCAST site over shared data (the k_site_bcast_smem kernel, slot
+ * in the rank-one layout, with the guide's Beta implicit-gradient factors as its side job, mi_side)
+ * and one one-element Beta guide factor whose only source is that slot. The launch's last blocks
+ * reduce its partials and run mi_elbo_forward's tail: `total` and `slot_grad` as the deferred
+ * reduction writes them, *loss, the factor's saved sums and its gradients for an upstream of 1
+ * (MI_ELBO_FINAL_GRADS), the generator step and the flag mirror. elbo: the step's descriptor with
+ * num_terms 0 and num_reduce 0, factor 0 that Beta factor (source slot_grad, dgrad = side.out).
+ * mi_group_elbo_supported reports whether the pair qualifies and the elbo workspace it needs;
+ * otherwise mi_group_elbo_forward returns MI_EUNSUPPORTED without launching. Replaces
+ * nn.py:224-228 for that step together with the site (core.py:241-273). */
+int mi_group_elbo_supported(const mi_group* group, const struct mi_elbo* elbo, int* supported,
+                            size_t* elbo_workspace_bytes);
+int mi_group_elbo_forward(const mi_group* group, const struct mi_elbo* elbo, void* workspace,
+                          size_t workspace_bytes, float* total, float* slot_grad, uint32_t* flags,
+                          void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
+                          void* start_event, void* stop_event, void* stream);
+
 /* ---- device-resident minibatches (replaces examples/minibatch.md:78-88, the host DataLoader) ---- */
 
 /* Row indices of the next minibatch of an n-row dataset: with c = counter[0] (then counter[0] =

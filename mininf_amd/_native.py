@@ -283,6 +283,12 @@ _SIGNATURES = {
     "mi_linear_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo), c_vp,
                                               ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
                                               ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp]),
+    "mi_group_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo),
+                                               ctypes.POINTER(ctypes.c_int),
+                                               ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_group_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo), c_vp,
+                                             ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
+                                             ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp]),
     "mi_elbo_final_grads": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
                                         c_vp]),

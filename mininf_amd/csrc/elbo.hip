@@ -15,6 +15,7 @@
 // finish (device-scope counter, reset by that block) adds the partials in a fixed order.
 #include <cmath>
 #include "beta_grad.hpp"
+#include "entropy.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -23,31 +24,6 @@ namespace mi {
 
 constexpr int kElboThreads = 256;
 constexpr int kElboMaxBlocks = 1024;
-
-// fp32 digamma / trigamma for the Beta entropy, evaluated in the guide's dtype as torch does
-// (torch.digamma / torch.polygamma(1, .) on float tensors). Recurrence up to x >= 6, then the
-// asymptotic series.
-MI_DEV float digammaf(float x) {
-  float shift = 0.0f;
-  while (x < 6.0f) {
-    shift -= 1.0f / x;
-    x += 1.0f;
-  }
-  const float r = 1.0f / (x * x);
-  const float series = r * (1.0f / 12 - r * (1.0f / 120 - r * (1.0f / 252 - r * (1.0f / 240))));
-  return shift + logf(x) - 0.5f / x - series;
-}
-
-MI_DEV float trigammaf(float x) {
-  float acc = 0.0f;
-  while (x < 6.0f) {
-    acc += 1.0f / (x * x);
-    x += 1.0f;
-  }
-  const float r = 1.0f / (x * x);
-  return acc + 1.0f / x + 0.5f * r +
-         r / x * (1.0f / 6 - r * (1.0f / 30 - r * (1.0f / 42 - r * (1.0f / 30))));
-}
 
 // Entropy of element i of a factor (fp32 terms, as torch evaluates them; sums are carried in
 // fp64 by the callers).
@@ -1225,8 +1201,9 @@ int64_t longest_factor(const mi_elbo* e) {
 // from kCounterFirst on; the forward's group counters (kGroupCounters words, 64 bytes apart) in
 // between.
 constexpr int64_t kCounterFirst = mi::kGroupCounterWord + mi::kGroupCounters * mi::kGroupCounterStride;
-// (the last 32 words belong to mi_linear_elbo_forward, linear.hip kLinFinishCounterWord)
-constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 32;
+// (the last 128 words belong to the ELBO-finishing site launches: mi_linear_elbo_forward,
+// linear.hip kLinFinishCounterWord, and mi_group_elbo_forward, sites.hip kBcastFinishCounterWord)
+constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 128;
 
 // Launch plans of both kernels and the layout of the fp64 work area that follows the counters:
 // [loss partials | forward absorbed partials | backward absorbed partials]. All of it is scratch

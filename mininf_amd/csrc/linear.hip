@@ -227,6 +227,8 @@ struct LinFinish {
 
 // Counter words of the mi_elbo workspace the launch uses (kept clear of mi_elbo_forward's).
 constexpr int64_t kLinFinishCounterWord = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 32;
+static_assert(kLinFinishCounterWord >= MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 128 + 96,
+              "clear of sites.hip kBcastFinishCounterWord's words");
 
 template <bool COHERENT>
 MI_DEV void st_part(float* p, float v) {

@@ -1368,6 +1368,7 @@ class _ElboPlan:
         self.flags: Optional[torch.Tensor] = None
         self.state = None
         self.fused_linear = False   # the linear launch ran the ELBO forward (mi_linear_elbo_forward)
+        self.fused_group = False    # the group launch ran it (mi_group_elbo_forward)
         self.deferred_count = 0
         self.absorbed = absorbed or {}
         # operands / linear inputs whose gradient an absorbed factor consumes
@@ -1505,6 +1506,10 @@ class _ElboPlan:
             self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
         if self._linear_elbo_candidate():
             loss = self._forward_linear_elbo()
+            if loss is not None:
+                return loss
+        if self._group_elbo_candidate():
+            loss = self._forward_group_elbo()
             if loss is not None:
                 return loss
         cursor = len(self.categorical) + sum(len(l.flag_sites) for l in self.linears)
@@ -1744,7 +1749,103 @@ class _ElboPlan:
             "deferred_reductions": self.deferred_count,
             "final_grads": int(getattr(self, "final", None) is not None),
             "linear_elbo": int(self.fused_linear),
+            "group_elbo": int(self.fused_group),
         }
+
+    def _group_elbo_candidate(self) -> bool:
+        """
+        The step is one site group over the guide's one one-element Beta factor whose draws only
+        that group reads (the README model, README.md:40-69): its launch may run the whole ELBO
+        forward (mi_group_elbo_forward; the library decides, MININF_AMD_GROUP_ELBO=0 disables it).
+        """
+        if len(self.launchers) != 1 or self.linears or self.categorical or self.fallback or \
+                self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
+            return False
+        plan = self.absorbed[0]
+        return (self.factors[0].family == nat.BETA and plan.kind == nat.DRAW_SOURCES and
+                plan.drawn is not None and plan.drawn.conc is not None and
+                plan.drawn.dgrad is None and self.factors[0].n == 1 and
+                os.environ.get("MININF_AMD_BETA_SIDE", "1") != "0" and
+                os.environ.get("MININF_AMD_GROUP_ELBO", "1") != "0" and
+                os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
+
+    def _forward_group_elbo(self) -> Optional[torch.Tensor]:
+        """
+        The site group's launch with the ELBO forward finished by its last blocks (the Beta
+        draws' implicit-gradient factors as the launch's side job): one kernel after the guide's
+        draw. None (nothing launched) when the library does not take this step.
+        """
+        device, lib = self.device, nat.lib()
+        launcher, holder = self.launchers[0], self.holders[0]
+        plan = self.absorbed[0]
+        K, N = launcher.K, launcher.N
+        if not any(op.mode != nat.GRAD_NONE for op in launcher.operands):
+            return None
+        flags = self.flags[:len(launcher.flag_sites)]
+        launcher.exp_pending = None
+        group, grads = launcher.describe(True, fuse_exp=True)
+        if launcher.exp_pending is not None or any(g is not None for g in grads):
+            return None   # (dense operands or a fused draw: not the BCAST shape)
+        group.options |= nat.GROUP_FLAGS_ZEROED
+        if launcher.prior is not None:   # its word after the group's own
+            group.prior.flags = flags.data_ptr() + 4 * len(launcher.sites)
+        x = plan.drawn.base.reshape(self.K, plan.drawn.N)
+        conc = plan.drawn.conc
+        side_out = torch.empty((x.shape[0], x.shape[1], 2), dtype=torch.float64, device=device)
+        sd = group.side
+        sd.x, sd.c1, sd.c1_stride = x.data_ptr(), conc.data_ptr(), 2
+        sd.c0, sd.c0_stride = conc.data_ptr() + 4, 2
+        sd.K, sd.N, sd.out = x.shape[0], x.shape[1], side_out.data_ptr()
+        size = ctypes.c_size_t()
+        nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
+                  "mi_group_workspace_bytes")
+        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
+        total = torch.empty(K, dtype=torch.float32, device=device)
+        slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
+        plan.side_dgrad = side_out
+        E = self._describe([], [], fill=False)   # (the draw wrote the concentrations)
+        self._describe_absorbed(E, [(grads, slot_grad, workspace)], [])
+        if self.step_words is not None:
+            E.step_counter = self.step_words[0].data_ptr()
+            E.step_snapshot = self.step_words[1].data_ptr()
+        if self.mirror is not None:
+            E.flags = self.flags.data_ptr()
+            E.flags_mirror = self.mirror.data_ptr()
+            E.nflags = min(self.flags.numel(), self.mirror.numel())
+        final = self._factor_grads(E)
+        E.options |= nat.ELBO_FINAL_GRADS
+        supported, need = ctypes.c_int(0), ctypes.c_size_t()
+        nat.check(lib.mi_group_elbo_supported(ctypes.byref(group), ctypes.byref(E),
+                                              ctypes.byref(supported), ctypes.byref(need)),
+                  "mi_group_elbo_supported")
+        if not supported.value:
+            plan.side_dgrad = None
+            return None
+        elbo_need = ctypes.c_size_t()
+        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(elbo_need)),
+                  "mi_elbo_workspace_bytes")   # (the backward of a non-unit upstream uses it)
+        ws = _elbo_workspace(device, max(need.value, elbo_need.value))
+        loss = torch.empty((), dtype=torch.float32, device=device)
+        start = stop = None
+        if KERNEL_TIMER is not None:
+            start, stop = KERNEL_TIMER.pair(launcher)
+        guide.join_side()
+        code = lib.mi_group_elbo_forward(
+            ctypes.byref(group), ctypes.byref(E), workspace.data_ptr(), size.value,
+            total.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(),
+            loss.data_ptr(), None if start is None else start.cuda_event,
+            None if stop is None else stop.cuda_event, nat.stream_handle(device))
+        if code == nat.MI_EUNSUPPORTED:
+            plan.side_dgrad = None
+            return None
+        nat.check(code, "mi_group_elbo_forward")
+        launcher.reduce, launcher.workspace, launcher.side_out = None, workspace, side_out
+        launcher.partials = None
+        holder["flags"], holder["site_lp"] = flags, None
+        self.final = final
+        self.fused_group = True
+        self.state = (E, [(grads, slot_grad, workspace)], [], [], [], [])
+        return loss
 
     def _reduce_ok(self) -> bool:
         """

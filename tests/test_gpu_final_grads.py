@@ -50,6 +50,9 @@ def _spy_backward(monkeypatch):
 
 def _steps(device, monkeypatch, final, steps=3):
     monkeypatch.setenv("MININF_AMD_FINAL_GRADS", "1" if final else "0")
+    # the ELBO forward's own tail (the site launch finishing the whole ELBO is
+    # test_gpu_group_elbo.py's subject)
+    monkeypatch.setenv("MININF_AMD_GROUP_ELBO", "0")
     model, guide, loss_fn = _setup(device)
     out = []
     for _ in range(steps):
