@@ -205,7 +205,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 struct LinFinish {
   unsigned* counters;      // [0] arrivals, [16] helpers done: zero between launches
   double* work;            // [nv][nsc][K] fp64 chunk sums
-  int helpers;             // nv * nsc
+  int helpers;             // blocks that stay to run the jobs: min(jobs, grid)
+  int jobs;                // nv * nsc
   int nsc;                 // segment chunks per value
   int nv;                  // values of the slab (1 + slots)
   int kp;                  // particle lanes per job: a power of two >= K, <= NT
@@ -285,9 +286,12 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
   if (h < 0) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double* lds = reinterpret_cast<double*>(scratch);   // [NT] doubles during the jobs
-  {
-    // job h: value v, segments [s0, s1) of every particle
-    const int v = h / F.nsc, c = h - v * F.nsc;
+  // jobs h, h + helpers, ... (more jobs than blocks in a small launch); the block that completes
+  // the last job runs the tail (it has no job left: every job was counted before it)
+  bool final_block = false;
+  for (int job = h; job < F.jobs; job += F.helpers) {
+    // job: value v, segments [s0, s1) of every particle
+    const int v = job / F.nsc, c = job - v * F.nsc;
     const int64_t s0 = (int64_t)c * F.segc;
     const int64_t s1 = min(ntile, s0 + F.segc);
     const int kp = F.kp, G = NT / kp;
@@ -312,15 +316,16 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
       __hip_atomic_store(&F.work[((int64_t)v * F.nsc + c) * K + kl], t, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned t = atomicAdd(F.counters + 16, 1u);
+      role = t == (unsigned)F.jobs - 1u ? 1 : -1;
+    }
+    __syncthreads();
+    final_block = role > 0;
   }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned t = atomicAdd(F.counters + 16, 1u);
-    role = t == (unsigned)F.helpers - 1u ? 1 : -1;
-  }
-  __syncthreads();
-  if (role < 0) return;
+  if (!final_block) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 
   // ---- the last helper: chunk sums in a fixed order, then the tail --------------------------
@@ -1151,7 +1156,7 @@ int finish_plan(const mi_linear* site, const mi_elbo* E, const Geometry& g, mi::
   // segment chunks: 16 loads per helper thread (one round of memory latency)
   const int64_t per_chunk = (int64_t)16 * (NT / kp);
   const int64_t nsc = ceil_div(g.ntile, per_chunk);
-  if (nsc > mi::kFinChunks || nv * nsc > grid) return MI_EUNSUPPORTED;
+  if (nsc > mi::kFinChunks) return MI_EUNSUPPORTED;
   // the tail's feature quads split evenly over the block's threads
   const int64_t nq = P / 4;
   if (P % 4 != 0 || (nq & (nq - 1)) != 0 || NT % nq != 0) return MI_EUNSUPPORTED;
@@ -1159,7 +1164,8 @@ int finish_plan(const mi_linear* site, const mi_elbo* E, const Geometry& g, mi::
   const int64_t xs_bytes = (int64_t)((NT >= 512 ? 256 : 128) / g.pt) * (32 * g.pt + 4) * 4;
   if ((int64_t)NT * 8 * 8 > xs_bytes || npairs * 4 > xs_bytes) return MI_EUNSUPPORTED;
   F = mi::LinFinish{};
-  F.helpers = (int)(nv * nsc);
+  F.jobs = (int)(nv * nsc);
+  F.helpers = (int)std::min<int64_t>(F.jobs, grid);
   F.nsc = (int)nsc;
   F.nv = nv;
   F.kp = kp;

@@ -576,10 +576,10 @@ typedef const __attribute__((address_space(4))) float smem_float;
 struct BcastFinish {
   unsigned* counters;     // [0] arrivals, [16] chunks done, [32 + kc] jobs done of chunk kc
   double* work;           // [nkc][nsc][256] job sums, then [nkc][4] chunk shares
-  int helpers;            // nkc * nsc
+  int helpers;            // blocks that stay to run the jobs: min(jobs, grid)
+  int jobs;               // nkc * nsc
   int nsc;                // segment chunks
   int nkc;                // particle chunks of 256
-  int pad0;
   int64_t segc;           // segments per chunk
   float* loss;
   float* total;           // [K]
@@ -665,72 +665,78 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
   const int h = role;
   if (h < 0) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // ---- 1. job h: particles [kc * 256, +256) over segments [sc * segc, +segc) -------------------
-  const int kc = h / F.nsc, sc = h - kc * F.nsc;
-  const int64_t k = (int64_t)kc * kBcastThreads + tid;
-  const int64_t kk = k < K ? k : K - 1;
-  {
-    const int64_t s0 = (int64_t)sc * F.segc, s1 = min(nseg, s0 + F.segc);
-    double acc = 0.0;
-    int64_t s = s0;
-    for (; s + 16 <= s1; s += 16) {
-      float x[16];
+  // jobs h, h + helpers, ... (a small launch has fewer blocks than jobs); a block completes a
+  // particle chunk's jobs -> its chunk stage; the block completing the last chunk -> the tail
+  bool final_block = false;
+  for (int job = h; job < F.jobs && !final_block; job += F.helpers) {
+    // ---- 1. job: particles [kc * 256, +256) over segments [sc * segc, +segc) ----------------
+    const int kc = job / F.nsc, sc = job - kc * F.nsc;
+    const int64_t k = (int64_t)kc * kBcastThreads + tid;
+    const int64_t kk = k < K ? k : K - 1;
+    {
+      const int64_t s0 = (int64_t)sc * F.segc, s1 = min(nseg, s0 + F.segc);
+      double acc = 0.0;
+      int64_t s = s0;
+      for (; s + 16 <= s1; s += 16) {
+        float x[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = ld_coh(part + (s + j) * K + kk);
+        for (int j = 0; j < 16; ++j) x[j] = ld_coh(part + (s + j) * K + kk);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc += (double)x[j];
+        for (int j = 0; j < 16; ++j) acc += (double)x[j];
+      }
+      for (; s < s1; ++s) acc += (double)ld_coh(part + s * K + kk);
+      st_coh<true>(&F.work[((int64_t)kc * F.nsc + sc) * kBcastThreads + tid], acc);
     }
-    for (; s < s1; ++s) acc += (double)ld_coh(part + s * K + kk);
-    st_coh<true>(&F.work[((int64_t)kc * F.nsc + sc) * kBcastThreads + tid], acc);
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned t = atomicAdd(F.counters + 32 + kc, 1u);
-    role = t == (unsigned)F.nsc - 1u ? 1 : -1;
-  }
-  __syncthreads();
-  if (role < 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // ---- 2. the chunk's particles: totals, rank-one slot gradients, loss share, tail sums --------
-  const float* slot = part + nseg * K;   // value 1: u[0 .. nseg), then f[K], e[K]
-  double tot = 0.0;
-  for (int c = 0; c < F.nsc; ++c) tot += ld_coh(&F.work[((int64_t)kc * F.nsc + c) * kBcastThreads + tid]);
-  const float fk = ld_coh(slot + nseg + kk), ek = ld_coh(slot + nseg + K + kk);
-  const double dg0 = ld_coh(F.dgrad + 2 * kk), dg1 = ld_coh(F.dgrad + 2 * kk + 1);
-  double usum = 0.0;   // sum_c u_c in a fixed order: lanes over segments, then the block tree
-  for (int64_t c = tid; c < nseg; c += kBcastThreads) usum += (double)ld_coh(slot + c);
-  red[tid] = usum;
-  __syncthreads();
-  for (int half = kBcastThreads / 2; half > 0; half >>= 1) {
-    if (tid < half) red[tid] += red[tid + half];
-    __syncthreads();
-  }
-  const double U = red[0];
-  double v3[3] = {0.0, 0.0, 0.0};
-  if (k < K) {
-    const float tf = (float)(tot * F.site_scale);
-    const float gv = (float)(((double)fk * U + (double)ek) * (double)G.grad_scale);
-    F.total[k] = tf;
-    F.slot_grad[k] = gv;
-    v3[0] = (double)G.grad_scale * (double)tf;
-    if (gv != 0.0f) {   // a zero upstream never meets the factor (as mi_elbo_forward's tails)
-      v3[1] = (double)gv * dg0;
-      v3[2] = (double)gv * dg1;
-    }
-  }
-  block_sum3(v3, red3);
-  if (tid == 0) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      st_coh<true>(&F.work[(int64_t)F.nkc * F.nsc * kBcastThreads + kc * 4 + q], v3[q]);
     __builtin_amdgcn_s_waitcnt(0);
-    __hip_atomic_store(F.counters + 32 + kc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = atomicAdd(F.counters + 16, 1u);
-    role = t == (unsigned)F.nkc - 1u ? 1 : -1;
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned t = atomicAdd(F.counters + 32 + kc, 1u);
+      role = t == (unsigned)F.nsc - 1u ? 1 : -1;
+    }
+    __syncthreads();
+    if (role < 0) continue;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // ---- 2. the chunk's particles: totals, rank-one slot gradients, loss share, tail sums ------
+    const float* slot = part + nseg * K;   // value 1: u[0 .. nseg), then f[K], e[K]
+    double tot = 0.0;
+    for (int c = 0; c < F.nsc; ++c) tot += ld_coh(&F.work[((int64_t)kc * F.nsc + c) * kBcastThreads + tid]);
+    const float fk = ld_coh(slot + nseg + kk), ek = ld_coh(slot + nseg + K + kk);
+    const double dg0 = ld_coh(F.dgrad + 2 * kk), dg1 = ld_coh(F.dgrad + 2 * kk + 1);
+    double usum = 0.0;   // sum_c u_c in a fixed order: lanes over segments, then the block tree
+    for (int64_t c = tid; c < nseg; c += kBcastThreads) usum += (double)ld_coh(slot + c);
+    red[tid] = usum;
+    __syncthreads();
+    for (int half = kBcastThreads / 2; half > 0; half >>= 1) {
+      if (tid < half) red[tid] += red[tid + half];
+      __syncthreads();
+    }
+    const double U = red[0];
+    double v3[3] = {0.0, 0.0, 0.0};
+    if (k < K) {
+      const float tf = (float)(tot * F.site_scale);
+      const float gv = (float)(((double)fk * U + (double)ek) * (double)G.grad_scale);
+      F.total[k] = tf;
+      F.slot_grad[k] = gv;
+      v3[0] = (double)G.grad_scale * (double)tf;
+      if (gv != 0.0f) {   // a zero upstream never meets the factor (as mi_elbo_forward's tails)
+        v3[1] = (double)gv * dg0;
+        v3[2] = (double)gv * dg1;
+      }
+    }
+    block_sum3(v3, red3);
+    if (tid == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        st_coh<true>(&F.work[(int64_t)F.nkc * F.nsc * kBcastThreads + kc * 4 + q], v3[q]);
+      __builtin_amdgcn_s_waitcnt(0);
+      __hip_atomic_store(F.counters + 32 + kc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned t = atomicAdd(F.counters + 16, 1u);
+      role = t == (unsigned)F.nkc - 1u ? 1 : -1;
+    }
+    __syncthreads();
+    final_block = role > 0;
   }
-  __syncthreads();
-  if (role < 0) return;
+  if (!final_block) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // ---- 3. the loss, the Beta factor's sums and final gradients, the step, the mirror ---------
   const uint32_t fw = (int64_t)tid < F.nflags ? ld_coh(F.flags + tid) : 0u;
@@ -1600,9 +1606,10 @@ int bcast_finish_plan(const mi_group* group, const mi_elbo* E, const Plan& p, mi
   const int64_t nsc = ceil_div(p.nseg, 16);   // 16 loads per helper thread
   const int64_t chunks = p.nseg - 1;
   const int64_t grid = ceil_div(chunks, 8) * 8 * p.grid.y + ((int64_t)p.grid.x - chunks);
-  if (nkc > 64 || nkc * nsc > grid || nkc * nsc > 1024) return MI_EUNSUPPORTED;
+  if (nkc > 64) return MI_EUNSUPPORTED;
   F = mi::BcastFinish{};
-  F.helpers = (int)(nkc * nsc);
+  F.jobs = (int)(nkc * nsc);
+  F.helpers = (int)std::min<int64_t>({(int64_t)F.jobs, grid, (int64_t)1024});
   F.nsc = (int)nsc;
   F.nkc = (int)nkc;
   F.segc = 16;

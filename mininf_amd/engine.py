@@ -1369,6 +1369,7 @@ class _ElboPlan:
         self.state = None
         self.fused_linear = False   # the linear launch ran the ELBO forward (mi_linear_elbo_forward)
         self.fused_group = False    # the group launch ran it (mi_group_elbo_forward)
+        self.tensor_inputs: Optional[List[bool]] = None
         self.deferred_count = 0
         self.absorbed = absorbed or {}
         # operands / linear inputs whose gradient an absorbed factor consumes
@@ -2071,7 +2072,10 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)
     plan = _ElboPlan(trace.K, g0, device, launchers, categorical, fallback, factors,
                      entropy_scale, linears, absorbed, flags, step_words, mirror)
-    loss = _ElboFn.apply(plan, *plan.inputs())
+    inputs = plan.inputs()
+    # which autograd inputs are tensors (nn._Loss.backward maps the gradients to next_functions)
+    plan.tensor_inputs = [isinstance(t, torch.Tensor) for t in inputs]
+    loss = _ElboFn.apply(plan, *inputs)
     global LAST_FUSIONS
     LAST_FUSIONS = plan.fusions()
     pending: List[Tuple[str, dict, List[SiteRecord]]] = []

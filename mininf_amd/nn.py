@@ -317,7 +317,61 @@ class _Loss(torch.Tensor):
                                                            device=self.device)
             if gradient is not None and gradient.dtype != self.dtype:
                 gradient = None
+            if gradient is not None and inputs is None and not retain_graph and \
+                    _accumulate_final_grads(self, gradient):
+                return
         torch.Tensor.backward(self, gradient, retain_graph, create_graph, inputs)
+
+
+def _accumulate_final_grads(loss: torch.Tensor, unit: torch.Tensor) -> bool:
+    """
+    ``loss.backward()`` of a fused ELBO whose forward already wrote the guide gradients for this
+    upstream (engine MI_ELBO_FINAL_GRADS, the README training loop): when every gradient goes
+    straight to a leaf parameter (no hooks, same layout), accumulate them as AccumulateGrad would
+    -- ``p.grad = g``, or ``p.grad += g`` -- without starting the autograd engine (its device
+    thread hand-off is most of an eager backward's host time). False (nothing done): let autograd
+    run. MININF_AMD_DIRECT_GRADS=0 disables it.
+    """
+    fn = loss.grad_fn
+    plan = getattr(fn, "plan", None)
+    tensor_inputs = getattr(plan, "tensor_inputs", None)
+    if plan is None or getattr(plan, "final", None) is None or plan.state is None or \
+            tensor_inputs is None or loss._backward_hooks or \
+            os.environ.get("MININF_AMD_DIRECT_GRADS", "1") == "0":
+        return False
+    # next_functions: one entry per tensor input of _ElboFn.apply (None inputs have none)
+    nexts = fn.next_functions
+    if len(nexts) != sum(tensor_inputs):
+        return False
+    leaves = []
+    cursor = 0
+    for is_tensor in tensor_inputs:
+        if not is_tensor:
+            leaves.append(None)
+            continue
+        node = nexts[cursor][0]
+        cursor += 1
+        if node is None:   # an input that needs no gradient
+            leaves.append(None)
+            continue
+        var = getattr(node, "variable", None)   # AccumulateGrad of a leaf
+        if var is None or var._backward_hooks or \
+                getattr(var, "_post_accumulate_grad_hooks", None) or not var.is_contiguous():
+            return False
+        leaves.append(var)
+    grads = plan.backward(unit)
+    if len(grads) != len(leaves):
+        raise RuntimeError("fused ELBO: gradient count does not match the autograd inputs")
+    for var, grad in zip(leaves, grads):
+        if var is None or grad is None:
+            continue
+        if grad.shape != var.shape:
+            grad = grad.reshape(var.shape)
+        if var.grad is None:
+            var.grad = grad
+        else:
+            var.grad += grad
+    return True
 
     def __repr__(self, *, tensor_contents=None):
         return torch._tensor_str._str(self, tensor_contents=tensor_contents).replace(

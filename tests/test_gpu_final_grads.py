@@ -226,3 +226,40 @@ def test_masked_model_final_grads_match_the_backward_launch(device, monkeypatch)
         assert lf == lp
         for a, b in zip(gf, gp):
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6 * float(b.abs().max()))
+
+
+@pytest.mark.parametrize("set_to_none", [True, False])
+def test_direct_accumulation_matches_autograd(device, monkeypatch, set_to_none):
+    """nn._Loss.backward hands the forward's final gradients to the leaf parameters itself
+    (MININF_AMD_DIRECT_GRADS, no autograd engine): the same gradients as the engine's
+    AccumulateGrad, assigned or accumulated into existing .grad tensors."""
+    def run(direct):
+        monkeypatch.setenv("MININF_AMD_DIRECT_GRADS", "1" if direct else "0")
+        model, guide, loss_fn = _setup(device)
+        params = list(guide.parameters())
+        out = []
+        for _ in range(2):
+            if set_to_none:
+                for p in params:
+                    p.grad = None
+            loss = loss_fn(model, {"theta": guide()})
+            loss.backward()
+            out.append([p.grad.clone() for p in params])
+        return out
+
+    direct, engine = run(True), run(False)
+    for gd, ge in zip(direct, engine):
+        for a, b in zip(gd, ge):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_direct_accumulation_keeps_tensor_hooks(device, monkeypatch):
+    """A hook on a parameter sends the backward through the autograd engine (the hook runs)."""
+    monkeypatch.setenv("MININF_AMD_DIRECT_GRADS", "1")
+    model, guide, loss_fn = _setup(device)
+    seen = []
+    p0 = next(iter(guide.parameters()))
+    p0.register_hook(lambda g: seen.append(1))
+    loss = loss_fn(model, {"theta": guide()})
+    loss.backward()
+    assert seen == [1]
