@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 13
+#define MI_ABI_VERSION 14
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -563,7 +563,8 @@ int mi_linear_elbo_supported(const mi_linear* site, const struct mi_elbo* elbo, 
 int mi_linear_elbo_forward(const mi_linear* site, const struct mi_elbo* elbo, void* workspace,
                            size_t workspace_bytes, float* total, float* dslots, uint32_t* flags,
                            void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                           void* start_event, void* stop_event, void* stream);
+                           const struct mi_adam* adam, void* start_event, void* stop_event,
+                           void* stream);
 
 /* The whole ELBO forward in a site group's launch (ABI 13), for the README model's step
  * (README.md:40-69): one Bernoulli BCAST site over shared data (the k_site_bcast_smem kernel, slot
@@ -581,7 +582,16 @@ int mi_group_elbo_supported(const mi_group* group, const struct mi_elbo* elbo, i
 int mi_group_elbo_forward(const mi_group* group, const struct mi_elbo* elbo, void* workspace,
                           size_t workspace_bytes, float* total, float* slot_grad, uint32_t* flags,
                           void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                          void* start_event, void* stop_event, void* stream);
+                          const struct mi_adam* adam, void* start_event, void* stop_event,
+                          void* stream);
+
+/* The optimizer step in a finishing launch (ABI 14): `adam` (NULL: none) is an mi_adam_step
+ * descriptor whose gradients are the final gradients the launch writes; the launch's last block
+ * runs the step after writing them, with mi_adam_step's arithmetic (torch's fused Adam), so a
+ * whole training step -- draws, sites, ELBO, gradients, parameter update -- is one kernel.
+ * At most 16384 elements in all (MI_EUNSUPPORTED otherwise, nothing launched); malformed
+ * descriptors are MI_EINVAL. Replaces torch.optim.Adam.step (optimizer.step() in
+ * examples/minibatch.md:86 and README.md:63) for that step. */
 
 /* ---- device-resident minibatches (replaces examples/minibatch.md:78-88, the host DataLoader) ---- */
 

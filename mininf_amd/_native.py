@@ -38,7 +38,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 13   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 14   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -282,13 +282,15 @@ _SIGNATURES = {
                                                 ctypes.POINTER(ctypes.c_size_t)]),
     "mi_linear_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo), c_vp,
                                               ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
-                                              ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp]),
+                                              ctypes.c_size_t, c_vp, ctypes.POINTER(Adam),
+                                              c_vp, c_vp, c_vp]),
     "mi_group_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_int),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_group_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo), c_vp,
                                              ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
-                                             ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp]),
+                                             ctypes.c_size_t, c_vp, ctypes.POINTER(Adam),
+                                             c_vp, c_vp, c_vp]),
     "mi_elbo_final_grads": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
                                         c_vp]),
@@ -333,10 +335,22 @@ def check(code: int, what: str) -> None:
         raise NativeError(f"{what} failed: {kind}")
 
 
+_LAUNCH_HOOK = None
+
+
+def set_launch_hook(hook) -> None:
+    """``hook()`` runs before every native launch (engine: enqueue a held finishing launch)."""
+    global _LAUNCH_HOOK
+    _LAUNCH_HOOK = hook
+
+
 def stream_handle(device: torch.device) -> int:
     """
     hipStream_t of torch's current stream on ``device`` (kernels are ordered with torch's own).
+    Every launch asks for it, so a held launch (engine._PendingStep) is enqueued here first.
     """
+    if _LAUNCH_HOOK is not None:
+        _LAUNCH_HOOK()
     return torch.cuda.current_stream(device).cuda_stream
 
 

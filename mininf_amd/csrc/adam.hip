@@ -10,6 +10,7 @@
 // Every block reads its tensor's step s and uses s + 1; the last block of the tensor to finish
 // (completion count, two levels: groups of kGroup blocks, then the tensor) stores s + 1, so no
 // block can read the advanced value.
+#include "adam_math.hpp"
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -36,15 +37,7 @@ MI_DEV T pick_adam(const T (&arr)[N], int a) {
   return v;
 }
 
-MI_DEV mi_adam_tensor tensor_at(const mi_adam& A, int t) {
-  switch (t) {
-#define MI_ADAM_CASE(Q) case Q: return A.tensors[Q];
-    MI_ADAM_CASE(1) MI_ADAM_CASE(2) MI_ADAM_CASE(3) MI_ADAM_CASE(4) MI_ADAM_CASE(5)
-    MI_ADAM_CASE(6) MI_ADAM_CASE(7)
-#undef MI_ADAM_CASE
-    default: return A.tensors[0];
-  }
-}
+MI_DEV mi_adam_tensor tensor_at(const mi_adam& A, int t) { return adam_tensor_at(A, t); }
 
 // NT: non-temporal 16-byte loads and stores (streamed once per step; MININF_AMD_ADAM_NT)
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -139,18 +132,9 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
     __builtin_amdgcn_s_barrier();
     if (threadIdx.x == 0) started_last = last_block();
   }
-  const float bc1 = (float)(1.0 - pow(A.beta1, (double)s1));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow(A.beta2, (double)s1));
-  const float step_size = (float)(A.lr / (double)bc1);
+  const AdamCoef coef = adam_coef(A, s1);   // (adam_math.hpp: torch's fused Adam arithmetic)
   auto update = [&](float& param, float grad, float& m, float& v) {
-    if (A.maximize) grad = -grad;
-    // the contractions spelled out: fma(beta, moment, (1 - beta) * grad [* grad]), the form
-    // torch's kernel compiles to (the compiler may pick another when left to itself)
-    if (A.weight_decay != 0.0) grad = (float)fma((double)param, A.weight_decay, (double)grad);
-    m = (float)fma(A.beta1, (double)m, (1.0 - A.beta1) * (double)grad);
-    v = (float)fma(A.beta2, (double)v, ((1.0 - A.beta2) * (double)grad) * (double)grad);
-    const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + A.eps);
-    param -= step_size * m / denom;
+    adam_update(A, coef, param, grad, m, v);
   };
   auto step4 = [&](float4& p, const float4& g, float4& m, float4& v) {
     update(p.x, g.x, m.x, v.x);

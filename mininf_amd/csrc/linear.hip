@@ -13,6 +13,7 @@
 // Layout: lanes along particles (kb = min(256, pow2(K)) per block, 256 / kb row groups), rows of X
 // staged through LDS in chunks of 64 and read as wave-wide broadcasts; theta_k and the gradient
 // accumulators live in registers. Per-(tile, particle) partials are reduced in fp64 by k_finalize.
+#include "adam_math.hpp"
 #include "common.hpp"
 #include "internal.hpp"
 #include "rows.hpp"
@@ -224,6 +225,7 @@ struct LinFinish {
   const uint32_t* flags;   // NULL: no mirror
   uint32_t* flags_mirror;
   int64_t nflags;
+  mi_adam adam;            // num 0: no optimizer step in the launch
 };
 
 // Counter words of the mi_elbo workspace the launch uses (kept clear of mi_elbo_forward's).
@@ -455,6 +457,12 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
     }
     __hip_atomic_store(F.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.counters + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (F.adam.num > 0) {
+    // the optimizer step over the gradients just written (every block has read the parameters
+    // for its draw before arriving): the training step ends inside this launch
+    __syncthreads();
+    adam_block<NT>(F.adam);
   }
 }
 
@@ -1366,10 +1374,12 @@ int mi_linear_elbo_supported(const mi_linear* site, const mi_elbo* elbo, int* su
 int mi_linear_elbo_forward(const mi_linear* site, const mi_elbo* elbo, void* workspace,
                            size_t workspace_bytes, float* total, float* dslots, uint32_t* flags,
                            void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                           void* start_event, void* stop_event, void* stream) {
+                           const mi_adam* adam, void* start_event, void* stop_event,
+                           void* stream) {
   if (!valid(site) || elbo == nullptr || total == nullptr || flags == nullptr || dslots == nullptr ||
       loss == nullptr || elbo_workspace == nullptr)
     return MI_EINVAL;
+  if (const int arc = mi::fused_adam_check(adam); arc != 0) return arc;
   size_t need = 0;
   mi_linear_workspace_bytes(site, &need);
   if (workspace == nullptr || workspace_bytes < need) return MI_EWORKSPACE;
@@ -1393,6 +1403,7 @@ int mi_linear_elbo_forward(const mi_linear* site, const mi_elbo* elbo, void* wor
   F.loss = loss;
   F.total = total;
   F.dslots = dslots;
+  if (adam != nullptr) F.adam = *adam;
   if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
     return to_code(e);
   float* part = static_cast<float*>(workspace);

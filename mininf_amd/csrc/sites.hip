@@ -19,6 +19,7 @@
 //            log p is hoisted out of the element loop, leaving one FMA per (particle, element).
 // All three write per-(segment, particle) partial sums (fp32) that k_finalize reduces in fp64 in a
 // fixed order, so results are deterministic run to run.
+#include "adam_math.hpp"
 #include "beta_grad.hpp"
 #include "common.hpp"
 #include "entropy.hpp"
@@ -598,6 +599,7 @@ struct BcastFinish {
   const uint32_t* flags;
   uint32_t* flags_mirror;
   int64_t nflags;
+  mi_adam adam;           // num 0: no optimizer step in the launch
 };
 
 template <bool COHERENT>
@@ -778,6 +780,11 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
   if ((int64_t)tid < F.nflags) F.flags_mirror[tid] = fw;
   for (int64_t i = tid + kBcastThreads; i < F.nflags; i += kBcastThreads)
     F.flags_mirror[i] = ld_coh(F.flags + i);
+  if (F.adam.num > 0) {
+    // the optimizer step over the gradients thread 0 wrote: the training step ends here
+    __syncthreads();
+    adam_block<kBcastThreads>(F.adam);
+  }
 }
 
 // One workgroup of a group's side job (mi_side): the mi_beta_dgrad factors of 256 (draw, component)
@@ -1867,10 +1874,12 @@ int mi_group_elbo_supported(const mi_group* group, const mi_elbo* elbo, int* sup
 int mi_group_elbo_forward(const mi_group* group, const mi_elbo* elbo, void* workspace,
                           size_t workspace_bytes, float* total, float* slot_grad, uint32_t* flags,
                           void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                          void* start_event, void* stop_event, void* stream) {
+                          const mi_adam* adam, void* start_event, void* stop_event,
+                          void* stream) {
   if (!validate_group(group) || elbo == nullptr || total == nullptr || slot_grad == nullptr ||
       flags == nullptr || loss == nullptr || elbo_workspace == nullptr)
     return MI_EINVAL;
+  if (const int arc = mi::fused_adam_check(adam); arc != 0) return arc;
   const Plan p = make_plan(group);
   if (workspace == nullptr || workspace_bytes < ::workspace_bytes(group, p)) return MI_EWORKSPACE;
   mi::BcastFinish F{};
@@ -1892,6 +1901,7 @@ int mi_group_elbo_forward(const mi_group* group, const mi_elbo* elbo, void* work
   F.loss = loss;
   F.total = total;
   F.slot_grad = slot_grad;
+  if (adam != nullptr) F.adam = *adam;
   if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
     return to_code(e);
   float* part = static_cast<float*>(workspace);

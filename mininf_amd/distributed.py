@@ -17,6 +17,8 @@ from typing import Iterable, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import engine
+
 
 @dataclasses.dataclass(frozen=True)
 class DataShard:
@@ -83,6 +85,7 @@ def all_reduce_gradients(parameters: Iterable[torch.nn.Parameter], group=None,
     Returns:
         The summed loss if ``loss`` was given, else ``None``.
     """
+    engine.flush_pending_step()   # (a held finishing launch writes the gradients)
     grads = [p.grad for p in parameters if p.grad is not None]
     parts = [g.reshape(-1) for g in grads]
     if loss is not None:
@@ -141,6 +144,7 @@ class GradientBucket:
 
     def pack(self, loss: Optional[torch.Tensor] = None) -> None:
         """Copy this rank's gradients (and loss share, with ``with_loss``) into the flat buffer."""
+        engine.flush_pending_step()
         grads = []
         for p in self.params:
             if p.grad is None:

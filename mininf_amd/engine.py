@@ -873,6 +873,7 @@ class LogJoint:
         All validation results of the step as one int64 device vector: one MI_FLAG_* word per
         kernel-evaluated site, then one 0/1 per deferred support / constraint check.
         """
+        flush_pending_step()   # (the held finishing launch writes the words)
         if self.flags is not None and not self.checks:
             return self.flags
         parts = []
@@ -1709,14 +1710,21 @@ class _ElboPlan:
         start = stop = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(linear)
-        code = lib.mi_linear_elbo_forward(
-            ctypes.byref(L), ctypes.byref(E), workspace.data_ptr(), size.value, total.data_ptr(),
-            dslots.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(), loss.data_ptr(),
-            None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
-            nat.stream_handle(device))
-        if code == nat.MI_EUNSUPPORTED:
-            return None
-        nat.check(code, "mi_linear_elbo_forward")
+        head = (ctypes.byref(L), ctypes.byref(E), workspace.data_ptr(), size.value,
+                total.data_ptr(), dslots.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(),
+                loss.data_ptr())
+        tail = (None if start is None else start.cuda_event,
+                None if stop is None else stop.cuda_event, nat.stream_handle(device))
+
+        def launch(adam):
+            return lib.mi_linear_elbo_forward(*head, None if adam is None else ctypes.byref(adam),
+                                              *tail)
+        if not _defer_step(launch, "mi_linear_elbo_forward", final,
+                           (self, L, E, workspace, total, dslots, ws, loss, final)):
+            code = launch(None)
+            if code == nat.MI_EUNSUPPORTED:
+                return None
+            nat.check(code, "mi_linear_elbo_forward")
         guide.take_draw(linear.draw)
         linear.drew_theta = True
         if L.rows.counter:
@@ -1831,15 +1839,23 @@ class _ElboPlan:
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(launcher)
         guide.join_side()
-        code = lib.mi_group_elbo_forward(
-            ctypes.byref(group), ctypes.byref(E), workspace.data_ptr(), size.value,
-            total.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(),
-            loss.data_ptr(), None if start is None else start.cuda_event,
-            None if stop is None else stop.cuda_event, nat.stream_handle(device))
-        if code == nat.MI_EUNSUPPORTED:
-            plan.side_dgrad = None
-            return None
-        nat.check(code, "mi_group_elbo_forward")
+        head = (ctypes.byref(group), ctypes.byref(E), workspace.data_ptr(), size.value,
+                total.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(), ws.data_ptr(),
+                ws.numel(), loss.data_ptr())
+        tail = (None if start is None else start.cuda_event,
+                None if stop is None else stop.cuda_event, nat.stream_handle(device))
+
+        def launch(adam):
+            return lib.mi_group_elbo_forward(*head, None if adam is None else ctypes.byref(adam),
+                                             *tail)
+        if not _defer_step(launch, "mi_group_elbo_forward", final,
+                           (self, group, E, workspace, total, slot_grad, side_out, ws, loss,
+                            final)):
+            code = launch(None)
+            if code == nat.MI_EUNSUPPORTED:
+                plan.side_dgrad = None
+                return None
+            nat.check(code, "mi_group_elbo_forward")
         launcher.reduce, launcher.workspace, launcher.side_out = None, workspace, side_out
         launcher.partials = None
         holder["flags"], holder["site_lp"] = flags, None
@@ -1863,7 +1879,7 @@ class _ElboPlan:
                 return False
         return True
 
-    def backward(self, u: torch.Tensor) -> List[Optional[torch.Tensor]]:
+    def backward(self, u: torch.Tensor, hold: bool = False) -> List[Optional[torch.Tensor]]:
         if self.state is None:   # a second backward through the same graph: recompute
             # with this evaluation's generator step (the snapshot) and without advancing it again
             self.recompute = True
@@ -1875,7 +1891,10 @@ class _ElboPlan:
         self.state = None
         final, self.final = getattr(self, "final", None), None
         if final is not None and _is_unit_seed(u):
-            # the forward wrote the gradients of exactly this upstream (MI_ELBO_FINAL_GRADS)
+            # the forward wrote the gradients of exactly this upstream (MI_ELBO_FINAL_GRADS);
+            # autograd reads them next (nn._accumulate_final_grads may hold them instead)
+            if not hold:
+                flush_pending_step()
             return self._outputs(results, cat_results, lin_results, None, final)
         device = self.device
         u = u.to(torch.float32).contiguous()
@@ -1959,6 +1978,130 @@ def _is_unit_seed(u: torch.Tensor) -> bool:
     seed = _UNIT.get(u.device)
     return seed is not None and u.dtype == torch.float32 and u.numel() == 1 and \
         u.data_ptr() == seed.data_ptr()
+
+
+# ---- the step-finishing launch held for the optimizer --------------------------------------------
+# A finishing launch (mi_linear_elbo_forward / mi_group_elbo_forward) writes the loss and the guide
+# gradients of loss.backward() itself; the step's only other kernel is the optimizer's. The launch
+# is therefore held (not enqueued) until its first consumer: when that is the Adam step over its
+# gradients (mininf_amd.optim.Adam), the launch runs the update in its last block (ABI 14) and the
+# whole training step is ONE kernel. Any other consumer enqueues it first, as it would have been:
+# every native launch (_native.stream_handle), every torch operation on the loss (nn._Loss) or on
+# a held gradient (PendingGrad) other than metadata queries, the validation read, graph capture
+# boundaries (graph.StepGraph) and the distributed gradient reductions. MININF_AMD_DEFER_STEP=0
+# launches at once.
+
+_PENDING: Optional["_PendingStep"] = None
+
+# queries that read no tensor data (they run before the launch without flushing it)
+_NO_FLUSH = frozenset({
+    torch.Tensor.dim, torch.Tensor.size, torch.Tensor.numel, torch.Tensor.nelement,
+    torch.Tensor.is_contiguous, torch.Tensor.data_ptr, torch.Tensor.stride,
+    torch.Tensor.storage_offset, torch.Tensor.element_size, torch.Tensor.is_floating_point,
+    torch.Tensor.is_complex, torch.Tensor.get_device, torch.Tensor.ndimension,
+    torch.Tensor.requires_grad_})
+# tensor-valued properties (everything else read through a property is metadata)
+_DATA_PROPERTIES = frozenset({"data", "T", "mT", "H", "mH", "real", "imag", "grad", "_base"})
+
+
+def _flushes(func) -> bool:
+    if func in _NO_FLUSH:
+        return False
+    if getattr(func, "__name__", None) == "__get__":
+        return getattr(getattr(func, "__self__", None), "__name__", None) in _DATA_PROPERTIES
+    return True
+
+
+def torch_function_flush(func, types, args, kwargs):
+    """__torch_function__ of the tensors a held launch writes: flush, then the plain operation."""
+    if _PENDING is not None and _flushes(func):
+        flush_pending_step()
+    return torch._C._disabled_torch_function_impl(func, types, args,
+                                                 {} if kwargs is None else kwargs)
+
+
+class PendingGrad(torch.Tensor):
+    """
+    A guide gradient (``param.grad``) that the held finishing launch writes: an ordinary tensor
+    whose first data use enqueues the launch. Plain ``torch.Tensor`` again once it has run.
+    """
+    __torch_function__ = classmethod(lambda cls, func, types, args=(), kwargs=None:
+                                     torch_function_flush(func, types, args, kwargs))
+
+
+class _PendingStep:
+    def __init__(self, launch, what: str, grads: List[torch.Tensor], keep) -> None:
+        self._launch = launch        # launch(adam descriptor or None) -> error code
+        self.what = what
+        self.grad_ptrs = {g.data_ptr() for g in grads if g is not None}
+        self.held: List[Tuple[torch.Tensor, torch.Tensor]] = []   # (param, PendingGrad)
+        self._keep = keep            # the launch's buffers, alive until it has run
+
+    def hold(self, var: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
+        """``grad`` as the PendingGrad to assign to ``var.grad``."""
+        held = grad.as_subclass(PendingGrad)
+        self.held.append((var, held))
+        return held
+
+    def run(self, adam=None) -> None:
+        code = self._launch(adam)
+        self._keep = None
+        for var, held in self.held:   # the gradients are ordinary tensors from here on
+            if var.grad is held:
+                var.grad = held.as_subclass(torch.Tensor)
+        self.held = []
+        nat.check(code, self.what)
+
+
+def flush_pending_step() -> None:
+    """Enqueue the held finishing launch, if any (without an optimizer step)."""
+    global _PENDING
+    step = _PENDING
+    if step is not None:
+        _PENDING = None
+        step.run(None)
+
+
+def discard_pending_step() -> None:
+    """Drop the held finishing launch unlaunched (a capture that failed part-way)."""
+    global _PENDING
+    _PENDING = None
+
+
+def pending_step() -> Optional[_PendingStep]:
+    return _PENDING
+
+
+def attach_optimizer(adam, grads: Sequence[torch.Tensor]) -> bool:
+    """
+    Run the held finishing launch with the optimizer step ``adam`` (an ``mi_adam`` descriptor over
+    ``grads``) in its last block, when the launch writes at least one of those gradients and the
+    step is small enough (<= 16384 elements, csrc/adam_math.hpp kFusedAdamMaxNumel); the other
+    gradients are complete already (earlier launches on the stream). False: nothing done.
+    """
+    global _PENDING
+    step = _PENDING
+    if step is None or adam.num < 1 or             sum(adam.tensors[j].numel for j in range(adam.num)) > _FUSED_ADAM_MAX_NUMEL or             not any(g.data_ptr() in step.grad_ptrs for g in grads):
+        return False
+    _PENDING = None
+    step.run(adam)
+    return True
+
+
+_FUSED_ADAM_MAX_NUMEL = 16384
+
+
+def _defer_step(launch, what: str, grads, keep) -> bool:
+    """Hold ``launch`` for the optimizer (True), or False: the caller launches now."""
+    global _PENDING
+    if os.environ.get("MININF_AMD_DEFER_STEP", "1") == "0":
+        return False
+    flush_pending_step()
+    _PENDING = _PendingStep(launch, what, [g for gs in grads for g in gs if g is not None], keep)
+    return True
+
+
+nat.set_launch_hook(flush_pending_step)
 
 
 class _ElboFn(torch.autograd.Function):

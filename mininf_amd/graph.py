@@ -166,6 +166,12 @@ class CaptureError(RuntimeError):
     """A training step could not be captured into a hipGraph (see :class:`StepGraph`)."""
 
 
+def _flush_held_launch() -> None:
+    """Enqueue a held step-finishing launch (engine._PendingStep) on the current stream."""
+    from . import engine
+    engine.flush_pending_step()
+
+
 def _abandon_capture(cuda_graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Stream") -> None:
     """
     End a capture that failed part-way: torch's ``capture_end`` (which also hands the graph's
@@ -174,6 +180,8 @@ def _abandon_capture(cuda_graph: "torch.cuda.CUDAGraph", stream: "torch.cuda.Str
     is no longer capturing; finally wait for the work queued before the capture.
     """
     from . import _native as nat
+    from . import engine
+    engine.discard_pending_step()   # a launch held inside the failed capture never runs
     try:
         cuda_graph.capture_end()
     except Exception:   # invalidated: torch raised before ending the capture
@@ -250,6 +258,7 @@ class StepGraph:
                 collector: List = []
                 with graph_safe(collector), _capture_safe_distributions():
                     (warmup_step or step)()
+                _flush_held_launch()
                 count = _check_warmup(collector)
                 # the joints hold the step's loss: drop them, or the warm-up's autograd graph
                 # (its AccumulateGrad nodes on this side stream) stays alive into the capture --
@@ -290,6 +299,7 @@ class StepGraph:
                         # detached: holding the captured step's autograd graph would keep its
                         # AccumulateGrad nodes (and their capture stream) alive past the capture
                         self.output = _detached(step())
+                    _flush_held_launch()   # (a step without an optimizer leaves it held)
                     mirror = self._record_validation(count)
                 self.graph.capture_end()
             except BaseException as error:

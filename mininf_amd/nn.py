@@ -305,9 +305,15 @@ class _Loss(torch.Tensor):
     """
     The loss tensor the fused ELBO returns: an ordinary 0-d tensor (operations on it give plain
     tensors) whose ``backward()`` seeds autograd with a cached device 1.0 instead of
-    ``torch.ones_like(loss)`` -- otherwise a fill launch in every (captured) training step.
+    ``torch.ones_like(loss)`` -- otherwise a fill launch in every (captured) training step. An
+    operation on it first enqueues the step's held finishing launch (engine._PendingStep).
     """
-    __torch_function__ = torch._C._disabled_torch_function_impl
+    __torch_function__ = classmethod(lambda cls, func, types, args=(), kwargs=None:
+                                     engine.torch_function_flush(func, types, args, kwargs))
+
+    def __repr__(self, *, tensor_contents=None):
+        return torch._tensor_str._str(self, tensor_contents=tensor_contents).replace(
+            type(self).__name__ + "(", "tensor(", 1)
 
     def backward(self, gradient=None, retain_graph=None, create_graph=False, inputs=None):
         if gradient is None and self.dim() == 0 and self.is_cuda and not create_graph:
@@ -359,23 +365,25 @@ def _accumulate_final_grads(loss: torch.Tensor, unit: torch.Tensor) -> bool:
                 getattr(var, "_post_accumulate_grad_hooks", None) or not var.is_contiguous():
             return False
         leaves.append(var)
-    grads = plan.backward(unit)
+    grads = plan.backward(unit, hold=True)
     if len(grads) != len(leaves):
         raise RuntimeError("fused ELBO: gradient count does not match the autograd inputs")
+    pending = engine.pending_step()
     for var, grad in zip(leaves, grads):
         if var is None or grad is None:
             continue
         if grad.shape != var.shape:
-            grad = grad.reshape(var.shape)
+            grad = grad.reshape(var.shape)   # (contiguous: a view)
         if var.grad is None:
+            # a gradient the held finishing launch writes stays held (the optimizer step may
+            # join that launch): its first use enqueues it
+            if pending is not None and grad.data_ptr() in pending.grad_ptrs:
+                grad = pending.hold(var, grad)
             var.grad = grad
         else:
+            engine.flush_pending_step()
             var.grad += grad
     return True
-
-    def __repr__(self, *, tensor_contents=None):
-        return torch._tensor_str._str(self, tensor_contents=tensor_contents).replace(
-            type(self).__name__ + "(", "tensor(", 1)
 
 
 class EvidenceLowerBoundLoss(nn.Module):
@@ -555,6 +563,7 @@ class EvidenceLowerBoundLoss(nn.Module):
                 extra = cast(torch.Tensor, sum(
                     f.entropy().sum() / (world if shared is None or names[id(f)] in shared else 1)
                     for f in rest))
+                engine.flush_pending_step()
                 loss = loss - extra
             if loss.is_cuda and loss.dim() == 0 and type(loss) is torch.Tensor:
                 loss.__class__ = _Loss   # the same tensor object and autograd node

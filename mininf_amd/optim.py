@@ -2,7 +2,8 @@
 MI355X optimizer step: :class:`Adam`, a drop-in ``torch.optim.Adam`` whose ``step()`` is one HIP
 launch (``mi_adam_step``, ``csrc/adam.hip``) for up to eight parameters, step-count increment
 included -- torch's capturable fused Adam needs a ``_foreach_add_`` launch for the step counts
-plus the fused update. Same arithmetic as ``torch.optim.Adam(fused=True)`` (bit-identical
+plus the fused update. After a fused ELBO whose finishing launch is held (engine._PendingStep) the
+step joins that launch instead: no launch of its own. Same arithmetic as ``torch.optim.Adam(fused=True)`` (bit-identical
 updates), same ``state`` layout (``step``, ``exp_avg``, ``exp_avg_sq``), so ``state_dict`` moves
 between the two.
 
@@ -17,6 +18,7 @@ from typing import Dict, Iterable, Tuple
 import torch
 
 from . import _native as nat
+from . import engine
 
 
 class Adam(torch.optim.Optimizer):
@@ -168,6 +170,11 @@ class _Plan:
             if not fresh:
                 for j in range(desc.num):
                     desc.tensors[j].grad = active[cursor + j].grad.data_ptr()
+            grads = [p.grad for p in active[cursor:cursor + desc.num]]
             cursor += desc.num
+            # the step's held finishing launch writes these gradients: the update runs in its
+            # last block (one kernel for the whole training step, engine._PendingStep)
+            if engine.attach_optimizer(desc, grads):
+                continue
             nat.check(lib.mi_adam_step(ctypes.byref(desc), counter_words(device).data_ptr(),
                                        nat.stream_handle(device)), "mi_adam_step")

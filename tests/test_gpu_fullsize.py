@@ -217,3 +217,101 @@ def test_c4_full_size_bench_configuration(device, monkeypatch):
     assert separate_draws == [], "theta should be drawn inside the linear launch"
     assert backward_calls == [], "the ELBO forward should write the final gradients"
     assert int(loader.counter[0]) == 2
+
+
+def test_c3_full_size_on_device_draws(device, c3_data):
+    """
+    C3 as the bench runs it (n = 1e6, p = 32, K = 256): theta drawn by the linear launch itself
+    (mi_linear.draw), the prior folded into it, final gradients written by the ELBO forward --
+    nothing injected. Two steps (Adam between them) against the Gram-form oracle with the eps of
+    liboracle (stream 0, steps 0 and 1), at 1e-5.
+    """
+    from mininf_amd.optim import Adam
+    X, y, (G, Xty, yty) = c3_data
+    n, p = X.shape
+    K, seed = 256, 21
+    Xd, yd = torch.as_tensor(X, device=device), torch.as_tensor(y, device=device)
+
+    def model():
+        theta = mi.sample("theta", Normal(0, 1), sample_shape=p)
+        with mi.batch(n):
+            with mi.no_log_prob():
+                Xs = mi.sample("X", Normal(0, 1), sample_shape=(n, p))
+            mi.sample("y", Normal(Xs @ theta, 1))
+
+    gen = torch.Generator().manual_seed(7)
+    guide = mi.nn.ParameterizedDistribution(
+        Normal, loc=1e-3 * torch.randn(p, generator=gen),
+        scale=(1e-3 * torch.randn(p, generator=gen)).exp()).to(device)
+    optimizer = Adam(guide.parameters(), lr=0.01)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed)
+    cond = mi.condition(model, X=Xd, y=yd)
+    lib = oracle_build.load()
+    for step in range(2):
+        optimizer.zero_grad(set_to_none=True)
+        q = guide()
+        loss = loss_fn(cond, {"theta": q})
+        loss.backward()
+        assert loss_fn.last_fusions["linear_theta_draws"] == 1
+        loc = q.loc.detach().cpu().numpy().astype(np.float32)
+        scale = q.scale.detach().cpu().numpy().astype(np.float32)
+        params = guide.distribution_parameters
+        grads = {k: v.grad.detach().cpu().numpy().copy() for k, v in params.items()}
+        value = float(loss)
+        optimizer.step()
+        eps = np.empty((K, p), np.float32)
+        lib.oracle_guide_normals(K, p, seed, step, 0, 0, eps.ctypes.data)
+        ref = oracle.regression_elbo_gram(G, Xty, yty, n, loc, scale, eps)
+        assert abs(value - ref["loss"]) <= 1e-5 * abs(ref["loss"]), (step, value, ref["loss"])
+        _close(grads["loc"], ref["grad_loc"], f"step {step} grad loc")
+        _close(grads["scale"], ref["grad_u_scale"], f"step {step} grad log-scale")
+
+
+def test_c5_data_shards_sum_to_the_full_step(device):
+    """
+    C5's data-sharded layout at full size (n = 1e6, K = 1024; bench.py's N > 1 default): the four
+    element slices of a four-rank run, evaluated one after another in this process, add up to the
+    one-process ELBO -- the loss, mu's gradients (the only all-reduced ones) and each slice's z
+    gradients equal the full run's slice -- to 1e-5 (the slices draw by global element index).
+    """
+    from mininf_amd.distributed import element_shard
+    n, K, W, seed = 1_000_000, 1024, 4, 5
+    gen = torch.Generator().manual_seed(0)
+    y = torch.randn(n, generator=gen)
+    b = (torch.rand(n, generator=gen) < 0.5).float()
+    mask = torch.rand(n, generator=gen) > 0.2
+
+    def run(sl, shard):
+        m = sl.stop - sl.start
+        yd, bd, md = y[sl].to(device), b[sl].to(device), mask[sl].to(device)
+
+        def model():
+            mu = mi.sample("mu", Normal(0.0, 1.0))
+            z = mi.sample("z", Normal(mu, 1.0), sample_shape=[m])
+            mi.sample("y", Normal(z, 0.5))
+            mi.sample("b", Bernoulli(logits=z))
+
+        approx = mi.nn.ParameterizedFactorizedDistribution(
+            mu=mi.nn.ParameterizedDistribution(Normal, loc=0.1, scale=0.9),
+            z=mi.nn.ParameterizedDistribution(Normal, loc=torch.linspace(-1, 1, n)[sl],
+                                              scale=torch.linspace(0.5, 1.5, n)[sl])).to(device)
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed, data_shard=shard)
+        cond = mi.condition(model, y=torch.masked.as_masked_tensor(yd, md),
+                            b=torch.masked.as_masked_tensor(bd, md))
+        loss = loss_fn(cond, approx())
+        loss.backward()
+        mu_p, z_p = approx["mu"].distribution_parameters, approx["z"].distribution_parameters
+        return (float(loss), np.array([float(mu_p["loc"].grad), float(mu_p["scale"].grad)]),
+                z_p["loc"].grad.cpu().numpy(), z_p["scale"].grad.cpu().numpy())
+
+    full = run(slice(0, n), None)
+    total, dmu = 0.0, np.zeros(2)
+    for r in range(W):
+        shard = element_shard(n, shared=("mu",), world=W, rank=r)
+        part = run(slice(shard.start, shard.stop), shard)
+        total += part[0]
+        dmu += part[1]
+        _close(part[2], full[2][shard.start:shard.stop], f"rank {r} z loc grad")
+        _close(part[3], full[3][shard.start:shard.stop], f"rank {r} z log-scale grad")
+    assert abs(total - full[0]) <= 1e-5 * abs(full[0]), (total, full[0])
+    _close(dmu, full[1], "mu grads")

@@ -63,14 +63,20 @@ def _run(device, monkeypatch, fused, n, K, steps=3):
     return out, [q.detach().clone() for q in module.parameters()], loss_fn.last_fusions
 
 
-@pytest.mark.parametrize("n,K", [(50_000, 256), (123_457, 1000), (1_000_000, 4096), (4096, 64)])
-def test_fused_forward_matches_two_launches(device, monkeypatch, n, K):
+@pytest.mark.parametrize("n,K,takes", [(50_000, 256, True), (123_457, 1000, True),
+                                       (1_000_000, 4096, True),
+                                       (4096, 64, False)])   # one chunk: no rank-one slot layout
+def test_fused_forward_matches_two_launches(device, monkeypatch, n, K, takes):
     fwd = _spy(monkeypatch, "mi_elbo_forward")
     bwd = _spy(monkeypatch, "mi_elbo_backward")
     fused_calls = _spy(monkeypatch, "mi_group_elbo_forward")
     fused, params_f, fusions = _run(device, monkeypatch, True, n, K)
-    assert fwd == [] and bwd == [] and len(fused_calls) == 3, "one site kernel per step expected"
-    assert fusions["group_elbo"] == 1 and fusions["folded_priors"] == 1
+    if takes:
+        assert fwd == [] and bwd == [] and len(fused_calls) == 3, "one site kernel per step expected"
+        assert fusions["group_elbo"] == 1 and fusions["folded_priors"] == 1
+    else:
+        assert fused_calls == [] and len(fwd) == 3 and fusions["group_elbo"] == 0
+    fwd.clear()
     plain, params_p, _ = _run(device, monkeypatch, False, n, K)
     assert len(fwd) == 3
     for (lf, gf), (lp, gp) in zip(fused, plain):

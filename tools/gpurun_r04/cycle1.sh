@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out
 run() { local t=$1; shift; local log=$1; shift; timeout -k 10 "$t" "$@" > "gpurun_out/$log" 2>&1; local rc=$?; echo "$log rc=$rc"; return $rc; }
 T="python -u -m pytest -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider"
-run 400 c1_linelbo.log $T tests/test_gpu_linear_elbo.py tests/test_gpu_group_elbo.py -x || exit 1
+run 400 c1_linelbo.log $T tests/test_gpu_linear_elbo.py tests/test_gpu_group_elbo.py
 run 500 c1_new.log $T tests/test_gpu_final_grads.py tests/test_gpu_fusions.py tests/test_gpu_samplers.py tests/test_gpu_fullsize.py tests/test_gpu_minibatch.py tests/test_gpu_graph.py
 run 900 c1_tests.log python -u -m pytest tests -m gpu -q --maxfail=8 --timeout 240 --timeout-method thread -p no:cacheprovider || exit 1
 run 400 c1_bench.log python -u bench.py || exit 1
