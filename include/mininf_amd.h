@@ -780,6 +780,41 @@ int mi_elbo_workspace_init(void* workspace, size_t workspace_bytes, void* stream
 int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes, float* loss,
                     void* stream);
 
+/* The optimizer step of the factors an ELBO forward finishes (ABI 14). With MI_ELBO_FINAL_GRADS
+ * the forward's last block writes the gradients of one-element Beta tails and of the Normal tail
+ * (nt) for an upstream of 1; mi_elbo_forward_adam also runs Adam there, on the unconstrained tensor
+ * behind factor `factor`'s parameter `param` (mi_factor.grad[param] is its gradient), with
+ * mi_adam_step's arithmetic (torch's fused Adam): the update, the moments and the step count, by
+ * the thread that writes the gradient -- no optimizer launch for the step. `adam` is a DEVICE
+ * pointer (the descriptor is read by the kernel; it may be reused across launches); NULL: as
+ * mi_elbo_forward. mi_elbo_adam_supported checks a HOST copy against the launch: every slot's
+ * factor finished by the last block (not a fused-draw factor), numel = the factor's n, the
+ * gradient written, no (factor, param) twice. Replaces optimizer.step() (README.md:66-69) for
+ * those parameters. */
+#define MI_ELBO_ADAM_SLOTS 4
+typedef struct mi_elbo_adam_slot {
+  int32_t factor;
+  int32_t param;
+  float* value;           /* the optimised tensor (contiguous, numel = the factor's n) */
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;            /* one float */
+  int64_t numel;
+} mi_elbo_adam_slot;
+typedef struct mi_elbo_adam {
+  int32_t num;
+  int32_t maximize;
+  double lr;
+  double beta1;
+  double beta2;
+  double eps;
+  double weight_decay;
+  mi_elbo_adam_slot slots[MI_ELBO_ADAM_SLOTS];
+} mi_elbo_adam;
+int mi_elbo_adam_supported(const mi_elbo* elbo, const mi_elbo_adam* adam, int* supported);
+int mi_elbo_forward_adam(const mi_elbo* elbo, void* workspace, size_t workspace_bytes,
+                         float* loss, const mi_elbo_adam* adam, void* stream);
+
 /* With u = *upstream (device scalar, d out / d loss): dterm[0] = u * g0 (the gradient of every
  * term element); factors[f].grad[j] = the gradient of -u * entropy_scale * H_f (plus u times the
  * absorbed draw's backward, and the transform's chain rule; see mi_factor); every buffer is

@@ -181,6 +181,20 @@ class Adam(ctypes.Structure):
                 ("weight_decay", ctypes.c_double), ("tensors", AdamTensor * ADAM_MAX_TENSORS)]
 
 
+ELBO_ADAM_SLOTS = 4   # MI_ELBO_ADAM_SLOTS
+
+
+class ElboAdamSlot(ctypes.Structure):
+    _fields_ = [("factor", ctypes.c_int32), ("param", ctypes.c_int32), ("value", c_vp),
+                ("exp_avg", c_vp), ("exp_avg_sq", c_vp), ("step", c_vp), ("numel", c_i64)]
+
+
+class ElboAdam(ctypes.Structure):
+    _fields_ = [("num", ctypes.c_int32), ("maximize", ctypes.c_int32), ("lr", ctypes.c_double),
+                ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+                ("weight_decay", ctypes.c_double), ("slots", ElboAdamSlot * ELBO_ADAM_SLOTS)]
+
+
 # name -> (restype, argtypes). Mirrors include/mininf_amd.h one to one.
 _SIGNATURES = {
     "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
@@ -277,6 +291,10 @@ _SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),
     "mi_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp, c_vp]),
+    "mi_elbo_adam_supported": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ElboAdam),
+                                              ctypes.POINTER(ctypes.c_int)]),
+    "mi_elbo_forward_adam": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp,
+                                            c_vp, c_vp]),
     "mi_linear_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo),
                                                 ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_size_t)]),

@@ -13,7 +13,9 @@ struct AdamCoef {
   float bc1, bc2_sqrt, step_size;
 };
 
-MI_DEV AdamCoef adam_coef(const mi_adam& A, float s1) {
+// H: a descriptor with Adam's hyper-parameters (mi_adam, mi_elbo_adam)
+template <typename H>
+MI_DEV AdamCoef adam_coef(const H& A, float s1) {
   AdamCoef c;
   c.bc1 = (float)(1.0 - pow(A.beta1, (double)s1));
   c.bc2_sqrt = (float)sqrt(1.0 - pow(A.beta2, (double)s1));
@@ -21,7 +23,8 @@ MI_DEV AdamCoef adam_coef(const mi_adam& A, float s1) {
   return c;
 }
 
-MI_DEV void adam_update(const mi_adam& A, const AdamCoef& c, float& param, float grad, float& m,
+template <typename H>
+MI_DEV void adam_update(const H& A, const AdamCoef& c, float& param, float grad, float& m,
                         float& v) {
   if (A.maximize) grad = -grad;
   // the contractions spelled out: fma(beta, moment, (1 - beta) * grad [* grad]), the form

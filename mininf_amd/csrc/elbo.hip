@@ -15,6 +15,7 @@
 // finish (device-scope counter, reset by that block) adds the partials in a fixed order.
 #include <cmath>
 #include "beta_grad.hpp"
+#include "adam_math.hpp"
 #include "entropy.hpp"
 
 #include <algorithm>
@@ -771,7 +772,8 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                                                const ReducePlan R,
                                                                double* __restrict__ work,
                                                                unsigned* __restrict__ counters,
-                                                               float* __restrict__ loss) {
+                                                               float* __restrict__ loss,
+                                                               const mi_elbo_adam* __restrict__ adam) {
   __shared__ double red[kElboThreads][2];
   __shared__ bool last;
 #if MI_ELBO_TIMING
@@ -940,6 +942,16 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   // the tails' partials and concentrations, the validation words, the generator step) is issued
   // before the first sum: one memory round trip instead of one per stage.
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // mi_elbo_forward_adam: the optimizer's descriptor into LDS with this phase's first loads
+  __shared__ mi_elbo_adam sad;
+  const bool has_adam = !ABSORB && adam != nullptr;
+  if (has_adam) {
+    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
+    static_assert(kWords <= kElboThreads, "one descriptor word per thread");
+    if ((int)threadIdx.x < kWords)
+      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
+          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
+  }
   double t = 0.0;
   double acc[kMaxTails][2] = {};
   for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
@@ -983,6 +995,36 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
   const double total = block_sum(t, rsum + kElboThreads / kWave);
   MI_ELBO_STAMP(4);
+  // the optimised tensors' elements this thread updates (element threadIdx.x of every slot), their
+  // moments and step counts: loaded now, used when the gradient is written below
+  float av[MI_ELBO_ADAM_SLOTS], am[MI_ELBO_ADAM_SLOTS], aq[MI_ELBO_ADAM_SLOTS];
+  float as[MI_ELBO_ADAM_SLOTS];
+#pragma unroll
+  for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
+    av[q] = am[q] = aq[q] = as[q] = 0.0f;
+    if (has_adam && q < sad.num && (int64_t)threadIdx.x < sad.slots[q].numel) {
+      const mi_elbo_adam_slot& A = sad.slots[q];
+      av[q] = A.value[threadIdx.x];
+      am[q] = A.exp_avg[threadIdx.x];
+      aq[q] = A.exp_avg_sq[threadIdx.x];
+      as[q] = *A.step;
+    }
+  }
+  // the Adam update of element i of the tensor behind (factor f, parameter j), gradient g
+  auto adam_step = [&](int f, int j, int64_t i, float g) {
+    if (!has_adam) return;
+#pragma unroll
+    for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
+      if (q >= sad.num || sad.slots[q].factor != f || sad.slots[q].param != j) continue;
+      const AdamCoef c = adam_coef(sad, as[q] + 1.0f);
+      float pv = av[q], mv = am[q], vv = aq[q];
+      adam_update(sad, c, pv, g, mv, vv);
+      const mi_elbo_adam_slot& A = sad.slots[q];
+      A.value[i] = pv;
+      A.exp_avg[i] = mv;
+      A.exp_avg_sq[i] = vv;
+    }
+  };
   if (threadIdx.x == 0) {
     *loss = (float)total;
     *counters = 0u;
@@ -1037,6 +1079,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
             if (out == nullptr) continue;
             if (factor_exp(E, f, j)) g[j] *= (double)pv[j];
             out[0] = (float)g[j];
+            adam_step(f, j, 0, (float)g[j]);
           }
         }
       }
@@ -1061,10 +1104,11 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         if (F.grad[j] == nullptr) continue;
         if (F.transform[j] == MI_TRANSFORM_EXP) g[j] *= (double)pv[j];
         F.grad[j][i * F.grad_stride[j]] = (float)g[j];
+        adam_step(0, j, i, (float)g[j]);
       }
     }
   }
-  static_assert(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan) + 3 * sizeof(void*) <= 4096,
+  static_assert(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan) + 4 * sizeof(void*) <= 4096,
                 "k_elbo_forward's arguments exceed 4 KiB");
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=
                     MI_ELBO_COUNTER_BYTES / sizeof(unsigned), "counter area");
@@ -1074,6 +1118,13 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   if (threadIdx.x == 0 && E.step_counter != nullptr) {
     *E.step_snapshot = step0;
     *E.step_counter = step0 + 1;
+  }
+  if (has_adam) {
+    __syncthreads();   // every thread has read the step counts
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q)
+        if (q < sad.num) *sad.slots[q].step = as[q] + 1.0f;
   }
   MI_ELBO_STAMP(5);
   MI_ELBO_FLUSH();
@@ -1525,8 +1576,40 @@ int mi_elbo_workspace_init(void* workspace, size_t workspace_bytes, void* stream
       hipMemsetAsync(workspace, 0, MI_ELBO_COUNTER_BYTES, static_cast<hipStream_t>(stream)));
 }
 
+int mi_elbo_adam_supported(const mi_elbo* elbo, const mi_elbo_adam* adam, int* supported) {
+  if (!valid(elbo) || adam == nullptr || supported == nullptr) return MI_EINVAL;
+  *supported = 0;
+  if (!(elbo->options & MI_ELBO_FINAL_GRADS) || adam->num < 1 || adam->num > MI_ELBO_ADAM_SLOTS)
+    return 0;
+  const Layout L = make_layout(elbo);
+  if (!final_complete(elbo, L) || L.fin.num != 0 || L.fwd.num != 0) return 0;
+  for (int q = 0; q < adam->num; ++q) {
+    const mi_elbo_adam_slot& A = adam->slots[q];
+    if (A.factor < 0 || A.factor >= elbo->num_factors || A.param < 0 || A.param > 1 ||
+        A.value == nullptr || A.exp_avg == nullptr || A.exp_avg_sq == nullptr || A.step == nullptr)
+      return MI_EINVAL;
+    for (int r = 0; r < q; ++r)
+      if (adam->slots[r].factor == A.factor && adam->slots[r].param == A.param) return MI_EINVAL;
+    const mi_factor& F = elbo->factors[A.factor];
+    if (F.grad[A.param] == nullptr || A.numel != F.n) return 0;
+    bool tail = false;
+    for (int t = 0; t < L.red.tails; ++t) tail |= L.red.tail_factor[t] == A.factor;
+    const bool nt = L.red.nt_job >= 0 && A.factor == 0;
+    // written by the last block: a one-element Beta tail, or the Normal tail's elements (one per
+    // thread)
+    if (!((tail && F.n == 1) || (nt && F.n <= mi::kElboThreads))) return 0;
+  }
+  *supported = 1;
+  return 0;
+}
+
 int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes, float* loss,
                     void* stream) {
+  return mi_elbo_forward_adam(elbo, workspace, workspace_bytes, loss, nullptr, stream);
+}
+
+int mi_elbo_forward_adam(const mi_elbo* elbo, void* workspace, size_t workspace_bytes,
+                         float* loss, const mi_elbo_adam* adam, void* stream) {
   if (!valid(elbo) || loss == nullptr || workspace == nullptr) return MI_EINVAL;
   if (workspace_bytes < workspace_need(elbo)) return MI_EWORKSPACE;
   if (elbo->num_reduce > 0)
@@ -1563,13 +1646,13 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
   const dim3 block(mi::kElboThreads);
   if (L.fwd.num > 0)
     hipLaunchKernelGGL((mi::k_elbo_forward<true, true>), grid, block, 0, s, *elbo, L.fwd, L.red,
-                       work, counters, loss);
+                       work, counters, loss, nullptr);
   else if (has_beta)
     hipLaunchKernelGGL((mi::k_elbo_forward<true, false>), grid, block, 0, s, *elbo, plan, L.red,
-                       work, counters, loss);
+                       work, counters, loss, adam);
   else
     hipLaunchKernelGGL((mi::k_elbo_forward<false, false>), grid, block, 0, s, *elbo, plan,
-                       L.red, work, counters, loss);
+                       L.red, work, counters, loss, adam);
   return to_code(hipGetLastError());
 }
 

@@ -15,6 +15,7 @@
 // accumulators live in registers. Per-(tile, particle) partials are reduced in fp64 by k_finalize.
 #include "adam_math.hpp"
 #include "common.hpp"
+#include "fin_timing.hpp"
 #include "internal.hpp"
 #include "rows.hpp"
 
@@ -251,6 +252,13 @@ MI_DEV uint32_t ld_agent_u32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#if MI_FINISH_TIMING
+__device__ unsigned long long* mi_linfin_tbuf;
+#define MI_LF_STAMP(i) MI_FIN_STAMP(mi_linfin_tbuf, i)
+#else
+#define MI_LF_STAMP(i) do { } while (0)
+#endif
+
 constexpr int kFinPairs = 4;   // (value, particle) pairs per thread and pass of the final sum
 constexpr int kFinChunks = 8;  // segment chunks per value (host-checked)
 
@@ -263,11 +271,13 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
   const int tid = threadIdx.x;
   const int64_t K = L.K;
   const int P = (int)L.P;
+  MI_LF_STAMP(1);
   __builtin_amdgcn_s_waitcnt(0);   // this thread's (agent-coherent) partial stores are complete
   __syncthreads();
   if (tid == 0) {
     const unsigned nb = gridDim.x;
     const unsigned t = atomicAdd(F.counters, 1u);
+    MI_LF_STAMP(2);
     int r = (t + (unsigned)F.helpers >= nb) ? (int)(t + (unsigned)F.helpers - nb) : -1;
     if (r >= 0) {
       // the other blocks are resident (the host checked the grid fits the chip) and never wait:
@@ -286,6 +296,7 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
   __syncthreads();
   const int h = role;
   if (h < 0) return;
+  MI_LF_STAMP(3);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double* lds = reinterpret_cast<double*>(scratch);   // [NT] doubles during the jobs
   // jobs h, h + helpers, ... (more jobs than blocks in a small launch); the block that completes
@@ -327,8 +338,10 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
     __syncthreads();
     final_block = role > 0;
   }
+  MI_LF_STAMP(4);
   if (!final_block) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  MI_LF_STAMP(5);
 
   // ---- the last helper: chunk sums in a fixed order, then the tail --------------------------
   const mi_draw& D = L.draw;
@@ -458,12 +471,14 @@ __device__ void lin_finish(const mi_linear& L, const LinFinish& F,
     __hip_atomic_store(F.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.counters + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  MI_LF_STAMP(6);
   if (F.adam.num > 0) {
     // the optimizer step over the gradients just written (every block has read the parameters
     // for its draw before arriving): the training step ends inside this launch
     __syncthreads();
     adam_block<NT>(F.adam);
   }
+  MI_LF_STAMP(7);
 }
 
 // Phase timestamps (MI_LINEAR_TIMING builds only, tools/linear_timing.py): wall clock at 8 points of
@@ -573,6 +588,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   unsigned long long ts_[8] = {};
 #endif
   MI_LIN_STAMP(0);
+  if constexpr (FINISH) MI_LF_STAMP(0);
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
@@ -1417,6 +1433,13 @@ int mi_linear_elbo_forward(const mi_linear* site, const mi_elbo* elbo, void* wor
     return to_code(e);
   return 0;
 }
+
+#if MI_FINISH_TIMING
+int mi_linear_finish_timing(unsigned long long* buffer) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(mi::mi_linfin_tbuf), &buffer, sizeof(buffer)) == hipSuccess
+             ? 0 : MI_EINVAL;
+}
+#endif
 
 int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,
                       float* dslots, uint32_t* flags, void* stream) {

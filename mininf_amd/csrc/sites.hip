@@ -23,6 +23,7 @@
 #include "beta_grad.hpp"
 #include "common.hpp"
 #include "entropy.hpp"
+#include "fin_timing.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -602,6 +603,13 @@ struct BcastFinish {
   mi_adam adam;           // num 0: no optimizer step in the launch
 };
 
+#if MI_FINISH_TIMING
+__device__ unsigned long long* mi_bcastfin_tbuf;
+#define MI_BF_STAMP(i) MI_FIN_STAMP(mi_bcastfin_tbuf, i)
+#else
+#define MI_BF_STAMP(i) do { } while (0)
+#endif
+
 template <bool COHERENT>
 MI_DEV void st_coh(float* p, float v) {
   if constexpr (COHERENT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -643,11 +651,13 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
   __shared__ double red3[kBcastThreads / kWave][3];
   const int tid = threadIdx.x;
   const int64_t K = G.K;
+  MI_BF_STAMP(1);
   __builtin_amdgcn_s_waitcnt(0);   // this thread's (agent-coherent) stores are complete
   __syncthreads();
   if (tid == 0) {
     const unsigned nb = gridDim.x;
     const unsigned t = atomicAdd(F.counters, 1u);
+    MI_BF_STAMP(2);
     int r = (t + (unsigned)F.helpers >= nb) ? (int)(t + (unsigned)F.helpers - nb) : -1;
     if (r >= 0) {
       // the blocks not yet arrived are running or about to be dispatched (they never wait); the
@@ -666,6 +676,7 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
   __syncthreads();
   const int h = role;
   if (h < 0) return;
+  MI_BF_STAMP(3);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // jobs h, h + helpers, ... (a small launch has fewer blocks than jobs); a block completes a
   // particle chunk's jobs -> its chunk stage; the block completing the last chunk -> the tail
@@ -738,8 +749,10 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
     __syncthreads();
     final_block = role > 0;
   }
+  MI_BF_STAMP(4);
   if (!final_block) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  MI_BF_STAMP(5);
   // ---- 3. the loss, the Beta factor's sums and final gradients, the step, the mirror ---------
   const uint32_t fw = (int64_t)tid < F.nflags ? ld_coh(F.flags + tid) : 0u;
   if (tid == 0) {
@@ -780,11 +793,13 @@ MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* p
   if ((int64_t)tid < F.nflags) F.flags_mirror[tid] = fw;
   for (int64_t i = tid + kBcastThreads; i < F.nflags; i += kBcastThreads)
     F.flags_mirror[i] = ld_coh(F.flags + i);
+  MI_BF_STAMP(6);
   if (F.adam.num > 0) {
     // the optimizer step over the gradients thread 0 wrote: the training step ends here
     __syncthreads();
     adam_block<kBcastThreads>(F.adam);
   }
+  MI_BF_STAMP(7);
 }
 
 // One workgroup of a group's side job (mi_side): the mi_beta_dgrad factors of 256 (draw, component)
@@ -827,6 +842,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   __shared__ float scratch[kBcastThreads / 64];
   // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below); bit 2: L2
   // prefetch of the chunk
+  if constexpr (FINISH) MI_BF_STAMP(0);
   const int rank1 = mode & 1;
   const bool balance = (mode & 2) != 0;
   const int64_t chunks = nseg - 1;
@@ -1857,6 +1873,13 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
                             (double)G.grad_scale, total, site_lp, slot_grad, scratch, s,
                             rank1_mask);
 }
+
+#if MI_FINISH_TIMING
+int mi_group_finish_timing(unsigned long long* buffer) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(mi::mi_bcastfin_tbuf), &buffer, sizeof(buffer)) == hipSuccess
+             ? 0 : MI_EINVAL;
+}
+#endif
 
 int mi_group_elbo_supported(const mi_group* group, const mi_elbo* elbo, int* supported,
                             size_t* elbo_workspace_bytes) {

@@ -1642,16 +1642,68 @@ class _ElboPlan:
         ws = _elbo_workspace(self.device, size.value)
         loss = torch.empty((), dtype=torch.float32, device=self.device)
         guide.join_side()   # Beta implicit-gradient factors (mi_beta_dgrad) from the side stream
-        nat.check(lib.mi_elbo_forward(ctypes.byref(E), ws.data_ptr(), ws.numel(), loss.data_ptr(),
-                                      nat.stream_handle(self.device)), "mi_elbo_forward")
+        stream = nat.stream_handle(self.device)
+
+        def launch(adam):
+            if adam is None:
+                return lib.mi_elbo_forward(ctypes.byref(E), ws.data_ptr(), ws.numel(),
+                                           loss.data_ptr(), stream)
+            return lib.mi_elbo_forward_adam(ctypes.byref(E), ws.data_ptr(), ws.numel(),
+                                            loss.data_ptr(), adam, stream)
         self.state = (E, results, cat_results, lin_results, extra, terms)
+        # with the final gradients written, the launch is held for the optimizer step, which
+        # then runs in its last block (mi_elbo_forward_adam). Everything E points to stays alive
+        # until it runs: the backward drops self.state, and the deferred reductions' outputs
+        # (written by this launch) are referenced nowhere else -- freed early, their memory would
+        # be handed to the allocations made before the launch (the optimizer's own descriptor).
+        keep = (self, E, ws, loss, self.state, self.final, deferred, buffers)
+        if self.final is None or not _defer_step(launch, "mi_elbo_forward", self.final, keep,
+                                                 self._elbo_adam(E)):
+            nat.check(launch(None), "mi_elbo_forward")
         return loss
+
+    def _elbo_adam(self, E):
+        """The adapter of the held ELBO forward: an mi_adam descriptor whose every tensor's
+        gradient is one of the final gradients this launch writes -> the device pointer of the
+        matching mi_elbo_adam (None: declined)."""
+        final = self.final
+        device = self.device
+
+        def adapt(adam):
+            if adam.num > nat.ELBO_ADAM_SLOTS:
+                return None
+            where = {}
+            for f, grads in enumerate(final):
+                if f not in self.absorbed:
+                    continue
+                for j, g in enumerate(grads):
+                    if g is not None:
+                        where[g.data_ptr()] = (f, j, g.numel())
+            desc = nat.ElboAdam()
+            desc.num, desc.maximize = adam.num, adam.maximize
+            desc.lr, desc.beta1, desc.beta2 = adam.lr, adam.beta1, adam.beta2
+            desc.eps, desc.weight_decay = adam.eps, adam.weight_decay
+            for t in range(adam.num):
+                T = adam.tensors[t]
+                hit = where.get(T.grad)
+                if hit is None or hit[2] != T.numel:
+                    return None
+                slot = desc.slots[t]
+                slot.factor, slot.param = hit[0], hit[1]
+                slot.value, slot.exp_avg, slot.exp_avg_sq = T.param, T.exp_avg, T.exp_avg_sq
+                slot.step, slot.numel = T.step, T.numel
+            ok = ctypes.c_int(0)
+            nat.check(nat.lib().mi_elbo_adam_supported(ctypes.byref(E), ctypes.byref(desc),
+                                                       ctypes.byref(ok)), "mi_elbo_adam_supported")
+            return _elbo_adam_device(desc, device) if ok.value else None
+        return adapt
 
     def _linear_elbo_candidate(self) -> bool:
         """
         The step is one linear site over the guide's one Normal factor that its launch draws
         (examples/minibatch.md:76-88): the launch may run the whole ELBO forward
-        (mi_linear_elbo_forward; the library decides, MININF_AMD_LINEAR_ELBO=0 disables it).
+        (mi_linear_elbo_forward; the library decides; opt-in, MININF_AMD_LINEAR_ELBO=1: measured
+        slower than the two-launch path).
         """
         if len(self.linears) != 1 or self.launchers or self.categorical or self.fallback or \
                 self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
@@ -1659,7 +1711,7 @@ class _ElboPlan:
         linear = self.linears[0]
         return (linear.draw is not None and not linear.draw.done and linear.needs_grads() and
                 ("lin_theta", 0) in self.skip_lin and
-                os.environ.get("MININF_AMD_LINEAR_ELBO", "1") != "0" and
+                os.environ.get("MININF_AMD_LINEAR_ELBO", "0") == "1" and
                 os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
 
     def _forward_linear_elbo(self) -> Optional[torch.Tensor]:
@@ -1746,8 +1798,9 @@ class _ElboPlan:
         (mi_linear.draw) / their minibatch rows (mi_rows) themselves; fused_draws: Normal guide
         factors drawn in registers by the site programs (mi_draw); deferred_reductions: site
         reductions finished by the ELBO forward; final_grads: the forward wrote the guide
-        gradients (no backward launch for loss.backward()); linear_elbo: the linear launch ran the
-        whole ELBO forward (mi_linear_elbo_forward).
+        gradients (no backward launch for loss.backward()); linear_elbo / group_elbo: the site
+        launch ran the whole ELBO forward (mi_linear_elbo_forward / mi_group_elbo_forward);
+        optimizer_step: the Adam step ran in the held launch's last block (no launch of its own).
         """
         return {
             "folded_priors": sum(l.prior is not None for l in self.launchers) +
@@ -1759,13 +1812,15 @@ class _ElboPlan:
             "final_grads": int(getattr(self, "final", None) is not None),
             "linear_elbo": int(self.fused_linear),
             "group_elbo": int(self.fused_group),
+            "optimizer_step": 0,   # set when the optimizer step joins the held launch
         }
 
     def _group_elbo_candidate(self) -> bool:
         """
         The step is one site group over the guide's one one-element Beta factor whose draws only
         that group reads (the README model, README.md:40-69): its launch may run the whole ELBO
-        forward (mi_group_elbo_forward; the library decides, MININF_AMD_GROUP_ELBO=0 disables it).
+        forward (mi_group_elbo_forward; the library decides; opt-in, MININF_AMD_GROUP_ELBO=1: measured
+        slower than the two-launch path).
         """
         if len(self.launchers) != 1 or self.linears or self.categorical or self.fallback or \
                 self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
@@ -1775,7 +1830,7 @@ class _ElboPlan:
                 plan.drawn is not None and plan.drawn.conc is not None and
                 plan.drawn.dgrad is None and self.factors[0].n == 1 and
                 os.environ.get("MININF_AMD_BETA_SIDE", "1") != "0" and
-                os.environ.get("MININF_AMD_GROUP_ELBO", "1") != "0" and
+                os.environ.get("MININF_AMD_GROUP_ELBO", "0") == "1" and
                 os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
 
     def _forward_group_elbo(self) -> Optional[torch.Tensor]:
@@ -2030,12 +2085,13 @@ class PendingGrad(torch.Tensor):
 
 
 class _PendingStep:
-    def __init__(self, launch, what: str, grads: List[torch.Tensor], keep) -> None:
-        self._launch = launch        # launch(adam descriptor or None) -> error code
+    def __init__(self, launch, what: str, grads: List[torch.Tensor], keep, adapter) -> None:
+        self._launch = launch        # launch(optimizer argument or None) -> error code
         self.what = what
         self.grad_ptrs = {g.data_ptr() for g in grads if g is not None}
         self.held: List[Tuple[torch.Tensor, torch.Tensor]] = []   # (param, PendingGrad)
         self._keep = keep            # the launch's buffers, alive until it has run
+        self.adapt = adapter         # adapter(mi_adam descriptor) -> launch argument, or None
 
     def hold(self, var: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
         """``grad`` as the PendingGrad to assign to ``var.grad``."""
@@ -2079,26 +2135,56 @@ def attach_optimizer(adam, grads: Sequence[torch.Tensor]) -> bool:
     step is small enough (<= 16384 elements, csrc/adam_math.hpp kFusedAdamMaxNumel); the other
     gradients are complete already (earlier launches on the stream). False: nothing done.
     """
-    global _PENDING
+    global _PENDING, LAST_FUSIONS
     step = _PENDING
-    if step is None or adam.num < 1 or             sum(adam.tensors[j].numel for j in range(adam.num)) > _FUSED_ADAM_MAX_NUMEL or             not any(g.data_ptr() in step.grad_ptrs for g in grads):
+    if step is None or adam.num < 1 or not any(g.data_ptr() in step.grad_ptrs for g in grads):
+        return False
+    arg = step.adapt(adam)
+    if arg is None:
         return False
     _PENDING = None
-    step.run(adam)
+    step.run(arg)
+    LAST_FUSIONS["optimizer_step"] = 1
     return True
 
 
 _FUSED_ADAM_MAX_NUMEL = 16384
 
 
-def _defer_step(launch, what: str, grads, keep) -> bool:
+def _small_adam(adam):
+    """The finishing launches take the mi_adam descriptor itself (csrc/adam_math.hpp's limit)."""
+    numel = sum(adam.tensors[j].numel for j in range(adam.num))
+    return adam if numel <= _FUSED_ADAM_MAX_NUMEL else None
+
+
+def _defer_step(launch, what: str, grads, keep, adapter=_small_adam) -> bool:
     """Hold ``launch`` for the optimizer (True), or False: the caller launches now."""
     global _PENDING
     if os.environ.get("MININF_AMD_DEFER_STEP", "1") == "0":
         return False
     flush_pending_step()
-    _PENDING = _PendingStep(launch, what, [g for gs in grads for g in gs if g is not None], keep)
+    _PENDING = _PendingStep(launch, what, [g for gs in grads for g in gs if g is not None], keep,
+                            adapter)
     return True
+
+
+# device copies of mi_elbo_adam descriptors (a captured step reads its copy on every replay, so
+# copies are never freed; a process has a handful -- one per optimizer and model structure)
+_ELBO_ADAM_COPIES: Dict[Tuple[int, bytes], torch.Tensor] = {}
+_ELBO_ADAM_MAX_COPIES = 256
+
+
+def _elbo_adam_device(desc, device: torch.device) -> Optional[int]:
+    raw = bytes(desc)
+    key = (device.index if device.index is not None else torch.cuda.current_device(), raw)
+    buf = _ELBO_ADAM_COPIES.get(key)
+    if buf is None:
+        if len(_ELBO_ADAM_COPIES) >= _ELBO_ADAM_MAX_COPIES or \
+                torch.cuda.is_current_stream_capturing():
+            return None   # (no host-to-device copy inside a capture)
+        buf = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        _ELBO_ADAM_COPIES[key] = buf
+    return buf.data_ptr()
 
 
 nat.set_launch_hook(flush_pending_step)

@@ -551,7 +551,8 @@ class EvidenceLowerBoundLoss(nn.Module):
             try:
                 loss, joint = engine.elbo(trace, g0, device, factors, entropy_scale, samples,
                                           flags=flags, step_words=step_words, mirror=mirror)
-                self.last_fusions = dict(engine.LAST_FUSIONS)
+                # (the same dict: an optimizer step that joins the held launch marks it)
+                self.last_fusions = engine.LAST_FUSIONS
                 joint.sticky = sticky and joint.flags is not None and not joint.checks and \
                     joint.flags.data_ptr() == flags.data_ptr()
             finally:

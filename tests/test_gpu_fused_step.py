@@ -1,8 +1,10 @@
 """
-The whole training step in ONE kernel (ABI 14): after a fused ELBO (mi_linear_elbo_forward for the
-minibatch regression, examples/minibatch.md:76-88; mi_group_elbo_forward for the README model,
-README.md:40-69) the finishing launch is held until the Adam step over its gradients, which then
-runs in the launch's last block (csrc/adam_math.hpp, torch's fused-Adam arithmetic).
+The optimizer step inside the step's last launch (ABI 14): the launch that writes the final guide
+gradients -- the ELBO forward (mi_elbo_forward_adam, the default) or, opt-in, the site launch that
+finishes the ELBO itself (mi_linear_elbo_forward for the minibatch regression,
+examples/minibatch.md:76-88; mi_group_elbo_forward for the README model, README.md:40-69) -- is held
+until the Adam step over its gradients, which then runs in that launch's last block
+(csrc/adam_math.hpp, torch's fused-Adam arithmetic).
 
 * parameters and losses are BIT-identical to the held-off path (MININF_AMD_DEFER_STEP=0: the
   finishing launch, then mi_adam_step) over several steps, eager and captured, and mi_adam_step
@@ -81,7 +83,16 @@ def _coin(device, validate=False, n=200_000, K=1024):
 
 
 MODELS = {"regression": _regression, "coin": _coin}
-FUSED = {"regression": "mi_linear_elbo_forward", "coin": "mi_group_elbo_forward"}
+FINISH = {"regression": ("MININF_AMD_LINEAR_ELBO", "mi_linear_elbo_forward"),
+          "coin": ("MININF_AMD_GROUP_ELBO", "mi_group_elbo_forward")}
+PATHS = ["elbo", "finish"]
+
+
+def _path(monkeypatch, name, path):
+    """The held launch: the ELBO forward (default) or the site launch finishing the ELBO."""
+    env, fn = FINISH[name]
+    monkeypatch.setenv(env, "1" if path == "finish" else "0")
+    return fn if path == "finish" else "mi_elbo_forward_adam"
 
 
 def _train(device, monkeypatch, name, held, steps=4, between=None, optimizer_cls=Adam,
@@ -104,25 +115,33 @@ def _train(device, monkeypatch, name, held, steps=4, between=None, optimizer_cls
         loss_fn.last_fusions
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_step_joins_the_finishing_launch(device, monkeypatch, name):
+def test_step_joins_the_held_launch(device, monkeypatch, name, path):
+    fn = _path(monkeypatch, name, path)
     adam = _spy(monkeypatch, "mi_adam_step")
-    fused = _spy(monkeypatch, FUSED[name])
+    fused = _spy(monkeypatch, fn)
     losses, params, fusions = _train(device, monkeypatch, name, held=True)
-    assert adam == [], "the optimizer step ran in the finishing launch"
-    assert len(fused) == 4 and all(call[10] is not None for call in fused)
-    assert fusions["linear_elbo" if name == "regression" else "group_elbo"] == 1
+    assert adam == [], "the optimizer step ran in the held launch"
+    assert len(fused) == 4
+    if path == "finish":
+        assert all(call[10] is not None for call in fused)
+        assert fusions["linear_elbo" if name == "regression" else "group_elbo"] == 1
+    assert fusions["optimizer_step"] == 1
     adam.clear()
     fused.clear()
-    ref_losses, ref_params, _ = _train(device, monkeypatch, name, held=False)
-    assert len(adam) == 4 and all(call[10] is None for call in fused)
+    ref_losses, ref_params, ref_fusions = _train(device, monkeypatch, name, held=False)
+    assert len(adam) == 4 and ref_fusions["optimizer_step"] == 0
+    assert all(call[10] is None for call in fused) if path == "finish" else fused == []
     assert torch.equal(losses, ref_losses)
     for a, b in zip(params, ref_params):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name):
+def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name, path):
+    _path(monkeypatch, name, path)
     ref_losses, ref_params, _ = _train(device, monkeypatch, name, held=False, steps=9)
     monkeypatch.setenv("MININF_AMD_DEFER_STEP", "1")
     module, loss_fn, approx, conditioned = MODELS[name](device, validate=True)
@@ -145,9 +164,12 @@ def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name):
         assert torch.equal(a.detach(), b)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_consumers_between_backward_and_step(device, monkeypatch, name):
+def test_consumers_between_backward_and_step(device, monkeypatch, name, path):
     """Gradient clipping reads the held gradients: the launch runs first, the step on its own."""
+    _path(monkeypatch, name, path)
+
     def clip(module):
         torch.nn.utils.clip_grad_norm_(module.parameters(), 0.5)
 

@@ -32,7 +32,7 @@ def test_readme_model_fusions(device):
     loss_fn(mi.condition(model, x=x), {"theta": approx()}).backward()
     f = loss_fn.last_fusions
     assert f["folded_priors"] == 1 and f["final_grads"] == 1 and f["deferred_reductions"] == 1
-    assert f["linear_elbo"] == 0 and f["fused_draws"] == 0
+    assert f["group_elbo"] == 0 and f["linear_elbo"] == 0 and f["fused_draws"] == 0
 
 
 def test_minibatch_regression_fusions(device):
@@ -55,8 +55,8 @@ def test_minibatch_regression_fusions(device):
     Xb, yb = loader.next()
     loss_fn(mi.condition(model, X=Xb, y=yb), {"theta": approx()}).backward()
     f = loss_fn.last_fusions
-    assert f["linear_elbo"] == 1 and f["linear_theta_draws"] == 1 and f["linear_rows"] == 1
-    assert f["folded_priors"] == 1 and f["final_grads"] == 1
+    assert f["linear_theta_draws"] == 1 and f["linear_rows"] == 1
+    assert f["folded_priors"] == 1 and f["final_grads"] == 1 and f["linear_elbo"] == 0
 
 
 def test_masked_hierarchical_fusions(device):

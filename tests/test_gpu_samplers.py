@@ -10,8 +10,12 @@ its own (Philox-4x32-7 blocks, Marsaglia-Tsang with the alpha < 1 boost), and th
   far away, so agreement of every draw to a few ulp means every decision agreed; the inputs are
   chosen so that rejections, the alpha < 1 boost and several Philox blocks per draw all occur
   (checked on the oracle's block counts, so the comparison is not vacuous);
-- values within ULP_TOL units in the last place: the device evaluates log / sqrt / cos / pow on the
-  float hardware and OCML routines, the oracle in double precision rounded to float.
+- values within REL_TOL relative: the device evaluates log / sqrt / cos / pow on the float
+  hardware and OCML routines, the oracle in double precision rounded to float. Most draws agree to
+  a few ulp; the algorithm amplifies the generator's ulp-level differences where it is
+  ill-conditioned -- v = (1 + c x)^3 near y = 0 (tens of ulp), the alpha < 1 boost U^(1/alpha)
+  at alpha = 0.05 (hundreds) -- so the bound is relative, far below the O(1) difference a single
+  differing accept / reject decision makes (a different normal).
 The full-size C2 step without injected draws ("Next round" 1b) then checks the bench's
 own path end to end: the ELBO over the device's Beta draws against the oracle ELBO over the
 restated draws.
@@ -27,9 +31,21 @@ from oracle import build as oracle_build, elbo as oracle
 
 pytestmark = pytest.mark.gpu
 
-# measured maximum over these draws: see the assertion messages (device transcendentals are a
-# few ulp from the correctly rounded double-precision values)
-ULP_TOL = 8
+# first GPU run: max 88 ulp (gamma, alpha = 1, y near 0), 1039 ulp (beta 0.05 / 0.05: the boost);
+# relative 6e-5 at most
+REL_TOL = 2e-4
+
+
+def check_draws(got, want):
+    """Every draw within REL_TOL relative; the bulk within a few ulp."""
+    got = np.asarray(got, np.float32)
+    want = np.asarray(want, np.float32)
+    rel = np.abs(got.astype(np.float64) - want) / np.maximum(np.abs(want.astype(np.float64)),
+                                                              1e-37)
+    at = np.unravel_index(rel.argmax(), rel.shape)
+    assert rel.max() <= REL_TOL, f"max relative {rel.max():.3g} at {at}: {got[at]} vs {want[at]}"
+    d = ulps(got, want)
+    assert np.median(d) <= 2 and (d <= 8).mean() >= 0.99, (np.median(d), (d <= 8).mean())
 
 
 def ulps(a, b):
@@ -56,9 +72,7 @@ def test_gamma_sampler_matches_restatement(device, seed, step, stream_id, offset
                                          None, stream_id, offset, None, g.data_ptr(), x.data_ptr(),
                                          None), "mi_gamma_rsample")
     want, blocks = oracle_build.gamma_draws(ALPHAS, K, seed, step, stream_id, offset)
-    got = g.cpu().numpy()
-    d = ulps(got, want)
-    assert d.max() <= ULP_TOL, f"max {d.max()} ulp at {np.unravel_index(d.argmax(), d.shape)}"
+    check_draws(g.cpu().numpy(), want)
     # the comparison covers rejections (more than one block for alpha >= 1) and several blocks
     assert (blocks[:, ALPHAS >= 1] > 1).sum() > 10
     assert blocks.max() >= 3
@@ -78,7 +92,7 @@ def test_gamma_sampler_device_step_counter(device):
                                          counter.data_ptr(), 4, 0, None, g.data_ptr(), x.data_ptr(),
                                          None), "mi_gamma_rsample")
     want, _ = oracle_build.gamma_draws(ALPHAS, K, seed, 7, 4, 0)
-    assert ulps(g.cpu().numpy(), want).max() <= ULP_TOL
+    check_draws(g.cpu().numpy(), want)
     np.testing.assert_allclose(x.cpu().numpy(), np.maximum(want / 2, 1.17549435e-38), rtol=1e-7)
 
 
@@ -98,10 +112,8 @@ def test_beta_sampler_matches_restatement(device, seed, step, stream_id, offset)
               "mi_beta_rsample")
     want, g1, g0, b1, b0 = oracle_build.beta_draws(C1, C0, K, seed, step, stream_id, offset)
     got = x.cpu().numpy()
-    # x = g1 / (g1 + g0): a few ulp in each gamma give a few ulp in x; x near 0 (alpha = 0.05)
-    # carries the relative error of g1 itself
-    d = ulps(got, want)
-    assert d.max() <= 2 * ULP_TOL, f"max {d.max()} ulp at {np.unravel_index(d.argmax(), d.shape)}"
+    # x = g1 / (g1 + g0): x near 0 (alpha = 0.05) carries the relative error of g1 itself
+    check_draws(got, want)
     assert (b1 > 1).sum() > 10 and (b0 > 1).sum() > 10
     assert ((got > 0) & (got < 1)).mean() > 0.99
 
@@ -122,7 +134,7 @@ def test_beta_sampler_exp_variant_matches_restatement(device):
     np.testing.assert_allclose(c[:, 0], np.exp(u1.cpu().double().numpy()), rtol=3e-7)
     np.testing.assert_allclose(c[:, 1], np.exp(u0.cpu().double().numpy()), rtol=3e-7)
     want = oracle_build.beta_draws(c[:, 0], c[:, 1], K, seed, step, 2, 0)[0]
-    assert ulps(x.cpu().numpy(), want).max() <= 2 * ULP_TOL
+    check_draws(x.cpu().numpy(), want)
 
 
 def test_gamma_guide_draw_through_the_elbo(device):
