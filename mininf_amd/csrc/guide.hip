@@ -212,6 +212,9 @@ MI_DEV float sample_gamma(float alpha, Stream& rng) {
 
 // EXP: c1 / c0 hold the unconstrained parameters; the concentrations are expf of them (as
 // k_transform_params) and the k = 0 threads write them to conc[i, 0..1].
+// Two lanes per draw: the even lane samples g1 (sub-stream 0), the odd lane g0 (sub-stream 1) --
+// the two rejection loops run side by side instead of one after the other (the draw is a short
+// latency-bound launch); the pair exchanges its variates and the even lane writes x = g1 / (g1 + g0).
 template <bool EXP>
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
     const float* __restrict__ c1, int64_t c1_s, const float* __restrict__ c0, int64_t c0_s,
@@ -219,25 +222,29 @@ __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample(
     uint32_t stream_id, int64_t poff, const float* __restrict__ x_in, float* __restrict__ x,
     float* __restrict__ conc) {
   const int64_t t = (int64_t)blockIdx.x * kGuideThreads + threadIdx.x;
-  if (t >= K * N) return;
-  const int64_t k = t / N, i = t - k * N;
+  if (t >= 2 * K * N) return;   // (whole pairs: the bound is even)
+  const int64_t d = t >> 1;
+  const uint32_t side = (uint32_t)(t & 1);
+  const int64_t k = d / N, i = d - k * N;
   const float a = EXP ? expf(c1[i * c1_s]) : c1[i * c1_s];
   const float b = EXP ? expf(c0[i * c0_s]) : c0[i * c0_s];
-  if (EXP && k == 0) {
+  if (EXP && k == 0 && side == 0) {
     conc[2 * i] = a;
     conc[2 * i + 1] = b;
   }
   if (x_in != nullptr) {
-    x[t] = x_in[t];
+    if (side == 0) x[d] = x_in[d];
     return;
   }
   if (step_dev != nullptr) step += *step_dev;
-  Stream ra{seed, step, stream_id, 0u, (uint64_t)i, (uint64_t)(poff + k)};
-  Stream rb{seed, step, stream_id, 1u, (uint64_t)i, (uint64_t)(poff + k)};
-  const float g1 = sample_gamma(a, ra);
-  const float g0 = sample_gamma(b, rb);
-  const float s = g1 + g0;
-  x[t] = s > 0.0f ? g1 / s : (a >= b ? 1.0f : 0.0f);
+  Stream rng{seed, step, stream_id, side, (uint64_t)i, (uint64_t)(poff + k)};
+  const float g = sample_gamma(side == 0 ? a : b, rng);
+  const float other = __shfl_xor(g, 1, kWave);
+  if (side == 0) {
+    const float g1 = g, g0 = other;
+    const float s = g1 + g0;
+    x[d] = s > 0.0f ? g1 / s : (a >= b ? 1.0f : 0.0f);
+  }
 }
 
 __global__ __launch_bounds__(kGuideThreads) void k_beta_rsample_bwd(
@@ -539,7 +546,7 @@ int mi_beta_rsample(const float* c1, int64_t c1_stride, const float* c0, int64_t
                     const float* x_in, float* x, void* stream) {
   if (c1 == nullptr || c0 == nullptr || x == nullptr || K < 1 || N < 1 || stream_id > 0xFFFFFFu)
     return MI_EINVAL;
-  hipLaunchKernelGGL(mi::k_beta_rsample<false>, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+  hipLaunchKernelGGL(mi::k_beta_rsample<false>, dim3((unsigned)ceil_div(2 * K * N, mi::kGuideThreads)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), c1, c1_stride,
                      c0, c0_stride, K, N, seed, step, step_device, stream_id, particle_offset, x_in,
                      x, nullptr);
@@ -553,7 +560,7 @@ int mi_beta_rsample_exp(const float* u1, int64_t u1_stride, const float* u0, int
   if (u1 == nullptr || u0 == nullptr || conc == nullptr || x == nullptr || K < 1 || N < 1 ||
       stream_id > 0xFFFFFFu)
     return MI_EINVAL;
-  hipLaunchKernelGGL(mi::k_beta_rsample<true>, dim3((unsigned)ceil_div(K * N, mi::kGuideThreads)),
+  hipLaunchKernelGGL(mi::k_beta_rsample<true>, dim3((unsigned)ceil_div(2 * K * N, mi::kGuideThreads)),
                      dim3(mi::kGuideThreads), 0, static_cast<hipStream_t>(stream), u1, u1_stride,
                      u0, u0_stride, K, N, seed, step, step_device, stream_id, particle_offset, x_in,
                      x, conc);

@@ -2,8 +2,9 @@
 Where a k_linear_mfma block spends its time: phase timestamps (wall clock, 100 MHz) from a build
 of the library with -DMI_LINEAR_TIMING=1, at the C4 shape.
 
-    python tools/linear_timing.py build        (on the CPU: tools/_timing/libmininf_amd.so)
+    python tools/linear_timing.py build        (on the CPU: tools/_timing/libmininf_amd_lin.so)
     python tools/linear_timing.py run [N P K]  (on the GPU)
+    python tools/linear_timing.py bench [c4]   (on the GPU: the bench step's own launch)
 
 Stamps per wave: 0 entry, 1 before staging, 2 staged (loads issued, LDS written), 3 after the
 staging barrier, 4 after the tiles, 5 after the tile barrier, 6 after the row-subset combine,
@@ -16,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "_timing", "libmininf_amd.so")
+OUT = os.path.join(ROOT, "tools", "_timing", "libmininf_amd_lin.so")
 
 
 def build():
@@ -85,8 +86,61 @@ def run(N=65536, P=32, K=32):
     print(f"  wave lifetime  mean {float(life.mean()):6.2f} us  max {float(life.max()):6.2f} us")
 
 
+def _phases(raw, label):
+    import torch
+    rows = raw[raw.numel() % 8:].reshape(-1, 8)
+    ok = (rows[:, 0] > 0) & ((rows[:, 1:] - rows[:, :-1]) >= 0).all(dim=1) & \
+        ((rows[:, 7] - rows[:, 0]) < 1_000_000)
+    rows = rows[ok]
+    rows = rows[(rows[:, 0] - rows[:, 0].median()).abs() < 1_000_000]
+    t = rows.double() / 100.0
+    base = t[:, 0].min()
+    names = ["entry->stage", "stage issue", "stage barrier", "tiles", "tile barrier", "combine",
+             "partials"]
+    print(f"{label}: waves {rows.shape[0]}  entry spread {float(t[:, 0].max() - base):.2f} us  "
+          f"last exit {float(t[:, 7].max() - base):.2f} us", flush=True)
+    for i, name in enumerate(names):
+        d = t[:, i + 1] - t[:, i]
+        q = torch.quantile(d, torch.tensor([0.5, 0.9], dtype=torch.float64))
+        print(f"  {name:14s} mean {float(d.mean()):6.2f}  p50 {float(q[0]):6.2f}  "
+              f"p90 {float(q[1]):6.2f}  max {float(d.max()):6.2f} us")
+    life = t[:, 7] - t[:, 0]
+    print(f"  wave lifetime  mean {float(life.mean()):6.2f} us  max {float(life.max()):6.2f} us")
+    start = t[:, 0] - base
+    print(f"  entry          p50 {float(start.median()):6.2f}  max {float(start.max()):6.2f} us")
+
+
+def run_bench(config="c4"):
+    """The bench's own step (rows, theta draw and prior in the launch): stamps of its linear
+    launch, read from the launcher's workspace after each eager step."""
+    import torch
+    from mininf_amd import _native as nat
+    nat.LIB_PATH = OUT
+    nat.lib()
+    import bench
+    import mininf_amd
+    device = torch.device("cuda", 0)
+    w = bench.workload(config, device, 1, 0)
+    optimizer = mininf_amd.optim.Adam(w["module"].parameters(), lr=w["lr"])
+    loss_fn = mininf_amd.nn.EvidenceLowerBoundLoss(num_particles=w["k_local"], seed=1)
+    for step in range(8):
+        optimizer.zero_grad(set_to_none=True)
+        loss = loss_fn(w["conditioned"](), w["guide"]())
+        plan = loss.grad_fn.plan
+        work = plan.linears[0].workspace
+        torch.cuda.synchronize()
+        raw = work.view(torch.int64).cpu()
+        loss.backward()
+        optimizer.step()
+        if step >= 5:
+            _phases(raw, f"{config} step {step}")
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
+    elif sys.argv[1] == "bench":
+        run_bench(*(sys.argv[2:3]))
     else:
         run(*(int(v) for v in sys.argv[2:5]))
