@@ -913,6 +913,18 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     }
   }
   MI_ELBO_STAMP(2);
+  // mi_elbo_forward_adam: every share-writing block fetches the optimizer's descriptor (240 B, an
+  // L2 hit after the first) into LDS while its completion count is in flight, so the last block
+  // can issue the optimised tensors' loads with its first loads
+  __shared__ mi_elbo_adam sad;
+  const bool has_adam = !ABSORB && adam != nullptr;
+  if (has_adam) {
+    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
+    static_assert(kWords <= kElboThreads, "one descriptor word per thread");
+    if ((int)threadIdx.x < kWords)
+      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
+          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
+  }
   if (threadIdx.x == 0) {
     // The shares (and the slot gradients the tail reads) are device-coherent stores, complete
     // (s_waitcnt) before the barrier / the counter update: no per-block L2 write-back fence,
@@ -942,15 +954,26 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   // the tails' partials and concentrations, the validation words, the generator step) is issued
   // before the first sum: one memory round trip instead of one per stage.
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // mi_elbo_forward_adam: the optimizer's descriptor into LDS with this phase's first loads
-  __shared__ mi_elbo_adam sad;
-  const bool has_adam = !ABSORB && adam != nullptr;
-  if (has_adam) {
-    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
-    static_assert(kWords <= kElboThreads, "one descriptor word per thread");
-    if ((int)threadIdx.x < kWords)
-      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
-          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
+  // the optimised tensors' elements this thread updates (element threadIdx.x of every slot) and
+  // their moments: loaded now, used when the gradient is written below. Lane q computes slot q's
+  // bias corrections (fp64 pow: a long dependent chain) meanwhile, into LDS.
+  float av[MI_ELBO_ADAM_SLOTS], am[MI_ELBO_ADAM_SLOTS], aq[MI_ELBO_ADAM_SLOTS];
+  __shared__ AdamCoef sco[MI_ELBO_ADAM_SLOTS];
+  __shared__ float sstep1[MI_ELBO_ADAM_SLOTS];
+#pragma unroll
+  for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
+    av[q] = am[q] = aq[q] = 0.0f;
+    if (has_adam && q < sad.num && (int64_t)threadIdx.x < sad.slots[q].numel) {
+      const mi_elbo_adam_slot& A = sad.slots[q];
+      av[q] = A.value[threadIdx.x];
+      am[q] = A.exp_avg[threadIdx.x];
+      aq[q] = A.exp_avg_sq[threadIdx.x];
+    }
+  }
+  if (has_adam && (int)threadIdx.x < sad.num) {   // (visible after block_sum's barrier below)
+    const float s1 = *sad.slots[threadIdx.x].step + 1.0f;
+    sco[threadIdx.x] = adam_coef(sad, s1);
+    sstep1[threadIdx.x] = s1;
   }
   double t = 0.0;
   double acc[kMaxTails][2] = {};
@@ -995,30 +1018,14 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
   const double total = block_sum(t, rsum + kElboThreads / kWave);
   MI_ELBO_STAMP(4);
-  // the optimised tensors' elements this thread updates (element threadIdx.x of every slot), their
-  // moments and step counts: loaded now, used when the gradient is written below
-  float av[MI_ELBO_ADAM_SLOTS], am[MI_ELBO_ADAM_SLOTS], aq[MI_ELBO_ADAM_SLOTS];
-  float as[MI_ELBO_ADAM_SLOTS];
-#pragma unroll
-  for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
-    av[q] = am[q] = aq[q] = as[q] = 0.0f;
-    if (has_adam && q < sad.num && (int64_t)threadIdx.x < sad.slots[q].numel) {
-      const mi_elbo_adam_slot& A = sad.slots[q];
-      av[q] = A.value[threadIdx.x];
-      am[q] = A.exp_avg[threadIdx.x];
-      aq[q] = A.exp_avg_sq[threadIdx.x];
-      as[q] = *A.step;
-    }
-  }
   // the Adam update of element i of the tensor behind (factor f, parameter j), gradient g
   auto adam_step = [&](int f, int j, int64_t i, float g) {
     if (!has_adam) return;
 #pragma unroll
     for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
       if (q >= sad.num || sad.slots[q].factor != f || sad.slots[q].param != j) continue;
-      const AdamCoef c = adam_coef(sad, as[q] + 1.0f);
       float pv = av[q], mv = am[q], vv = aq[q];
-      adam_update(sad, c, pv, g, mv, vv);
+      adam_update(sad, sco[q], pv, g, mv, vv);
       const mi_elbo_adam_slot& A = sad.slots[q];
       A.value[i] = pv;
       A.exp_avg[i] = mv;
@@ -1119,13 +1126,8 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     *E.step_snapshot = step0;
     *E.step_counter = step0 + 1;
   }
-  if (has_adam) {
-    __syncthreads();   // every thread has read the step counts
-    if (threadIdx.x == 0)
-#pragma unroll
-      for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q)
-        if (q < sad.num) *sad.slots[q].step = as[q] + 1.0f;
-  }
+  if (has_adam && (int)threadIdx.x < sad.num)   // (lane q alone read slot q's count)
+    *sad.slots[threadIdx.x].step = sstep1[threadIdx.x];
   MI_ELBO_STAMP(5);
   MI_ELBO_FLUSH();
 }

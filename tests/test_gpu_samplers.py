@@ -72,11 +72,13 @@ def test_gamma_sampler_matches_restatement(device, seed, step, stream_id, offset
                                          None, stream_id, offset, None, g.data_ptr(), x.data_ptr(),
                                          None), "mi_gamma_rsample")
     want, blocks = oracle_build.gamma_draws(ALPHAS, K, seed, step, stream_id, offset)
-    check_draws(g.cpu().numpy(), want)
+    got = g.cpu().numpy()
+    check_draws(got, want)
     # the comparison covers rejections (more than one block for alpha >= 1) and several blocks
     assert (blocks[:, ALPHAS >= 1] > 1).sum() > 10
     assert blocks.max() >= 3
-    np.testing.assert_array_equal(x.cpu().numpy(), np.maximum(want, np.float32(1.17549435e-38)))
+    # x = g / rate (rate 1), floored at the smallest normal float
+    np.testing.assert_array_equal(x.cpu().numpy(), np.maximum(got, np.float32(1.17549435e-38)))
 
 
 def test_gamma_sampler_device_step_counter(device):
@@ -92,8 +94,9 @@ def test_gamma_sampler_device_step_counter(device):
                                          counter.data_ptr(), 4, 0, None, g.data_ptr(), x.data_ptr(),
                                          None), "mi_gamma_rsample")
     want, _ = oracle_build.gamma_draws(ALPHAS, K, seed, 7, 4, 0)
-    check_draws(g.cpu().numpy(), want)
-    np.testing.assert_allclose(x.cpu().numpy(), np.maximum(want / 2, 1.17549435e-38), rtol=1e-7)
+    got = g.cpu().numpy()
+    check_draws(got, want)
+    np.testing.assert_array_equal(x.cpu().numpy(), np.maximum(got / np.float32(2), np.float32(1.17549435e-38)))
 
 
 C1 = np.array([0.3, 1.0, 2.5, 12.0, 0.3, 2.5, 0.05, 40.0], np.float32)
@@ -115,7 +118,8 @@ def test_beta_sampler_matches_restatement(device, seed, step, stream_id, offset)
     # x = g1 / (g1 + g0): x near 0 (alpha = 0.05) carries the relative error of g1 itself
     check_draws(got, want)
     assert (b1 > 1).sum() > 10 and (b0 > 1).sum() > 10
-    assert ((got > 0) & (got < 1)).mean() > 0.99
+    # (the 0.05 / 0.05 and 0.3 / 12 columns put many draws at exactly 0 or 1 in float32)
+    assert ((got > 0) & (got < 1)).mean() > 0.9
 
 
 def test_beta_sampler_exp_variant_matches_restatement(device):
