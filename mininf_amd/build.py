@@ -84,10 +84,13 @@ def build(force: bool = False, verbose: bool = True) -> str:
     failed = [job.args[-1] for job in jobs if job.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, f"hipcc {' '.join(failed)}")
-    command = [HIPCC, *FLAGS, "-o", TARGET, *objects, *LIBS]
+    # linked beside the target, then renamed over it: a reader never sees a half-written library
+    partial = TARGET + ".partial"
+    command = [HIPCC, *FLAGS, "-o", partial, *objects, *LIBS]
     if verbose:
         print(" ".join(command), file=sys.stderr)
     subprocess.run(command, check=True)
+    os.replace(partial, TARGET)
     return TARGET
 
 

@@ -783,6 +783,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   };
 
   if constexpr (ONESTAGE) {
+    // the draw's parameters first: their loads are in flight during the batch counter's round
+    // trip and the rows' permutation
+    if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (gen_rows) {
       // this batch's rows of the block's stage, from the batch number every block reads before
       // the last one to finish advances it (below)
@@ -800,7 +803,6 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       __syncthreads();
     }
     MI_LIN_STAMP(1);
-    if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
     if (drawn) draw_here();
     if (st0 < st1) store_stage();

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4, cycle 7: the linear launch issues its theta draw's parameter loads before the batch
+# counter read; tests of the linear paths, C4 step A/B against cycle 6, the default bench line,
+# the C4 launch's phase stamps.
+set -u
+mkdir -p gpurun_out
+run() { local t=$1; shift; local log=$1; shift; timeout -k 10 "$t" "$@" > "gpurun_out/$log" 2>&1; local rc=$?; echo "$log rc=$rc"; return $rc; }
+T="python -u -m pytest -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider"
+run 400 c7_lin.log $T -x tests/test_gpu_linear_draw.py tests/test_gpu_minibatch.py tests/test_gpu_linear_elbo.py tests/test_gpu_fused_step.py "tests/test_gpu_fullsize.py::test_c4_full_size_bench_configuration" || exit 1
+B="python -u bench.py --no-cpu-baseline --no-other-configs --steps 48 --warmup 8"
+run 100 c7_c4_a.log $B --config c4 || exit 1
+run 100 c7_c4_b.log $B --config c4 || exit 1
+run 150 c7_lin_c4.log python -u tools/linear_timing.py bench c4 || exit 1
+run 400 c7_bench.log python -u bench.py || exit 1
+exit 0
