@@ -727,15 +727,17 @@ def main():
                      0.0 if args.no_cpu_baseline else 12.0)
     others = ()
     if args.config == "c2" and not args.no_other_configs:
-        # the other configurations of BASELINE.json, measured in the same run (shorter: 10
-        # graph-replayed steps each; CPU baseline only for C3 at N = 1): C3 is a one-GPU config;
+        # the other configurations of BASELINE.json, measured in the same run (the same number
+        # of graph-replayed steps -- with 10 the fixed cost of the timed region's barriers and
+        # synchronisations added 5-9 us to C4's 40 us step; CPU baseline only for C3 at
+        # N = 1): C3 is a one-GPU config;
         # C4 (particle-sharded, 32 particles per GPU: 256 at N = 8) and C5 (data-sharded, all
         # 1024 particles on each rank's element slice) are the multi-GPU ones
         others = ("c3", "c4", "c5") if world == 1 and group is None else ("c4", "c5")
     if others:
         out["other_configs"] = {}
         for name in others:
-            sub = run_config(name, args, world, rank, device, group, min(args.steps, 10), 3,
+            sub = run_config(name, args, world, rank, device, group, args.steps, 3,
                              0.0 if (args.no_cpu_baseline or name != "c3") else 8.0)
             out["other_configs"][name] = {key: sub[key] for key in (
                 "value", "unit", "ms_per_step", "scaling", "config", "roofline", "cpu_baseline")

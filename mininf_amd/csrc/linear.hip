@@ -783,13 +783,15 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   };
 
   if constexpr (ONESTAGE) {
-    // the draw's parameters first: their loads are in flight during the batch counter's round
-    // trip and the rows' permutation
+    // the batch counter first, then the draw's parameters: loads complete in order, so the
+    // counter's use waits for it alone while the parameters stay in flight behind it (issued
+    // first, they held up the counter's round trip: measured no gain)
+    if (gen_rows)
+      batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (gen_rows) {
       // this batch's rows of the block's stage, from the batch number every block reads before
       // the last one to finish advances it (below)
-      batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tid < S::CH && st0 < st1) {
         const int64_t row = st0 * S::CH + tid;
         int32_t r = 0;
