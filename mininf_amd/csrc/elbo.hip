@@ -1093,6 +1093,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       __syncthreads();
     }
   }
+  MI_ELBO_STAMP(6);
   if (!ABSORB && R.nt_job >= 0 && (E.options & MI_ELBO_FINAL_GRADS)) {
     // the Normal tail's gradients for an upstream of 1: its blocks' sums in a fixed order, then
     // what k_elbo_backward's absorbed blocks write (u * s + w * dH, the exp chain rule)
@@ -1115,6 +1116,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       }
     }
   }
+  MI_ELBO_STAMP(7);
   static_assert(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan) + 4 * sizeof(void*) <= 4096,
                 "k_elbo_forward's arguments exceed 4 KiB");
   static_assert(kGroupCounterWord + kGroupCounters * kGroupCounterStride <=

@@ -783,15 +783,11 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   };
 
   if constexpr (ONESTAGE) {
-    // the batch counter first, then the draw's parameters: loads complete in order, so the
-    // counter's use waits for it alone while the parameters stay in flight behind it (issued
-    // first, they held up the counter's round trip: measured no gain)
-    if (gen_rows)
-      batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (gen_rows) {
       // this batch's rows of the block's stage, from the batch number every block reads before
-      // the last one to finish advances it (below)
+      // the last one to finish advances it (below). (Issuing the draw's parameter loads before
+      // or right after this read measured no faster: tools/linear_timing.py, round 4.)
+      batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tid < S::CH && st0 < st1) {
         const int64_t row = st0 * S::CH + tid;
         int32_t r = 0;
@@ -805,6 +801,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       __syncthreads();
     }
     MI_LIN_STAMP(1);
+    if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
     if (drawn) draw_here();
     if (st0 < st1) store_stage();

@@ -7,7 +7,8 @@ build of the library with -DMI_ELBO_TIMING=1, over eager steps of a bench config
 
 Stamps per block (thread 0): 0 entry, 1 the block's own work done (reduction or lead terms),
 2 tail partials and the block sum, 3 the completion count (the last block known); the last block
-only: 4 final loads and the loss sum, 5 end.
+only: 4 final loads and the loss sum, 6 the Beta tails (with their Adam updates), 7 the Normal
+tail (with its Adam updates), 5 end (flag mirror, generator and optimizer step counts).
 """
 import ctypes
 import os
@@ -62,7 +63,8 @@ def run(config="c2"):
               f"work {np.mean(rows[:, 1] - rows[:, 0]):.2f} (max {np.max(rows[:, 1] - rows[:, 0]):.2f})  "
               f"sum {np.mean(rows[:, 2] - rows[:, 1]):.2f}  count {np.mean(rows[:, 3] - rows[:, 2]):.2f} "
               f"(max {np.max(rows[:, 3] - rows[:, 2]):.2f})  last block: starts {last[0, 3] - base:.2f}, "
-              f"loads+sum {last[0, 4] - last[0, 3]:.2f}, rest {last[0, 5] - last[0, 4]:.2f}, "
+              f"loads+sum {last[0, 4] - last[0, 3]:.2f}, tails {last[0, 6] - last[0, 4]:.2f}, "
+              f"normal tail {last[0, 7] - last[0, 6]:.2f}, mirror+step {last[0, 5] - last[0, 7]:.2f}, "
               f"end {last[0, 5] - base:.2f} us", flush=True)
 
 
