@@ -569,7 +569,11 @@ struct ReducePlan {
   // linearity, into its own partial (nt_nkb = the reducing blocks, indexed by block).
   int nt_single;
   int nt_mask[MI_MAX_REDUCE];
+  // offset (doubles) of what block 0 computes early for the last block (early_tail): per tail the
+  // three trigammas of its entropy derivatives, then per optimizer slot (s1, bias corrections)
+  int64_t early;
 };
+constexpr int kEarlyDoubles = 3 * kMaxTails + 2 * MI_ELBO_ADAM_SLOTS;
 
 // Fields of factor f of the launch, by constant-index selects (see ReducePlan.tail_factor).
 MI_DEV float* factor_grad(const mi_elbo& E, int f, int j) {
@@ -661,7 +665,8 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
     double acc = 0.0;
     int64_t g = gl;
     // sixteen loads in flight per lane (a C2-sized list, ~250 segments over 8 groups, is two
-    // rounds of memory latency instead of four)
+    // rounds of memory latency instead of four), the last round padded with clamped loads whose
+    // values are dropped: a remainder loop waited one round trip per segment
     for (; g + 15 * kRedG < J.nseg; g += 16 * kRedG) {
       float x[16];
 #pragma unroll
@@ -669,15 +674,16 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc += (double)x[j];
     }
-    if (g + 7 * kRedG < J.nseg) {
-      float x[8];
+    if (g < J.nseg) {
+      float x[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = p[(g + j * kRedG) * stride];
+      for (int j = 0; j < 16; ++j) {
+        const int64_t gj = g + j * kRedG;
+        x[j] = keep_if(p[(gj < J.nseg ? gj : J.nseg - 1) * stride], gj < J.nseg);
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += (double)x[j];
-      g += 8 * kRedG;
+      for (int j = 0; j < 16; ++j) acc += (double)x[j];
     }
-    for (; g < J.nseg; g += kRedG) acc += (double)p[g * stride];
     __syncthreads();
     lds[gl * kRedK + kl] = acc;
     __syncthreads();
@@ -761,6 +767,39 @@ __device__ unsigned long long* mi_elbo_tbuf;
 #define MI_ELBO_FLUSH() do { } while (0)
 #endif
 
+// ---- what the last block needs that is known at the launch's start ---------------------------
+// Block 0 computes, while its own reduction's loads are in flight, the values the last block's
+// tail would otherwise compute on its critical path: the trigammas of each Beta tail's entropy
+// derivatives (the concentrations are written by the launch before) and each optimizer slot's
+// bias corrections (two fp64 pow per tensor). Device-coherent stores, complete before block 0's
+// completion count, so the last block reads them with its first loads.
+MI_DEV void early_tail(const mi_elbo& E, const ReducePlan& R, const mi_elbo_adam* __restrict__ adam,
+                       double* __restrict__ work) {
+  const int t = threadIdx.x;
+  double* out = work + R.early;
+  if (t < 3 * kMaxTails) {
+    const int q = t / 3, which = t % 3;
+    if (q < R.tails) {
+      const float a = *pick(R.tail_c1, q), b = *pick(R.tail_c0, q);
+      const float x = which == 0 ? a + b : which == 1 ? a : b;
+      __hip_atomic_store(out + t, (double)trigammaf(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (adam != nullptr && t >= kWave && t < kWave + MI_ELBO_ADAM_SLOTS) {
+    const int q = t - kWave;
+    if (q < adam->num) {
+      const float s1 = *adam->slots[q].step + 1.0f;
+      const AdamCoef c = adam_coef(*adam, s1);
+      // (s1, bc1) and (bc2_sqrt, step_size) as two doubles of float pairs
+      const float v[4] = {s1, c.bc1, c.bc2_sqrt, c.step_size};
+      double d[2];
+      __builtin_memcpy(d, v, sizeof(d));
+      double* o = out + 3 * kMaxTails + 2 * q;
+      __hip_atomic_store(o, d[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 1, d[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ---- forward --------------------------------------------------------------------------------
 // HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
 // of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
@@ -794,6 +833,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
     return;
   }
+  if (!ABSORB && blockIdx.x == 0 && (R.tails > 0 || adam != nullptr)) early_tail(E, R, adam, work);
   double* rsum = &red[0][0];
   double share;
   double c[kMaxTails][2] = {};   // this lane's tail contributions
@@ -970,11 +1010,20 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       aq[q] = A.exp_avg_sq[threadIdx.x];
     }
   }
-  if (has_adam && (int)threadIdx.x < sad.num) {   // (visible after block_sum's barrier below)
-    const float s1 = *sad.slots[threadIdx.x].step + 1.0f;
-    sco[threadIdx.x] = adam_coef(sad, s1);
-    sstep1[threadIdx.x] = s1;
+  if (has_adam && (int)threadIdx.x < sad.num) {   // block 0's (visible after block_sum's barrier)
+    const double* o = work + R.early + 3 * kMaxTails + 2 * threadIdx.x;
+    const double d[2] = {__hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __hip_atomic_load(o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+    float v[4];
+    __builtin_memcpy(v, d, sizeof(v));
+    sstep1[threadIdx.x] = v[0];
+    sco[threadIdx.x] = AdamCoef{v[1], v[2], v[3]};
   }
+  // block 0's trigammas of the Beta tails (lane 3 q + which), loaded with the shares
+  float tg_early = 0.0f;
+  if (!ABSORB && (int)threadIdx.x < 3 * R.tails)
+    tg_early = (float)__hip_atomic_load(work + R.early + threadIdx.x, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
   double t = 0.0;
   double acc[kMaxTails][2] = {};
   for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
@@ -1044,19 +1093,18 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       // entropy derivatives on lanes 0-2 meanwhile
       const float a = tc1[q], b = tc0[q];
       const float tsum = a + b;
-      const float tg = threadIdx.x == 0 ? trigammaf(tsum)
-                       : threadIdx.x == 1 ? trigammaf(a)
-                       : threadIdx.x == 2 ? trigammaf(b) : 0.0f;
+      // the trigammas of (a + b, a, b): block 0's (early_tail), on lanes 3 q .. 3 q + 2
+      __shared__ float tg_all[3 * kMaxTails];
+      if ((int)threadIdx.x < 3 * R.tails) tg_all[threadIdx.x] = tg_early;
       // wave sums, then the waves in order (fixed order, one barrier)
       const double w0 = wave_sum(acc[q][0]), w1 = wave_sum(acc[q][1]);
       __shared__ double tws[2][kElboThreads / kWave];
-      __shared__ float tgs[3];
+      const float* tgs = tg_all + 3 * q;
       const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
       if (lane == 0) {
         tws[0][wave] = w0;
         tws[1][wave] = w1;
       }
-      if (threadIdx.x < 3) tgs[threadIdx.x] = tg;
       __syncthreads();
       if (threadIdx.x == 0) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
         double s0 = 0.0, s1 = 0.0;
@@ -1496,6 +1544,8 @@ Layout make_layout(const mi_elbo* e) {
   doubles += (int64_t)L.red.tails * nshare * 2;
   L.red.nt_part = doubles;
   if (L.red.nt_job >= 0) doubles += e->factors[0].n * (int64_t)L.red.nt_nkb * 2;
+  L.red.early = doubles;
+  doubles += mi::kEarlyDoubles;
   int blocks = 0;
   for (int f = 0; f < e->num_factors; ++f)
     if (forward_absorbed(e->factors[f]) && !deferred)
