@@ -1052,16 +1052,43 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                       (int64_t)threadIdx.x < E.factors[0].n;
   double nt_s0 = 0.0, nt_s1 = 0.0;
   float nt_p0 = 1.0f, nt_p1 = 1.0f;
+  // the one-element tail (nt_single: one partial per reducing block, hundreds of them) is summed by
+  // every lane over a strided subset, then in a fixed order through LDS: a single lane's loop over
+  // the blocks was a long chain at the end of the launch
+  const bool nt_wide = !ABSORB && R.nt_job >= 0 && R.nt_single &&
+                       (E.options & MI_ELBO_FINAL_GRADS);
   if (nt_fin) {
     const mi_factor& F = E.factors[0];
     const int64_t i = threadIdx.x;
     nt_p0 = F.param[0][i * F.stride[0]];
     nt_p1 = F.param[1][i * F.stride[1]];
-    for (int kb = 0; kb < R.nt_nkb; ++kb) {
-      const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
-      nt_s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      nt_s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!nt_wide)
+      for (int kb = 0; kb < R.nt_nkb; ++kb) {
+        const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
+        nt_s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nt_s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  }
+  if (nt_wide) {   // (element 0 of factor 0; the whole block, uniform branch)
+    double q0 = 0.0, q1 = 0.0;
+    for (int kb = threadIdx.x; kb < R.nt_nkb; kb += kElboThreads) {
+      const double* w2 = &work[R.nt_part + (int64_t)kb * 2];
+      q0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    q0 = wave_sum(q0);
+    q1 = wave_sum(q1);
+    __shared__ double ntw[2][kElboThreads / kWave];
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      ntw[0][threadIdx.x / kWave] = q0;
+      ntw[1][threadIdx.x / kWave] = q1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int w = 0; w < kElboThreads / kWave; ++w) {
+        nt_s0 += ntw[0][w];
+        nt_s1 += ntw[1][w];
+      }
   }
   const uint32_t fw0 = (int64_t)threadIdx.x < E.nflags ? E.flags[threadIdx.x] : 0u;
   const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
