@@ -867,7 +867,17 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
           // 16-byte loads, all issued before the logs
           const int64_t nq = F.n >> 2;
           const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
-          for (int64_t q = first; q < nq; q += stride) {
+          int64_t q = first;
+          // four quads' loads in flight per round (a lead block covers ~16 elements per lane)
+          for (; q + 3 * stride < nq; q += 4 * stride) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sq[q + u * stride];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
+          }
+          for (; q < nq; q += stride) {
             const float4 v = sq[q];
             hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
           }
@@ -1454,7 +1464,12 @@ int env_kred() {
 
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
-  L.fwd.lead_blocks = (int)blocks_for(std::max(e->K, longest_factor(e)), mi::kElboMaxBlocks);
+  // about sixteen elements per lane of the longest term or factor (a lane's quads loaded four at
+  // a time): C5's 1e6-element scale entropy in 245 lead blocks instead of 977 -- the launch's
+  // 223-VGPR blocks fit two per CU, so a larger grid runs in several rounds
+  L.fwd.lead_blocks = (int)std::max<int64_t>(
+      1, std::min<int64_t>(mi::kElboMaxBlocks,
+                           ceil_div(std::max(e->K, longest_factor(e)), 16 * mi::kElboThreads)));
   int64_t longest = 1;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind == MI_DRAW_NONE) longest = std::max(longest, e->factors[f].n);
