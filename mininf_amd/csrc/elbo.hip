@@ -1462,6 +1462,15 @@ int env_kred() {
   return v;
 }
 
+int env_lead() {
+  static const int v = [] {
+    const char* e = getenv("MININF_AMD_ELBO_LEAD");
+    const int n = e != nullptr ? atoi(e) : 16;
+    return (n == 4 || n == 8 || n == 16 || n == 32) ? n : 16;
+  }();
+  return v;
+}
+
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
   // about sixteen elements per lane of the longest term or factor (a lane's quads loaded four at
@@ -1469,7 +1478,7 @@ Layout make_layout(const mi_elbo* e) {
   // 223-VGPR blocks fit two per CU, so a larger grid runs in several rounds
   L.fwd.lead_blocks = (int)std::max<int64_t>(
       1, std::min<int64_t>(mi::kElboMaxBlocks,
-                           ceil_div(std::max(e->K, longest_factor(e)), 16 * mi::kElboThreads)));
+                           ceil_div(std::max(e->K, longest_factor(e)), env_lead() * mi::kElboThreads)));
   int64_t longest = 1;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind == MI_DRAW_NONE) longest = std::max(longest, e->factors[f].n);
