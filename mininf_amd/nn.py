@@ -142,10 +142,12 @@ class ParameterizedDistribution(nn.Module):
         if not (u1.is_cuda and u1.dtype == torch.float32 and u0.dtype == torch.float32 and
                 u1.device == u0.device and u1.shape == u0.shape):
             return None
-        conc = _ExpStackFn.apply(u1, u0)
         validate = self.distribution_constants.get("validate_args")
         if validate is None:
             validate = distributions.Distribution._validate_args
+        # validated: the check below reads the array at once, so the transform is launched here
+        # instead of being left to the draw
+        conc = _ExpStackFn.apply(u1, u0, not validate)
         beta = distributions.Beta.__new__(distributions.Beta)
         beta._dirichlet = distributions.Dirichlet(conc, validate_args=False)
         distributions.Distribution.__init__(beta, beta._dirichlet._batch_shape,
@@ -230,7 +232,8 @@ class _ExpFn(torch.autograd.Function):
 class _ExpStackFn(torch.autograd.Function):
     """``torch.stack([exp(u1), exp(u0)], -1)`` in one launch (``mi_transform_params``)."""
     @staticmethod
-    def forward(ctx, u1: torch.Tensor, u0: torch.Tensor):  # type: ignore[override]
+    def forward(ctx, u1: torch.Tensor, u0: torch.Tensor,  # type: ignore[override]
+                defer: bool = True):
         out = torch.empty(tuple(u1.shape) + (2,), dtype=torch.float32, device=u1.device)
         P = _native.Params()
         P.m, P.n = 2, max(1, u1.numel())
@@ -240,7 +243,7 @@ class _ExpStackFn(torch.autograd.Function):
             P.stride[j] = flat.stride(0) if u.numel() > 1 else 0
             P.transform[j] = _native.TRANSFORM_EXP
         ctx.save_for_backward(out)
-        if _defer_exp() and u1.is_contiguous() and u0.is_contiguous():
+        if defer and _defer_exp() and u1.is_contiguous() and u0.is_contiguous():
             # the guide's draw computes and writes the array (mi_beta_rsample_exp); any earlier
             # reader launches the transform itself (guide.PendingConcentration). Only for
             # contiguous parameters: P then points into their own storage, not into a reshape
@@ -255,7 +258,7 @@ class _ExpStackFn(torch.autograd.Function):
     def backward(ctx, grad: torch.Tensor):  # type: ignore[override]
         (out,) = ctx.saved_tensors
         d = grad * out   # d exp(u) / du = exp(u)
-        return d[..., 0], d[..., 1]
+        return d[..., 0], d[..., 1], None
 
 
 class FactorizedDistribution(DistributionDict):

@@ -65,6 +65,17 @@ class Adam(torch.optim.Optimizer):
             return type(self).step.__wrapped__(self, closure) \
                 if hasattr(type(self).step, "__wrapped__") else type(self).step(self, closure)
 
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """``Optimizer.zero_grad``: with ``set_to_none`` (the default) every gradient is dropped
+        here directly -- torch's version runs behind a dynamo-disable wrapper and a profiler range,
+        tens of microseconds of Python per eager step for the same effect."""
+        if not set_to_none:
+            return super().zero_grad(set_to_none=False)
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    p.grad = None
+
     def _counter_words(self, device: torch.device) -> torch.Tensor:
         words = self._counters.get(device)
         if words is None:
