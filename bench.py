@@ -502,13 +502,19 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         eager_step()
     wait_device(device)
     arm(f"{config}: timed eager steps")
-    timer.active = True
     eager_steps = max(3, steps // 3) if args.graph else steps
     gc_clock = _GcClock()
     with gc_clock:
         eager_elapsed, loss = timed(eager_step, eager_steps)
-    timer.active = False
     eager_ms = 1e3 * eager_elapsed / eager_steps
+    wait_device(device)
+    # the kernel durations (roofline) from further eager steps with a HIP event pair around each
+    # launch, outside the eager timing (the events cost host time per launch)
+    arm(f"{config}: kernel-timed eager steps")
+    timer.active = True
+    for _ in range(eager_steps):
+        eager_step()
+    timer.active = False
     wait_device(device)
     elapsed, mode = eager_elapsed * steps / eager_steps, "eager"
     if args.graph:

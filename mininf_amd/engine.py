@@ -20,6 +20,7 @@ from __future__ import annotations
 import collections
 import ctypes
 import dataclasses
+import functools
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -121,8 +122,9 @@ class _View:
     constant: Optional[float] = None  # host scalar (e.g. the 2.0 of `Beta(2, 2)`): no operand
     draw: Optional[guide.LazyDraw] = None  # a guide draw computed inside the kernel (mi_draw)
 
-    @property
+    @functools.cached_property
     def key(self) -> Tuple:
+        """Identity of the operand (views are not modified after construction: computed once)."""
         if self.constant is not None:
             return ("constant", self.constant)
         if self.draw is not None:

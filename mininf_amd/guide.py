@@ -544,6 +544,8 @@ def _side_stream(device: torch.device) -> torch.cuda.Stream:
 
 def join_side() -> None:
     """Make the current stream wait for the side-stream work of the last draws."""
+    if not _PENDING:
+        return
     current = torch.cuda.current_stream()
     for event in _PENDING:
         current.wait_event(event)

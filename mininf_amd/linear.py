@@ -162,8 +162,10 @@ class DeferredMatmul(TorchFunctionMode):
             X, theta = args
             info = Deferred(X=X, theta=theta, shape=torch.Size([X.shape[0]]))
             return self._placeholder(theta, info.shape, info)
-        if not self.deferred and not _guide._LAZY and not _guide._PENDING_DRAWS:
-            return func(*args, **kwargs)   # no placeholder exists: nothing to look for
+        if not self.deferred and not _guide._LAZY and \
+                (not _guide._PENDING_DRAWS or func in _METADATA or func in _BROADCASTS):
+            # no placeholder exists, and no pending draw is read by this call: nothing to do
+            return func(*args, **kwargs)
         touched = []
         lazy = []
         for x in _leaves(args, kwargs):

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import struct
 from typing import Callable, cast, Dict, Optional, Set, Type
 
 import torch
@@ -193,6 +194,12 @@ def _construct(cls, arguments: Dict, constants: Dict) -> distributions.Distribut
             cls(**arguments, **plain, validate_args=True)   # raises torch's error
     distribution._validate_args = True
     return distribution
+
+
+def _float32(value: float) -> float:
+    """``value`` rounded to float32 (as ``float(torch.tensor(value, dtype=torch.float32))``,
+    without creating a tensor)."""
+    return struct.unpack("f", struct.pack("f", value))[0]
 
 
 def _defer_exp() -> bool:
@@ -531,7 +538,7 @@ class EvidenceLowerBoundLoss(nn.Module):
                                 f"but got a sample of type {type(samples)}")
             trace = particles.trace_particles(model, samples, K, validate=self.validate)
         # d loss / d T_k = -1 / K exactly (fp32), matching the `mul(-1/K)` below.
-        g0 = float(torch.tensor(-1.0 / self.num_particles, dtype=torch.float32))
+        g0 = _float32(-1.0 / self.num_particles)
         device = next((t.device for t in samples.values() if isinstance(t, torch.Tensor)),
                       torch.device("cuda", torch.cuda.current_device()))
         shared = set(self.data_shard.shared) if self.data_shard is not None else None

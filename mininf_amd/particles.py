@@ -49,6 +49,21 @@ def is_batched(tensor: Any) -> bool:
     return isinstance(tensor, torch.Tensor) and _functorch.is_batchedtensor(tensor)
 
 
+def broadcast_shapes(*shapes: Tuple[int, ...]) -> Tuple[int, ...]:
+    """``torch.broadcast_shapes`` of plain shape tuples in a few Python operations (torch's version
+    goes through its reference implementation: several microseconds per site and trace); a
+    mismatch is handed to torch, which raises its own error."""
+    ndim = max((len(s) for s in shapes), default=0)
+    out = [1] * ndim
+    for s in shapes:
+        for i, d in enumerate(s, ndim - len(s)):
+            if d != 1:
+                if out[i] != 1 and out[i] != d:
+                    return tuple(torch.broadcast_shapes(*shapes))
+                out[i] = d
+    return tuple(out)
+
+
 def vmap_tensors(fn: Callable, args: Sequence[torch.Tensor]) -> Tuple[torch.Tensor, ...]:
     """
     ``torch.func.vmap(fn, randomness="different")(*args)`` for positional tensor arguments batched
@@ -406,9 +421,9 @@ class ParticleTracer(TracerMixin):
             # (integer_interval's `value % 1 == 0`, constraints.py) are checked here (memoised).
             self._check_support(name, value, distribution, cast(Constraint, distribution.support))
         if family == "categorical":
-            shape = torch.broadcast_shapes(tuple(data.shape), distribution.batch_shape)
+            shape = broadcast_shapes(tuple(data.shape), tuple(distribution.batch_shape))
         elif family != "torch":
-            shape = torch.broadcast_shapes(tuple(data.shape), *[tuple(p.shape) for p in params])
+            shape = broadcast_shapes(tuple(data.shape), *[tuple(p.shape) for p in params])
         else:
             shape = torch.Size(tuple(data.shape)[:data.dim() - len(distribution.event_shape)])
         shape = torch.Size(shape)

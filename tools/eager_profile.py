@@ -47,6 +47,10 @@ def main():
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats(key).print_stats(70)
         print(buf.getvalue(), flush=True)
+    for pattern in filter(None, os.environ.get("CALLEES", "").split(",")):
+        buf = io.StringIO()   # what the named functions spend their time in
+        pstats.Stats(prof, stream=buf).sort_stats("cumtime").print_callees(pattern)
+        print(buf.getvalue(), flush=True)
 
 
 if __name__ == "__main__":
