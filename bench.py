@@ -492,6 +492,18 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
             seconds = float(t)
         return seconds, out
 
+    def warm_replays(replay, count):
+        """`count` replays, then more in blocks until the device has run them for --warm-ms: the
+        timed replays start with the clocks and caches at their steady state."""
+        t0 = time.perf_counter()
+        for _ in range(count):
+            replay()
+        wait_device(device)
+        while 1e3 * (time.perf_counter() - t0) < args.warm_ms:
+            for _ in range(8):
+                replay()
+            wait_device(device)
+
     def eager_step():
         # detached: keep no autograd graph alive across steps (graph capture needs it)
         return full_step().detach()
@@ -545,9 +557,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 return bucket.loss()
 
         arm(f"{config}: graph warm-up replays")
-        for _ in range(max(1, warmup // repeat)):
-            graph_step()
-        wait_device(device)
+        warm_replays(graph_step, max(1, warmup // repeat))
         arm(f"{config}: timed graph replays ({steps // repeat} replays of {repeat} steps)")
         elapsed, loss = timed(graph_step, steps // repeat)
         captured.check()
@@ -563,8 +573,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
             arm(f"{config}: reducible-floor graph")
             try:
                 floor_graph = StepGraph(forward_backward, warmup=2, repeat=repeat)
-                for _ in range(max(1, warmup // repeat)):
-                    floor_graph()
+                warm_replays(floor_graph, max(1, warmup // repeat))
                 floor_s, _ = timed(floor_graph, steps // repeat)
                 floor_graph.check()
                 floor_ms = 1e3 * floor_s / steps
@@ -652,8 +661,10 @@ def main():
     ap.add_argument("--graph-repeat", type=int, default=0,
                     help="steps captured per graph replay at N = 1 (0: the largest of 8, 6, 5, 4, 3, 2, 1 that "
                          "divides --steps)")
-    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--warm-ms", type=float, default=50.0,
+                    help="graph warm-up: replay until the device has run this long (ms)")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--eager", dest="graph", action="store_false",
