@@ -100,6 +100,9 @@ class ParameterizedDistribution(nn.Module):
         if fused is not None:
             return fused
         constraints = cast(Dict, self.distribution_cls.arg_constraints)
+        validate = self.distribution_constants.get("validate_args")
+        if validate is None:
+            validate = distributions.Distribution._validate_args
         arguments = {}
         sources = {}
         for name, unconstrained in self.distribution_parameters.items():
@@ -113,7 +116,9 @@ class ParameterizedDistribution(nn.Module):
                 forward = _forward_transform(transform)
                 if isinstance(forward, distributions.ExpTransform) and unconstrained.is_cuda and \
                         unconstrained.dtype == torch.float32:
-                    arguments[name] = _ExpFn.apply(unconstrained)   # one mi_transform_params
+                    # one mi_transform_params; left to the draw unless the argument check
+                    # below reads it at once
+                    arguments[name] = _ExpFn.apply(unconstrained, not validate)
                 else:
                     arguments[name] = forward(unconstrained)
                 if isinstance(forward, distributions.ExpTransform):
@@ -156,7 +161,7 @@ class ParameterizedDistribution(nn.Module):
         if validate:
             # Dirichlet's and Beta's three argument checks are all `conc > 0` elementwise: one
             # host synchronisation instead of three; torch raises its own error on failure
-            if not torch._is_all_true((conc > 0).all()):
+            if not torch._is_all_true(conc > 0):   # (it reduces the mask itself)
                 distributions.Beta(conc[..., 0], conc[..., 1], validate_args=True)
             beta._validate_args = beta._dirichlet._validate_args = True
         beta._mininf_amd_sources = {  # type: ignore[attr-defined]
@@ -187,9 +192,10 @@ def _construct(cls, arguments: Dict, constants: Dict) -> distributions.Distribut
     for param, constraint in distribution.arg_constraints.items():
         if distributions.constraints.is_dependent(constraint) or param not in distribution.__dict__:
             continue
-        checks.append(constraint.check(getattr(distribution, param)).all())
+        checks.append(constraint.check(getattr(distribution, param)).reshape(-1))
     if checks:
-        ok = checks[0] if len(checks) == 1 else torch.stack(checks).all()
+        # one reduction of every parameter's mask (torch._is_all_true reduces it itself)
+        ok = checks[0] if len(checks) == 1 else torch.cat(checks)
         if not torch._is_all_true(ok):
             cls(**arguments, **plain, validate_args=True)   # raises torch's error
     distribution._validate_args = True
@@ -211,7 +217,7 @@ class _ExpFn(torch.autograd.Function):
     """``exp(u)`` of a positive-constrained guide parameter (``transform_to(positive)``,
     nn.py:91-96) as one ``mi_transform_params`` launch."""
     @staticmethod
-    def forward(ctx, u: torch.Tensor):  # type: ignore[override]
+    def forward(ctx, u: torch.Tensor, defer: bool = True):  # type: ignore[override]
         out = torch.empty(u.shape, dtype=torch.float32, device=u.device)
         ctx.save_for_backward(out)
         if u.numel() > 0:
@@ -221,7 +227,7 @@ class _ExpFn(torch.autograd.Function):
             P.u[0] = flat.data_ptr()
             P.stride[0] = flat.stride(0) if flat.numel() > 1 else 0
             P.transform[0] = _native.TRANSFORM_EXP
-            if _defer_exp() and u.is_contiguous():
+            if defer and _defer_exp() and u.is_contiguous():
                 # the guide's draw computes and writes the scale (mi_normal_rsample_exp); any
                 # earlier reader launches the transform itself (guide.PendingConcentration)
                 return guide.defer_exp(out.as_subclass(guide.PendingConcentration), u, None, P)
@@ -233,7 +239,7 @@ class _ExpFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad: torch.Tensor):  # type: ignore[override]
         (out,) = ctx.saved_tensors
-        return grad * out   # d exp(u) / du = exp(u)
+        return grad * out, None   # d exp(u) / du = exp(u)
 
 
 class _ExpStackFn(torch.autograd.Function):
