@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -493,16 +494,26 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         return seconds, out
 
     def warm_replays(replay, count):
-        """`count` replays, then more in blocks until the device has run them for --warm-ms: the
-        timed replays start with the clocks and caches at their steady state."""
+        """`count` replays, then as many more as fill --warm-ms at the measured replay time: the
+        timed replays start with the clocks and caches at their steady state. Every rank runs the
+        same number (the slowest rank's replay time): a sharded replay holds a collective."""
         t0 = time.perf_counter()
         for _ in range(count):
             replay()
-        wait_device(device)
-        while 1e3 * (time.perf_counter() - t0) < args.warm_ms:
-            for _ in range(8):
-                replay()
-            wait_device(device)
+        barrier()
+        per = (time.perf_counter() - t0) / count
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([per], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            per = float(t)
+        extra = 0 if args.warm_ms <= 0 else \
+            min(10000, max(0, math.ceil((args.warm_ms / 1e3 - per * count) / per)))
+        for i in range(extra):
+            replay()
+            if i % 8 == 7:
+                wait_device(device)
+        barrier()
 
     def eager_step():
         # detached: keep no autograd graph alive across steps (graph capture needs it)

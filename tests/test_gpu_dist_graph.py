@@ -50,7 +50,7 @@ def _bench(*argv):
 
 def test_bench_two_gloo_ranks_match_one_rank(device):
     common = ["--config", "c4", "--steps", "4", "--warmup", "2", "--graph-repeat", "1",
-              "--no-other-configs", "--no-cpu-baseline"]
+              "--warm-ms", "0", "--no-other-configs", "--no-cpu-baseline"]
     two = _last_json(_bench("--gpus", "2", "--dist-backend", "gloo", "--particles-per-gpu", "32",
                             *common))
     one = _last_json(_bench("--particles-per-gpu", "64", *common))
@@ -65,7 +65,7 @@ def test_bench_two_gloo_ranks_match_one_rank_c5_data_sharded(device):
     gradients and the loss all-reduced) against one rank over all elements: the same final loss
     within 1e-5 after the same steps ("Next round" 2)."""
     common = ["--config", "c5", "--shard", "data", "--steps", "4", "--warmup", "2",
-              "--graph-repeat", "1", "--no-other-configs", "--no-cpu-baseline"]
+              "--graph-repeat", "1", "--warm-ms", "0", "--no-other-configs", "--no-cpu-baseline"]
     two = _last_json(_bench("--gpus", "2", "--dist-backend", "gloo", *common))
     one = _last_json(_bench(*common))
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
@@ -79,7 +79,7 @@ def test_bench_n2_default_run_measures_c4_and_c5(device):
     """`bench.py --gpus 2` (default C2 line) also measures C4 and C5 under other_configs, each
     entry carrying its rank count and layout."""
     line = _last_json(_bench("--gpus", "2", "--dist-backend", "gloo", "--steps", "4", "--warmup",
-                             "2", "--graph-repeat", "1", "--no-cpu-baseline"))
+                             "2", "--graph-repeat", "1", "--warm-ms", "0", "--no-cpu-baseline"))
     assert line["n_gpus"] == 2 and line["config"]["ranks"] == 2
     others = line["other_configs"]
     assert sorted(others) == ["c4", "c5"]
