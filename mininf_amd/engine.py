@@ -61,6 +61,9 @@ def _collapse(t: torch.Tensor, K: int, shape: torch.Size) -> "_View":
     if int(torch.Size(R).numel()) == 1:
         base = t.reshape(K, 1)
         return _View(base, base.stride(0), 0)
+    if R == tuple(shape):   # already [K, *shape]: no broadcast view needed
+        flat = t if len(R) == 1 else t.reshape(K, N)
+        return _View(flat, flat.stride(0), flat.stride(1) if N > 1 else 1)
     full = t.reshape((K,) + (1,) * (len(shape) - len(R)) + R).expand((K,) + tuple(shape))
     flat = full.reshape(K, N)
     return _View(flat, flat.stride(0), flat.stride(1) if N > 1 else 1)
