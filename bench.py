@@ -531,14 +531,20 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         eager_elapsed, loss = timed(eager_step, eager_steps)
     eager_ms = 1e3 * eager_elapsed / eager_steps
     wait_device(device)
-    # the kernel durations (roofline) from further eager steps with a HIP event pair around each
-    # launch, outside the eager timing (the events cost host time per launch)
-    arm(f"{config}: kernel-timed eager steps")
-    timer.active = True
-    for _ in range(eager_steps):
-        eager_step()
-    timer.active = False
-    wait_device(device)
+
+    def kernel_timed_steps():
+        """The kernel durations (roofline) from further eager steps with a HIP event pair around
+        the dominant launch, outside every timed region (the events cost host time per launch);
+        in graph mode after the replays, with the device at its steady clocks."""
+        arm(f"{config}: kernel-timed eager steps")
+        timer.active = True
+        for _ in range(eager_steps):
+            eager_step()
+        timer.active = False
+        wait_device(device)
+
+    if not args.graph:
+        kernel_timed_steps()
     elapsed, mode = eager_elapsed * steps / eager_steps, "eager"
     if args.graph:
         # The same step captured once into a hipGraph and replayed (mininf_amd.graph.StepGraph).
@@ -590,6 +596,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 floor_ms = 1e3 * floor_s / steps
             finally:
                 del os.environ["MININF_AMD_BCAST_SUFFSTAT"]
+        kernel_timed_steps()
 
     if args.profile_host and rank == 0:
         import cProfile
