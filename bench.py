@@ -529,6 +529,9 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     gc_clock = _GcClock()
     with gc_clock:
         eager_elapsed, loss = timed(eager_step, eager_steps)
+    # a copy: the sharded step's loss is a view into the gradient bucket, which later steps
+    # (the kernel-timed ones) overwrite
+    loss = loss.detach().clone()
     eager_ms = 1e3 * eager_elapsed / eager_steps
     wait_device(device)
 
@@ -577,6 +580,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         warm_replays(graph_step, max(1, warmup // repeat))
         arm(f"{config}: timed graph replays ({steps // repeat} replays of {repeat} steps)")
         elapsed, loss = timed(graph_step, steps // repeat)
+        loss = loss.detach().clone()   # (see above; the graph's own output is static as well)
         captured.check()
         mode = "hipGraph replay" + (f" ({repeat} steps per replay)" if repeat > 1 else "")
         if sharded:
