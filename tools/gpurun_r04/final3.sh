@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 run() { local t=$1; shift; local log=$1; shift; timeout -k 10 "$t" "$@" > "gpurun_out/$log" 2>&1; local rc=$?; echo "$log rc=$rc"; return $rc; }
-run 480 f3_tests.log python -u -m pytest -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider tests || exit 1
+run 400 f3_tests.log python -u -m pytest -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_dist_graph.py || exit 1
 run 400 f3_bench.log python -u bench.py || exit 1
 bash tools/gpurun_r04/c5sweep.sh || exit 1
 exit 0
