@@ -878,7 +878,12 @@ class LogJoint:
         All validation results of the step as one int64 device vector: one MI_FLAG_* word per
         kernel-evaluated site, then one 0/1 per deferred support / constraint check.
         """
-        flush_pending_step()   # (the held finishing launch writes the words)
+        step = _PENDING
+        if step is not None and (step.writes_flags or self.mirror is not None):
+            # a held site launch finishing the ELBO writes the words, a held ELBO forward their
+            # host mirror; a held ELBO forward with no mirror only reads them, and stays held for
+            # the optimizer step (the validation read then waits for the site kernels alone)
+            flush_pending_step()
         if self.flags is not None and not self.checks:
             return self.flags
         parts = []
@@ -912,6 +917,7 @@ class LogJoint:
                 bits = int(values[cursor])
                 cursor += 1
                 if bits & nat.FLAG_INTERNAL:
+                    flush_pending_step()
                     raise RuntimeError(f"site '{site.name}': an in-kernel completion wait of its "
                                        "launch timed out (results of this step are invalid)")
                 if bits & nat.FLAG_PARAM:
@@ -927,6 +933,7 @@ class LogJoint:
                 found.append((check.order, len(found), check.message))
             cursor += 1
         if found:
+            flush_pending_step()   # the step's launches all run, as without a violation
             raise ValueError(min(found)[2])
         for check, _ in self.checks:
             if check.memo is not None:
@@ -2093,6 +2100,9 @@ class _PendingStep:
     def __init__(self, launch, what: str, grads: List[torch.Tensor], keep, adapter) -> None:
         self._launch = launch        # launch(optimizer argument or None) -> error code
         self.what = what
+        # the site launches that finish the ELBO write the step's validation words themselves;
+        # the ELBO forward (mi_elbo_forward) only mirrors them
+        self.writes_flags = what != "mi_elbo_forward"
         self.grad_ptrs = {g.data_ptr() for g in grads if g is not None}
         self.held: List[Tuple[torch.Tensor, torch.Tensor]] = []   # (param, PendingGrad)
         self._keep = keep            # the launch's buffers, alive until it has run

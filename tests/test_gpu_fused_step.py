@@ -219,3 +219,18 @@ def test_gradients_read_before_the_step_are_complete(device, monkeypatch):
     for a, b in zip(seen, ref):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("name", ["regression", "coin"])
+def test_validated_step_joins_the_held_launch(device, monkeypatch, name):
+    """With validation on, the loss reads the step's validation words before returning: that read
+    waits for the site launches only -- the held ELBO forward (which writes no word) stays held and
+    the optimizer step still joins it. Results equal the held-off path bit for bit."""
+    _path(monkeypatch, name, "elbo")
+    adam = _spy(monkeypatch, "mi_adam_step")
+    losses, params, fusions = _train(device, monkeypatch, name, held=True, validate=True)
+    assert adam == [] and fusions["optimizer_step"] == 1
+    ref_losses, ref_params, _ = _train(device, monkeypatch, name, held=False, validate=True)
+    assert torch.equal(losses, ref_losses)
+    for a, b in zip(params, ref_params):
+        assert torch.equal(a, b)
