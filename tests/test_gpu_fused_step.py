@@ -82,7 +82,30 @@ def _coin(device, validate=False, n=200_000, K=1024):
     return module, loss_fn, (lambda: {"theta": module()}), (lambda: cond)
 
 
-MODELS = {"regression": _regression, "coin": _coin}
+def _hierarchical(device, validate=False, n=4096, K=128):
+    """The masked hierarchical model's shape (C5, examples/missing-observations.md): mu drawn
+    on its own, z ~ q(z) drawn inside the site program (a fused draw), its final gradients
+    written by the ELBO forward's final-gradient blocks."""
+    gen = torch.Generator().manual_seed(3)
+    y = torch.randn(n, generator=gen).to(device)
+    b = (torch.rand(n, generator=gen) < 0.4).float().to(device)
+
+    def model():
+        mu = mi.sample("mu", Normal(0.0, 1.0))
+        z = mi.sample("z", Normal(mu, 1.0), sample_shape=[n])
+        mi.sample("y", Normal(z, 0.5))
+        mi.sample("b", Bernoulli(logits=z))
+
+    module = mi.nn.ParameterizedFactorizedDistribution(
+        mu=mi.nn.ParameterizedDistribution(Normal, loc=0.1, scale=0.7),
+        z=mi.nn.ParameterizedDistribution(Normal, loc=torch.linspace(-1, 1, n),
+                                          scale=torch.linspace(0.2, 0.9, n))).to(device)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=5, validate=validate)
+    cond = mi.condition(model, y=y, b=b)
+    return module, loss_fn, (lambda: module()), (lambda: cond)
+
+
+MODELS = {"regression": _regression, "coin": _coin, "hierarchical": _hierarchical}
 FINISH = {"regression": ("MININF_AMD_LINEAR_ELBO", "mi_linear_elbo_forward"),
           "coin": ("MININF_AMD_GROUP_ELBO", "mi_group_elbo_forward")}
 PATHS = ["elbo", "finish"]
@@ -234,3 +257,48 @@ def test_validated_step_joins_the_held_launch(device, monkeypatch, name):
     assert torch.equal(losses, ref_losses)
     for a, b in zip(params, ref_params):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("validate", [False, True])
+def test_fused_draw_factor_steps_in_its_final_gradient_blocks(device, monkeypatch, validate):
+    """A fused-draw factor (10^3+ elements) is updated by the ELBO forward blocks that write its
+    final gradients, the one-element factor by the last block: no optimizer launch, parameters,
+    moments and losses bit-identical to the held-off path; the step counts advance once per
+    step (the last of the factor's blocks to read a count advances it)."""
+    adam = _spy(monkeypatch, "mi_adam_step")
+    fused = _spy(monkeypatch, "mi_elbo_forward_adam")
+    losses, params, fusions = _train(device, monkeypatch, "hierarchical", held=True, steps=5,
+                                     validate=validate)
+    assert adam == [] and fusions["optimizer_step"] == 1 and fusions["fused_draws"] == 1
+    assert len(fused) == 5 and all(call[4] is not None for call in fused)
+    ref_losses, ref_params, _ = _train(device, monkeypatch, "hierarchical", held=False, steps=5,
+                                       validate=validate)
+    assert torch.equal(losses, ref_losses)
+    for a, b in zip(params, ref_params):
+        assert torch.equal(a, b)
+
+
+def test_fused_draw_factor_steps_captured(device, monkeypatch):
+    """The same step captured (several steps per replay): the readers' words reset every step."""
+    ref_losses, ref_params, _ = _train(device, monkeypatch, "hierarchical", held=False, steps=9)
+    monkeypatch.setenv("MININF_AMD_DEFER_STEP", "1")
+    module, loss_fn, approx, conditioned = _hierarchical(device, validate=True)
+    optimizer = Adam(module.parameters(), lr=0.02)
+
+    def step():
+        optimizer.zero_grad(set_to_none=True)
+        loss = loss_fn(conditioned(), approx())
+        loss.backward()
+        optimizer.step()
+        return loss
+
+    adam = _spy(monkeypatch, "mi_adam_step")
+    graph = StepGraph(step, warmup=3, repeat=3)
+    assert adam == []
+    losses = [float(graph()) for _ in range(2)]
+    graph.check()
+    assert losses[0] == float(ref_losses[5]) and losses[1] == float(ref_losses[8])
+    for a, b in zip(module.parameters(), ref_params):
+        assert torch.equal(a.detach(), b)
+    for state in optimizer.state.values():
+        assert float(state["step"]) == 9.0
