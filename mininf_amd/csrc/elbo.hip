@@ -1778,11 +1778,11 @@ int mi_elbo_adam_supported(const mi_elbo* elbo, const mi_elbo_adam* adam, int* s
     for (int a = 0; a < L.fin.num; ++a)
       if (L.fin.index[a] == A.factor) fa = a;
     if (fa >= 0) {
-      static const bool fin_adam_on = [] {   // MININF_AMD_ELBO_FIN_ADAM=0: measurement A/B
-        const char* e = getenv("MININF_AMD_ELBO_FIN_ADAM");
-        return e == nullptr || atoi(e) != 0;
-      }();
-      if (!fin_adam_on) return 0;
+      // opt-in (MININF_AMD_ELBO_FIN_ADAM=1): measured slower on C5 (0.2122-0.2132 ms against
+      // 0.2086-0.2090 with Adam's own launch, one box) -- the streaming update runs at the
+      // launch's two blocks per CU (223 VGPR), where k_adam_step streams at full occupancy
+      const char* on = getenv("MININF_AMD_ELBO_FIN_ADAM");
+      if (on == nullptr || atoi(on) == 0) return 0;
       // updated by the factor's final-gradient blocks, quad by quad (fin_adam_quad): the 16-byte
       // path and aligned tensors. The scale is read by the lead blocks (the entropy), so the
       // updated tensor may not be it (an exp-transformed scale's parameter is the unconstrained
