@@ -788,9 +788,12 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
  * the thread that writes the gradient -- no optimizer launch for the step. `adam` is a DEVICE
  * pointer (the descriptor is read by the kernel; it may be reused across launches); NULL: as
  * mi_elbo_forward. mi_elbo_adam_supported checks a HOST copy against the launch: every slot's
- * factor finished by the last block (not a fused-draw factor), numel = the factor's n, the
- * gradient written, no (factor, param) twice. Replaces optimizer.step() (README.md:66-69) for
- * those parameters. */
+ * factor finished by the last block, numel = the factor's n, the gradient written, no
+ * (factor, param) twice. With the environment variable MININF_AMD_ELBO_FIN_ADAM=1 a fused-draw
+ * factor's slots are accepted as well (n % 4 == 0, 16-byte aligned tensors, not the scale the
+ * entropy reads): the blocks that write its final gradients update it, and the last of them to
+ * read a step count advances it (measured slower than mi_adam_step on C5: opt-in). Replaces
+ * optimizer.step() (README.md:66-69) for those parameters. */
 #define MI_ELBO_ADAM_SLOTS 4
 typedef struct mi_elbo_adam_slot {
   int32_t factor;
