@@ -1542,16 +1542,17 @@ int env_kred() {
 int env_lead() {
   static const int v = [] {
     const char* e = getenv("MININF_AMD_ELBO_LEAD");
-    const int n = e != nullptr ? atoi(e) : 16;
-    return (n == 4 || n == 8 || n == 16 || n == 32) ? n : 16;
+    // measured on MI355X (C5, steady clocks): 32 -> 0.2077-0.2079 ms, 16 -> 0.2091-0.2093
+    const int n = e != nullptr ? atoi(e) : 32;
+    return (n == 4 || n == 8 || n == 16 || n == 32) ? n : 32;
   }();
   return v;
 }
 
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
-  // about sixteen elements per lane of the longest term or factor (a lane's quads loaded four at
-  // a time): C5's 1e6-element scale entropy in 245 lead blocks instead of 977 -- the launch's
+  // about 32 elements per lane of the longest term or factor (a lane's quads loaded four at a
+  // time): C5's 1e6-element scale entropy in 123 lead blocks instead of 977 -- the launch's
   // 223-VGPR blocks fit two per CU, so a larger grid runs in several rounds
   L.fwd.lead_blocks = (int)std::max<int64_t>(
       1, std::min<int64_t>(mi::kElboMaxBlocks,
