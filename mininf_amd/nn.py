@@ -449,10 +449,27 @@ class EvidenceLowerBoundLoss(nn.Module):
         # the fast paths the last evaluation took (engine._ElboPlan.fusions)
         self.last_fusions: Dict[str, int] = {}
         self._sticky_flags: Optional[torch.Tensor] = None   # graph-mode validation words
+        # eager steps' validation words: rows of one zeroed block, a fresh block every
+        # FLAG_POOL steps (one fill launch per block instead of one per step)
+        self._flag_pool: Optional[torch.Tensor] = None
+        self._flag_next = 0
         self._mirror: Optional[torch.Tensor] = None   # their pinned host copy
 
     # validation words zeroed with the step counter's advance; plans with more sites zero their own
     FLAG_WORDS = 64
+    FLAG_POOL = 64
+
+    def _zeroed_flags(self, device: torch.device) -> torch.Tensor:
+        """Zeroed validation words for one eager step: a row no earlier step wrote (a used block
+        is never zeroed again: it is dropped, and lives on only while a joint still reads it)."""
+        pool = self._flag_pool
+        if pool is None or pool.device != device or self._flag_next >= pool.shape[0]:
+            pool = self._flag_pool = torch.zeros((self.FLAG_POOL, self.FLAG_WORDS),
+                                                 dtype=torch.int32, device=device)
+            self._flag_next = 0
+        row = pool[self._flag_next]
+        self._flag_next += 1
+        return row
 
     def _shard(self):
         """
@@ -518,7 +535,7 @@ class EvidenceLowerBoundLoss(nn.Module):
                                                    pin_memory=True)
                     flags, sticky, mirror = self._sticky_flags, True, self._mirror
                 else:
-                    flags = torch.zeros(self.FLAG_WORDS, dtype=torch.int32, device=device)
+                    flags = self._zeroed_flags(device)
             else:   # the samplers reject host guides with the engine's device error
                 step, flags = self._counter.clone(), None
                 self._counter.add_(1)
