@@ -74,3 +74,17 @@ def test_adam_zero_grad_matches_torch(set_to_none):
 @pytest.mark.parametrize("K", [1, 3, 7, 33, 1000, 4096, 123457])
 def test_float32_rounding_matches_torch(K):
     assert nn._float32(-1.0 / K) == float(torch.tensor(-1.0 / K, dtype=torch.float32))
+
+
+def test_eager_validation_words_are_fresh_zeroed_rows():
+    """Every eager step gets validation words no earlier step wrote: rows of a zeroed block, a new
+    block once the rows run out (the old block lives on while a step still holds its row)."""
+    loss = nn.EvidenceLowerBoundLoss(num_particles=4)
+    device = torch.device("cpu")
+    rows = [loss._zeroed_flags(device) for _ in range(loss.FLAG_POOL + 2)]
+    for r in rows:
+        assert r.shape == (loss.FLAG_WORDS,) and r.dtype == torch.int32 and not r.any()
+    ptrs = [r.data_ptr() for r in rows]
+    assert len(set(ptrs)) == len(ptrs)   # (the first block is still alive through its rows)
+    rows[0].fill_(7)                     # a step's kernels write its words ...
+    assert not loss._zeroed_flags(device).any()   # ... and no later step sees them
