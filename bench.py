@@ -10,7 +10,7 @@ observations and 4096 Monte-Carlo particles per GPU (particles are sharded acros
 scaling). One site-log_prob eval = one (particle, site, observed element) triple.
 
 Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (timed with HIP
-events around exactly that kernel during the timed steps) and the CPU baseline (the reference's
+event nodes around exactly that kernel in replays of the captured step, after the timed region) and the CPU baseline (the reference's
 torch-CPU semantics, oracle/cpu_port.py, on a bounded sample, N = 1 only).
 """
 from __future__ import annotations
@@ -43,26 +43,49 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
 
 class EventTimer:
     """
-    Collects (start, stop) HIP event pairs recorded by mi_group_forward_timed around the main site
-    kernel of each launch (engine.KERNEL_TIMER hook); keyed by the group's element count N so the
-    dominant kernel can be picked out.
+    Collects (start, stop) HIP event pairs that the library records around the main site kernel of
+    each launch (engine.KERNEL_TIMER hook: the event arguments of mi_group_forward_deferred /
+    mi_linear_forward_deferred), keyed by the group's element count N so the dominant kernel can
+    be picked out. With ``captured_only`` the pairs come from a pool created before a graph
+    capture and are handed out only while the stream is capturing: the library records them as
+    external event nodes (hipEventRecordExternal), so every replay of the graph times the kernel
+    as it runs in the replayed step.
     """
     def __init__(self):
         self.pairs = []
         self.active = False
+        self.captured_only = False
+        self._pool = []
+
+    def prepare(self, n):
+        """n event pairs, materialised outside any capture."""
+        for _ in range(n):
+            start = torch.cuda.Event(enable_timing=True)
+            stop = torch.cuda.Event(enable_timing=True)
+            start.record()
+            stop.record()
+            self._pool.append((start, stop))
 
     def pair(self, launcher):
         if not self.active:
             return None, None
-        start = torch.cuda.Event(enable_timing=True)
-        stop = torch.cuda.Event(enable_timing=True)
-        start.record()   # materialise the underlying hipEvent_t; re-recorded by the library
-        stop.record()
+        if self.captured_only:
+            if not torch.cuda.is_current_stream_capturing() or not self._pool:
+                return None, None
+            start, stop = self._pool.pop()
+        else:
+            start = torch.cuda.Event(enable_timing=True)
+            stop = torch.cuda.Event(enable_timing=True)
+            start.record()   # materialise the underlying hipEvent_t; re-recorded by the library
+            stop.record()
         self.pairs.append((launcher.N, launcher.K, start, stop))
         return start, stop
 
+    def times_ms(self, N):
+        return [s.elapsed_time(e) for n, _, s, e in self.pairs if n == N]
+
     def mean_ms(self, N):
-        times = [s.elapsed_time(e) for n, _, s, e in self.pairs if n == N]
+        times = self.times_ms(N)
         return sum(times) / len(times) if times else float("nan"), len(times)
 
 
@@ -536,15 +559,41 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     wait_device(device)
 
     def kernel_timed_steps():
-        """The kernel durations (roofline) from further eager steps with a HIP event pair around
-        the dominant launch, outside every timed region (the events cost host time per launch);
-        in graph mode after the replays, with the device at its steady clocks."""
+        """--eager (and split-graph gloo) runs: the kernel durations from further eager steps with
+        a HIP event pair around the dominant launch, outside every timed region (the events cost
+        host time per launch)."""
         arm(f"{config}: kernel-timed eager steps")
         timer.active = True
         for _ in range(eager_steps):
             eager_step()
         timer.active = False
         wait_device(device)
+
+    kernel_source = "eager steps (HIP events around the kernel)"
+
+    def kernel_timed_replays(repeat, replays=16):
+        """The dominant kernel's duration AS REPLAYED: the step captured once more with an external
+        event-record node before and after each dominant launch (EventTimer.captured_only), then
+        replayed `replays` times after the timed region; every replay re-records every pair, read
+        after it. The same kernels, grid and step structure as the timed graph."""
+        arm(f"{config}: kernel-timed graph replays")
+        timer.pairs = []
+        timer.prepare(8 * repeat)
+        timer.active, timer.captured_only = True, True
+        try:
+            timing_graph = StepGraph(full_step, warmup=1, repeat=repeat,
+                                     capture_error_mode="thread_local" if sharded else "global")
+        finally:
+            timer.active, timer.captured_only = False, False
+        pairs, timer.pairs = timer.pairs, []
+        samples = []
+        for i in range(replays + 2):
+            timing_graph()
+            wait_device(device)
+            if i >= 2:   # (the first replays after a capture are not steady)
+                samples += [(n, k, s.elapsed_time(e)) for n, k, s, e in pairs]
+        timing_graph.check()
+        return samples
 
     if not args.graph:
         kernel_timed_steps()
@@ -600,7 +649,12 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 floor_ms = 1e3 * floor_s / steps
             finally:
                 del os.environ["MININF_AMD_BCAST_SUFFSTAT"]
-        kernel_timed_steps()
+        if not sharded or collective_in_graph:
+            replay_samples = kernel_timed_replays(repeat)
+            kernel_source = (f"graph replays (external HIP event nodes around the kernel in a "
+                             f"capture of the same step, {repeat} steps per replay)")
+        else:
+            kernel_timed_steps()
 
     if args.profile_host and rank == 0:
         import cProfile
@@ -622,7 +676,12 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         dist.all_reduce(t)
         evals_all = float(t)
     value = evals_all * steps / elapsed
-    kernel_ms, launches = timer.mean_ms(w["dominant_N"])
+    if args.graph and (not sharded or collective_in_graph):
+        times = [t for n, _, t in replay_samples if n == w["dominant_N"]]
+        kernel_ms = sum(times) / len(times) if times else float("nan")
+        launches = len(times)
+    else:
+        kernel_ms, launches = timer.mean_ms(w["dominant_N"])
     kernel_s = kernel_ms * 1e-3
     if w["bound"] in ("valu", "mfma"):
         # FP32 VALU (v_pk_fma_f32) and FP32 MFMA (v_mfma_f32_32x32x2_f32) share the 157.3 TFLOP/s
@@ -632,6 +691,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         roof = {"bound": w["bound"], "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
                 "kernel": w["kernel"], "kernel_ms": kernel_ms, "launches_timed": launches,
+                "kernel_timing": kernel_source,
                 "algorithmic_per_launch": f"{flops:.4g} FLOP ({w['flop_note']})"}
     else:
         nbytes = w["bytes_per_launch"]
@@ -639,6 +699,7 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None, "kernel": w["kernel"],
                 "kernel_ms": kernel_ms, "launches_timed": launches,
+                "kernel_timing": kernel_source,
                 "algorithmic_per_launch": f"{nbytes:.4g} B"}
     traffic, source = measured_traffic(config)
     roof["traffic"] = traffic

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 14
+#define MI_ABI_VERSION 15
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -214,13 +214,6 @@ int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);
 int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,
                      double* site_lp, float* slot_grad, uint32_t* flags, void* stream);
 
-/* Same as mi_group_forward; when non-NULL, the hipEvent_t `start_event` / `stop_event` are recorded
- * on `stream` immediately before and after the main site kernel (not the flag reset or the
- * finalize reduction), so the caller can time exactly the roofline-bound kernel. */
-int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
-                           float* total, double* site_lp, float* slot_grad, uint32_t* flags,
-                           void* start_event, void* stop_event, void* stream);
-
 /* ---- deferred finalize reductions --------------------------------------------------------------
  * A site launch ends with a fixed-order fp64 reduction of its per-(segment, particle) partials
  *   part[(v * nseg + seg) * K + k],  v < num_sites: site log densities, then num_slots slot values
@@ -253,7 +246,11 @@ typedef struct mi_reduce {
   float* slot_grad;      /* [num_slots, K] (num_slots > 0) */
 } mi_reduce;
 
-/* mi_group_forward_timed with the finalize handed to the caller through *reduce (see above). */
+/* mi_group_forward with the finalize handed to the caller through *reduce (see above). When
+ * non-NULL, the hipEvent_t `start_event` / `stop_event` are recorded on `stream` immediately before
+ * and after the main site kernel (not the flag reset or the finalize reduction), as external event
+ * nodes under stream capture (hipEventRecordExternal), so the caller can time exactly the
+ * roofline-bound kernel -- also inside a replayed graph. */
 int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t workspace_bytes,
                               float* total, double* site_lp, float* slot_grad, uint32_t* flags,
                               void* start_event, void* stop_event, void* stream, mi_reduce* reduce);
@@ -533,65 +530,12 @@ int mi_linear_prior_supported(const mi_linear* site, int* supported);
 int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes);
 int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,
                       float* dslots, uint32_t* flags, void* stream);
-/* Same, recording the hipEvent_t start_event / stop_event (when non-NULL) around the site kernel
- * alone (not the fp64 finalize reduction). */
-int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t workspace_bytes,
-                            float* total, float* dslots, uint32_t* flags, void* start_event,
-                            void* stop_event, void* stream);
 int mi_linear_struct_size(size_t* bytes);
-/* mi_linear_forward_timed with the finalize handed to the caller through *reduce (see mi_reduce). */
+/* mi_linear_forward with the finalize handed to the caller through *reduce (see mi_reduce); the
+ * events as for mi_group_forward_deferred. */
 int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
                                float* total, float* dslots, uint32_t* flags, void* start_event,
                                void* stop_event, void* stream, mi_reduce* reduce);
-
-/* The whole ELBO forward in the linear site's launch (ABI 13). For a step whose ELBO is this one
- * site (with its folded prior) and one small Normal guide factor drawn by the same launch
- * (mi_linear.draw) -- the minibatch regression of examples/minibatch.md:76-88 -- the launch's last
- * blocks reduce its partials and run mi_elbo_forward's tail: `total` and `dslots` as the deferred
- * reduction writes them, *loss as mi_elbo_forward (elbo: the step's descriptor with num_terms 0
- * and num_reduce 0 -- the site's totals are not a term -- and factor 0 that Normal factor, its one
- * source dslots), the factor's gradients for an upstream of 1 (as with MI_ELBO_FINAL_GRADS), the
- * generator step advance and the flag mirror. One kernel instead of two (mi_linear_forward_deferred
- * + mi_elbo_forward). The completion counters and fp64 sums live in `elbo_workspace` (an
- * mi_elbo_forward workspace: zeroed counters, left zero). mi_linear_elbo_supported reports whether
- * the pair qualifies (one-stage matrix-core launch with gradients whose whole grid is resident,
- * K <= the block size, a short partial slab) and the elbo workspace it needs; otherwise
- * mi_linear_elbo_forward returns MI_EUNSUPPORTED without launching. Replaces nn.py:224-228 for
- * that step together with the site (core.py:241-273). */
-int mi_linear_elbo_supported(const mi_linear* site, const struct mi_elbo* elbo, int* supported,
-                             size_t* elbo_workspace_bytes);
-int mi_linear_elbo_forward(const mi_linear* site, const struct mi_elbo* elbo, void* workspace,
-                           size_t workspace_bytes, float* total, float* dslots, uint32_t* flags,
-                           void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                           const struct mi_adam* adam, void* start_event, void* stop_event,
-                           void* stream);
-
-/* The whole ELBO forward in a site group's launch (ABI 13), for the README model's step
- * (README.md:40-69): one Bernoulli BCAST site over shared data (the k_site_bcast_smem kernel, slot
- * in the rank-one layout, with the guide's Beta implicit-gradient factors as its side job, mi_side)
- * and one one-element Beta guide factor whose only source is that slot. The launch's last blocks
- * reduce its partials and run mi_elbo_forward's tail: `total` and `slot_grad` as the deferred
- * reduction writes them, *loss, the factor's saved sums and its gradients for an upstream of 1
- * (MI_ELBO_FINAL_GRADS), the generator step and the flag mirror. elbo: the step's descriptor with
- * num_terms 0 and num_reduce 0, factor 0 that Beta factor (source slot_grad, dgrad = side.out).
- * mi_group_elbo_supported reports whether the pair qualifies and the elbo workspace it needs;
- * otherwise mi_group_elbo_forward returns MI_EUNSUPPORTED without launching. Replaces
- * nn.py:224-228 for that step together with the site (core.py:241-273). */
-int mi_group_elbo_supported(const mi_group* group, const struct mi_elbo* elbo, int* supported,
-                            size_t* elbo_workspace_bytes);
-int mi_group_elbo_forward(const mi_group* group, const struct mi_elbo* elbo, void* workspace,
-                          size_t workspace_bytes, float* total, float* slot_grad, uint32_t* flags,
-                          void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                          const struct mi_adam* adam, void* start_event, void* stop_event,
-                          void* stream);
-
-/* The optimizer step in a finishing launch (ABI 14): `adam` (NULL: none) is an mi_adam_step
- * descriptor whose gradients are the final gradients the launch writes; the launch's last block
- * runs the step after writing them, with mi_adam_step's arithmetic (torch's fused Adam), so a
- * whole training step -- draws, sites, ELBO, gradients, parameter update -- is one kernel.
- * At most 16384 elements in all (MI_EUNSUPPORTED otherwise, nothing launched); malformed
- * descriptors are MI_EINVAL. Replaces torch.optim.Adam.step (optimizer.step() in
- * examples/minibatch.md:86 and README.md:63) for that step. */
 
 /* ---- device-resident minibatches (replaces examples/minibatch.md:78-88, the host DataLoader) ---- */
 
@@ -789,11 +733,8 @@ int mi_elbo_forward(const mi_elbo* elbo, void* workspace, size_t workspace_bytes
  * pointer (the descriptor is read by the kernel; it may be reused across launches); NULL: as
  * mi_elbo_forward. mi_elbo_adam_supported checks a HOST copy against the launch: every slot's
  * factor finished by the last block, numel = the factor's n, the gradient written, no
- * (factor, param) twice. With the environment variable MININF_AMD_ELBO_FIN_ADAM=1 a fused-draw
- * factor's slots are accepted as well (n % 4 == 0, 16-byte aligned tensors, not the scale the
- * entropy reads): the blocks that write its final gradients update it, and the last of them to
- * read a step count advances it (measured slower than mi_adam_step on C5: opt-in). Replaces
- * optimizer.step() (README.md:66-69) for those parameters. */
+ * (factor, param) twice; a fused-draw factor's slots are declined (mi_adam_step streams them at
+ * full occupancy). Replaces optimizer.step() (README.md:66-69) for those parameters. */
 #define MI_ELBO_ADAM_SLOTS 4
 typedef struct mi_elbo_adam_slot {
   int32_t factor;

@@ -38,7 +38,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 14   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 15   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -203,8 +203,6 @@ _SIGNATURES = {
                                                 ctypes.POINTER(ctypes.c_size_t)]),
     "mi_group_forward": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp, c_vp,
                                         c_vp, c_vp, c_vp]),
-    "mi_group_forward_timed": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp,
-                                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mi_group_forward_deferred": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                  ctypes.POINTER(Reduce)]),
@@ -278,8 +276,6 @@ _SIGNATURES = {
                                                  ctypes.POINTER(ctypes.c_size_t)]),
     "mi_linear_forward": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t, c_vp, c_vp,
                                          c_vp, c_vp]),
-    "mi_linear_forward_timed": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t, c_vp,
-                                               c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mi_linear_forward_deferred": (ctypes.c_int, [ctypes.POINTER(Linear), c_vp, ctypes.c_size_t,
                                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                   ctypes.POINTER(Reduce)]),
@@ -295,20 +291,6 @@ _SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_forward_adam": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, ctypes.c_size_t, c_vp,
                                             c_vp, c_vp]),
-    "mi_linear_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo),
-                                                ctypes.POINTER(ctypes.c_int),
-                                                ctypes.POINTER(ctypes.c_size_t)]),
-    "mi_linear_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Linear), ctypes.POINTER(Elbo), c_vp,
-                                              ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
-                                              ctypes.c_size_t, c_vp, ctypes.POINTER(Adam),
-                                              c_vp, c_vp, c_vp]),
-    "mi_group_elbo_supported": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo),
-                                               ctypes.POINTER(ctypes.c_int),
-                                               ctypes.POINTER(ctypes.c_size_t)]),
-    "mi_group_elbo_forward": (ctypes.c_int, [ctypes.POINTER(Group), ctypes.POINTER(Elbo), c_vp,
-                                             ctypes.c_size_t, c_vp, c_vp, c_vp, c_vp,
-                                             ctypes.c_size_t, c_vp, ctypes.POINTER(Adam),
-                                             c_vp, c_vp, c_vp]),
     "mi_elbo_final_grads": (ctypes.c_int, [ctypes.POINTER(Elbo), ctypes.POINTER(ctypes.c_int)]),
     "mi_elbo_backward": (ctypes.c_int, [ctypes.POINTER(Elbo), c_vp, c_vp, c_vp, ctypes.c_size_t,
                                         c_vp]),

@@ -20,7 +20,7 @@ SOURCES = [os.path.join(CSRC, name)
            for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "minibatch.hip",
                         "adam.hip", "mvn.hip", "jit.cpp")]
 HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "beta_grad.hpp", "jit.hpp",
-                                                 "internal.hpp", "entropy.hpp", "adam_math.hpp", "fin_timing.hpp")] + \
+                                                 "internal.hpp", "entropy.hpp", "adam_math.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]
 EMBEDDED = {"embedded_header.inc": os.path.join(INCLUDE, "mininf_amd.h"),
             "embedded_math.inc": os.path.join(CSRC, "device_math.hpp")}

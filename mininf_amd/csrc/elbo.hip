@@ -320,73 +320,13 @@ MI_DEV void partial_lane_elements(const mi_factor& F, int64_t base, int ti, int6
   }
 }
 
-// The optimizer step over a fused-draw factor whose final gradients blocks of the ELBO forward
-// write (mi_elbo_forward_adam): each of those blocks updates its own elements. Every block of the
-// factor reads the parameter's step count, then adds one to the slot's readers' count; the last
-// reader advances the step count and resets its word. One word per optimizer slot, below the 128
-// words of the ELBO-finishing site launches.
-constexpr int kAdamReaderWord = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 128 - MI_ELBO_ADAM_SLOTS;
-
-struct FinAdam {
-  const mi_elbo_adam* adam;   // nullptr: no update
-  int slot[2];                // the optimizer slot of each parameter of the factor, or -1
-  AdamCoef c[2];
-};
-
-// (block-uniform: every block of factor f calls it once; nb = the factor's blocks)
-MI_DEV FinAdam fin_adam(const mi_elbo_adam* __restrict__ adam, int f, int nb,
-                        unsigned* __restrict__ counters) {
-  __shared__ int sslot[2];
-  __shared__ AdamCoef scoef[2];
-  FinAdam fa{adam, {-1, -1}, {}};
-  if (adam == nullptr) return fa;
-  if (threadIdx.x < 2) sslot[threadIdx.x] = -1;
-  __syncthreads();
-  if ((int)threadIdx.x < adam->num && adam->slots[threadIdx.x].factor == f) {
-    const mi_elbo_adam_slot& A = adam->slots[threadIdx.x];
-    const float s1 = *A.step + 1.0f;
-    const int j = A.param != 0 ? 1 : 0;
-    scoef[j] = adam_coef(*adam, s1);
-    sslot[j] = (int)threadIdx.x;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the count read, then the arrival
-    unsigned* readers = counters + kAdamReaderWord + threadIdx.x;
-    if (atomicAdd(readers, 1u) == (unsigned)nb - 1u) {   // every block of the factor has read it
-      *A.step = s1;
-      *readers = 0u;
-    }
-  }
-  __syncthreads();
-  fa.slot[0] = sslot[0];
-  fa.slot[1] = sslot[1];
-  fa.c[0] = scoef[0];
-  fa.c[1] = scoef[1];
-  return fa;
-}
-
-// Adam over quad q of parameter j (16-byte value / moment accesses: checked by
-// mi_elbo_adam_supported), gradient g: torch's fused-Adam arithmetic (adam_math.hpp)
-MI_DEV void fin_adam_quad(const FinAdam& fa, int j, int64_t q, const float g[4]) {
-  const mi_elbo_adam_slot& A = fa.adam->slots[fa.slot[j]];
-  float4* __restrict__ pv = reinterpret_cast<float4*>(A.value) + q;
-  float4* __restrict__ mv = reinterpret_cast<float4*>(A.exp_avg) + q;
-  float4* __restrict__ vv = reinterpret_cast<float4*>(A.exp_avg_sq) + q;
-  const float4 p4 = *pv, m4 = *mv, v4 = *vv;
-  float p[4] = {p4.x, p4.y, p4.z, p4.w}, m[4] = {m4.x, m4.y, m4.z, m4.w};
-  float v[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) adam_update(*fa.adam, fa.c[j], p[e], g[e], m[e], v[e]);
-  *pv = make_float4(p[0], p[1], p[2], p[3]);
-  *mv = make_float4(m[0], m[1], m[2], m[3]);
-  *vv = make_float4(v[0], v[1], v[2], v[3]);
-}
-
 // The same backward with 16-byte accesses (Normal factors, n % 4 == 0, unit strides, aligned --
 // checked by the plan): lane quads q = first + p * ti, p < NP, every load of all NP quads in flight
 // before the first gradient is computed; the arithmetic and its order are those of
 // partial_lane_elements.
 template <int NP>
 MI_DEV void partial_lane_quads(const mi_factor& F, int64_t first, int ti, int64_t rows, float u,
-                               double w, const FinAdam& fa) {
+                               double w) {
   const bool exp0 = F.transform[0] == MI_TRANSFORM_EXP, exp1 = F.transform[1] == MI_TRANSFORM_EXP;
   const int64_t nq = F.n >> 2;
   const float4* __restrict__ sc = reinterpret_cast<const float4*>(F.param[1]);
@@ -440,8 +380,6 @@ MI_DEV void partial_lane_quads(const mi_factor& F, int64_t first, int ti, int64_
       reinterpret_cast<float4*>(F.grad[0])[q] = make_float4(g0[0], g0[1], g0[2], g0[3]);
     if (F.grad[1] != nullptr)
       reinterpret_cast<float4*>(F.grad[1])[q] = make_float4(g1[0], g1[1], g1[2], g1[3]);
-    if (fa.slot[0] >= 0) fin_adam_quad(fa, 0, q, g0);
-    if (fa.slot[1] >= 0) fin_adam_quad(fa, 1, q, g1);
   }
 }
 
@@ -450,8 +388,7 @@ MI_DEV void partial_lane_quads(const mi_factor& F, int64_t first, int ti, int64_
 template <bool FORWARD>
 MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float u,
                            unsigned* __restrict__ counters, double* __restrict__ work,
-                           double (*red)[2], bool* last,
-                           const mi_elbo_adam* __restrict__ adam = nullptr) {
+                           double (*red)[2], bool* last) {
   int a = 0;
 #pragma unroll
   for (int q = 1; q < MI_MAX_FACTORS; ++q)
@@ -484,12 +421,10 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   if (!FORWARD && pick(P.epl, a) < 0) {   // the same over quads: -epl quads per lane
     const int np = -pick(P.epl, a);
     const int64_t q0 = (int64_t)col * ti * np + tx;
-    const FinAdam fa = fin_adam(adam, pick(P.index, a), pick(P.first, a + 1) - pick(P.first, a),
-                                counters);
     switch (np) {
-      case 2: partial_lane_quads<2>(F, q0, ti, rows, u, w, fa); break;
-      case 4: partial_lane_quads<4>(F, q0, ti, rows, u, w, fa); break;
-      default: partial_lane_quads<1>(F, q0, ti, rows, u, w, fa); break;
+      case 2: partial_lane_quads<2>(F, q0, ti, rows, u, w); break;
+      case 4: partial_lane_quads<4>(F, q0, ti, rows, u, w); break;
+      default: partial_lane_quads<1>(F, q0, ti, rows, u, w); break;
     }
     return;
   }
@@ -904,7 +839,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     // MI_ELBO_FINAL_GRADS: the gradients of the fused-draw factors (MI_DRAW_PARTIALS) for an
     // upstream of 1 -- k_elbo_backward's absorbed blocks, run here (P: their plan); they read only
     // the site launches' partial rows, so they run beside the reductions
-    absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last, adam);
+    absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
     return;
   }
   if (!ABSORB && blockIdx.x == 0 && (R.tails > 0 || adam != nullptr))
@@ -1418,9 +1353,7 @@ int64_t longest_factor(const mi_elbo* e) {
 // from kCounterFirst on; the forward's group counters (kGroupCounters words, 64 bytes apart) in
 // between.
 constexpr int64_t kCounterFirst = mi::kGroupCounterWord + mi::kGroupCounters * mi::kGroupCounterStride;
-// (the last 128 words belong to the ELBO-finishing site launches: mi_linear_elbo_forward,
-// linear.hip kLinFinishCounterWord, and mi_group_elbo_forward, sites.hip kBcastFinishCounterWord)
-constexpr int64_t kMaxCounters = mi::kAdamReaderWord;   // (the optimizer readers' words above)
+constexpr int64_t kMaxCounters = MI_ELBO_COUNTER_BYTES / sizeof(unsigned);
 
 // Launch plans of both kernels and the layout of the fp64 work area that follows the counters:
 // [loss partials | forward absorbed partials | backward absorbed partials]. All of it is scratch
@@ -1778,22 +1711,7 @@ int mi_elbo_adam_supported(const mi_elbo* elbo, const mi_elbo_adam* adam, int* s
     int fa = -1;
     for (int a = 0; a < L.fin.num; ++a)
       if (L.fin.index[a] == A.factor) fa = a;
-    if (fa >= 0) {
-      // opt-in (MININF_AMD_ELBO_FIN_ADAM=1): measured slower on C5 (0.2122-0.2132 ms against
-      // 0.2086-0.2090 with Adam's own launch, one box) -- the streaming update runs at the
-      // launch's two blocks per CU (223 VGPR), where k_adam_step streams at full occupancy
-      const char* on = getenv("MININF_AMD_ELBO_FIN_ADAM");
-      if (on == nullptr || atoi(on) == 0) return 0;
-      // updated by the factor's final-gradient blocks, quad by quad (fin_adam_quad): the 16-byte
-      // path and aligned tensors. The scale is read by the lead blocks (the entropy), so the
-      // updated tensor may not be it (an exp-transformed scale's parameter is the unconstrained
-      // one); the location is read only by the lane that updates it, before the update
-      auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-      if (L.fin.epl[fa] >= 0 || F.n % 4 != 0 || !aligned(A.value) || !aligned(A.exp_avg) ||
-          !aligned(A.exp_avg_sq) || A.value == F.param[1])
-        return 0;
-      continue;
-    }
+    if (fa >= 0) return 0;   // (written by the fused-draw blocks: Adam's own launch streams them)
     bool tail = false;
     for (int t = 0; t < L.red.tails; ++t) tail |= L.red.tail_factor[t] == A.factor;
     const bool nt = L.red.nt_job >= 0 && A.factor == 0;

@@ -15,7 +15,6 @@
 // accumulators live in registers. Per-(tile, particle) partials are reduced in fp64 by k_finalize.
 #include "adam_math.hpp"
 #include "common.hpp"
-#include "fin_timing.hpp"
 #include "internal.hpp"
 #include "rows.hpp"
 
@@ -187,300 +186,6 @@ __global__ __launch_bounds__(kLinThreads) void k_linear(const mi_linear L, int k
 // subset), reduced in fp64 by k_finalize as for the VALU kernel.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// ---- the ELBO forward finished by the linear launch (mi_linear_elbo_forward) -------------------
-// A regression step whose whole ELBO is one linear site over theta ~ q (the guide's one small
-// Normal factor, drawn by this launch: mi_linear.draw) -- examples/minibatch.md:76-88 -- needs
-// nothing from mi_elbo_forward but the reduction of this launch's partial slab and a short tail
-// (loss, the factor's final gradients, the generator step, the validation mirror). The launch's
-// last blocks do it instead of a dependent launch:
-//   1. every block stores its partials agent-coherent and takes an arrival ticket; the last
-//      `helpers` arrivals stay, wait until every block has arrived (a bounded spin: the whole
-//      grid is resident, checked on the host) and each sums one (value, segment chunk) job of the
-//      slab for all particles into fp64 chunk sums;
-//   2. the last helper to finish adds the chunk sums in a fixed order -- totals and slot
-//      gradients, as mi_elbo_forward's deferred reduction writes them -- and runs the tail:
-//      loss = g0 sum_k total_k - entropy_scale weight H(q), the factor's gradients for an
-//      upstream of 1 (MI_ELBO_FINAL_GRADS: sum_k dz, sum_k dz eps with the regenerated eps, the
-//      entropy and exp-transform terms), the step counter advance and the flag mirror.
-// Deterministic: fixed job assignment and fixed summation orders (tickets only pick WHICH block
-// runs a job, not what it sums).
-struct LinFinish {
-  unsigned* counters;      // [0] arrivals, [16] helpers done: zero between launches
-  double* work;            // [nv][nsc][K] fp64 chunk sums
-  int helpers;             // blocks that stay to run the jobs: min(jobs, grid)
-  int jobs;                // nv * nsc
-  int nsc;                 // segment chunks per value
-  int nv;                  // values of the slab (1 + slots)
-  int kp;                  // particle lanes per job: a power of two >= K, <= NT
-  int64_t segc;            // segments per chunk
-  float* loss;
-  float* total;            // [K]
-  float* dslots;           // [nv - 1, K]
-  double entropy_scale;
-  double weight;           // the factor's entropy weight
-  float* grad[2];          // d loss / d (loc, u_scale) of the factor (upstream 1)
-  int64_t grad_stride[2];
-  int32_t transform[2];
-  uint64_t* step_counter;  // NULL: no advance
-  uint64_t* step_snapshot;
-  const uint32_t* flags;   // NULL: no mirror
-  uint32_t* flags_mirror;
-  int64_t nflags;
-  mi_adam adam;            // num 0: no optimizer step in the launch
-};
-
-// Counter words of the mi_elbo workspace the launch uses (kept clear of mi_elbo_forward's).
-constexpr int64_t kLinFinishCounterWord = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 32;
-static_assert(kLinFinishCounterWord >= MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 128 + 96,
-              "clear of sites.hip kBcastFinishCounterWord's words");
-
-template <bool COHERENT>
-MI_DEV void st_part(float* p, float v) {
-  if constexpr (COHERENT)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = v;
-}
-
-MI_DEV float ld_agent(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-MI_DEV double ld_agent(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-MI_DEV uint32_t ld_agent_u32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-#if MI_FINISH_TIMING
-__device__ unsigned long long* mi_linfin_tbuf;
-#define MI_LF_STAMP(i) MI_FIN_STAMP(mi_linfin_tbuf, i)
-#else
-#define MI_LF_STAMP(i) do { } while (0)
-#endif
-
-constexpr int kFinPairs = 4;   // (value, particle) pairs per thread and pass of the final sum
-constexpr int kFinChunks = 8;  // segment chunks per value (host-checked)
-
-// `scratch`: the kernel's X staging buffer (idle by now), host-checked to hold the tail's LDS.
-template <int NT>
-__device__ void lin_finish(const mi_linear& L, const LinFinish& F,
-                                                     const float* part, int64_t ntile,
-                                                     uint32_t* flags, float* scratch) {
-  __shared__ int role;
-  const int tid = threadIdx.x;
-  const int64_t K = L.K;
-  const int P = (int)L.P;
-  MI_LF_STAMP(1);
-  __builtin_amdgcn_s_waitcnt(0);   // this thread's (agent-coherent) partial stores are complete
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned nb = gridDim.x;
-    const unsigned t = atomicAdd(F.counters, 1u);
-    MI_LF_STAMP(2);
-    int r = (t + (unsigned)F.helpers >= nb) ? (int)(t + (unsigned)F.helpers - nb) : -1;
-    if (r >= 0) {
-      // the other blocks are resident (the host checked the grid fits the chip) and never wait:
-      // the count reaches nb; bounded anyway, reported through the site's flag word
-      unsigned spins = 0;
-      while (__hip_atomic_load(F.counters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nb) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {
-          atomicOr(flags, MI_FLAG_INTERNAL);
-          break;
-        }
-      }
-    }
-    role = r;
-  }
-  __syncthreads();
-  const int h = role;
-  if (h < 0) return;
-  MI_LF_STAMP(3);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  double* lds = reinterpret_cast<double*>(scratch);   // [NT] doubles during the jobs
-  // jobs h, h + helpers, ... (more jobs than blocks in a small launch); the block that completes
-  // the last job runs the tail (it has no job left: every job was counted before it)
-  bool final_block = false;
-  for (int job = h; job < F.jobs; job += F.helpers) {
-    // job: value v, segments [s0, s1) of every particle
-    const int v = job / F.nsc, c = job - v * F.nsc;
-    const int64_t s0 = (int64_t)c * F.segc;
-    const int64_t s1 = min(ntile, s0 + F.segc);
-    const int kp = F.kp, G = NT / kp;
-    const int kl = tid % kp, gl = tid / kp;
-    const int64_t kc = kl < K ? kl : K - 1;
-    const float* __restrict__ p = part + (int64_t)v * ntile * K + kc;
-    double acc = 0.0;
-    int64_t s = s0 + gl;
-    for (; s + 15 * G < s1; s += 16 * G) {
-      float x[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) x[j] = ld_agent(p + (s + j * G) * K);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc += (double)x[j];
-    }
-    for (; s < s1; s += G) acc += (double)ld_agent(p + s * K);
-    lds[tid] = acc;
-    __syncthreads();
-    if (gl == 0 && kl < K) {
-      double t = 0.0;
-      for (int q = 0; q < G; ++q) t += lds[q * kp + kl];
-      __hip_atomic_store(&F.work[((int64_t)v * F.nsc + c) * K + kl], t, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned t = atomicAdd(F.counters + 16, 1u);
-      role = t == (unsigned)F.jobs - 1u ? 1 : -1;
-    }
-    __syncthreads();
-    final_block = role > 0;
-  }
-  MI_LF_STAMP(4);
-  if (!final_block) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  MI_LF_STAMP(5);
-
-  // ---- the last helper: chunk sums in a fixed order, then the tail --------------------------
-  const mi_draw& D = L.draw;
-  const int nv = F.nv;
-  const int64_t npairs = (int64_t)nv * K;
-  // the factor's parameters, the step and the validation words, loaded before the sums
-  const int nq = P / 4;
-  const bool exp_scale = D.scale_exp != nullptr;
-  const float* sp = exp_scale ? D.scale_exp : D.scale;
-  float sc[4];
-  const int qh = tid < nq ? tid : 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) sc[j] = sp[(int64_t)(4 * qh + j) * D.scale_stride];
-  const int ip = tid < P ? tid : 0;
-  const float pv0 = D.loc[(int64_t)ip * D.loc_stride];
-  const float pv1 = sp[(int64_t)ip * D.scale_stride];
-  const uint64_t step = D.step + (D.step_device != nullptr ? *D.step_device : 0ull);
-  const uint32_t fw = (int64_t)tid < F.nflags ? ld_agent_u32(F.flags + tid) : 0u;
-
-  float* tf = scratch;   // [nv * K]: the totals, then the slot gradients
-  for (int64_t base = 0; base < npairs; base += (int64_t)kFinPairs * NT) {
-    // every load of a pass issued before its first sum: clamped addresses, unused ones skipped
-    double w[kFinPairs][kFinChunks];
-#pragma unroll
-    for (int j = 0; j < kFinPairs; ++j) {
-      const int64_t pr = base + tid + (int64_t)j * NT;
-      const int64_t pc = pr < npairs ? pr : npairs - 1;
-      const int64_t v = pc / K, k = pc - v * K;
-#pragma unroll
-      for (int c = 0; c < kFinChunks; ++c) {
-        const int cc = c < F.nsc ? c : 0;
-        w[j][c] = ld_agent(&F.work[(v * F.nsc + cc) * K + k]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kFinPairs; ++j) {
-      const int64_t pr = base + tid + (int64_t)j * NT;
-      if (pr >= npairs) break;
-      double t = 0.0;
-#pragma unroll
-      for (int c = 0; c < kFinChunks; ++c)
-        if (c < F.nsc) t += w[j][c];
-      const int64_t v = pr / K, k = pr - v * K;
-      if (v == 0) {
-        const float tv = (float)(t * L.site_scale);
-        F.total[k] = tv;
-        tf[pr] = tv;
-      } else {
-        const float gv = (float)(t * (double)L.grad_scale);
-        F.dslots[pr - K] = gv;
-        tf[pr] = gv;
-      }
-    }
-  }
-  __syncthreads();
-  // sum_k dz and sum_k dz * eps per feature: thread t takes the items (particle k, feature quad
-  // q = t % nq) of its column (nq divides NT, host-checked), eps regenerated as the draw made it
-  double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
-  {
-    const int q = tid % nq;
-    for (int64_t k = tid / nq; k < K; k += NT / nq) {
-      float e[4];
-      guide_normals(D.seed, step, D.stream_id, (uint64_t)(D.element_offset / 4 + q),
-                    (uint64_t)(D.particle_offset + k), e);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float gv = tf[(1 + 4 * q + j) * K + k];
-        a0[j] += (double)gv;
-        a1[j] += (double)gv * (double)e[j];
-      }
-    }
-  }
-  if (tid < 64) {
-    // loss = g0 sum_k total_k - entropy_scale weight H, H = sum_i log scale_i + n (1 + log 2 pi) / 2
-    double lp = 0.0;
-    for (int64_t k = tid; k < K; k += 64) lp += (double)L.grad_scale * (double)tf[k];
-    double hq = 0.0;
-    if (tid < nq) {
-      float s4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s4[j] = exp_scale ? expf(sc[j]) : sc[j];
-      hq = (double)((logf(s4[0]) + logf(s4[1])) + (logf(s4[2]) + logf(s4[3])));
-    }
-    lp = wave_sum(lp);
-    hq = wave_sum(hq);
-    if (tid == 0) {
-      const double H = hq + 1.4189385332046727 * (double)P;
-      *F.loss = (float)(lp - F.entropy_scale * F.weight * H);
-    }
-  }
-  __syncthreads();
-  double* red = reinterpret_cast<double*>(scratch);   // [NT][8] (over tf, read by now)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    red[tid * 8 + j] = a0[j];
-    red[tid * 8 + 4 + j] = a1[j];
-  }
-  __syncthreads();
-  if (tid < P) {
-    // the gradients k_elbo_backward writes for an upstream of 1 (mi_elbo_forward's Normal tail):
-    // the columns' sums in a fixed order, the entropy term, the exp-transform chain rule
-    const int i = tid, q = i / 4, j = i % 4;
-    double s0 = 0.0, s1 = 0.0;
-    for (int r = q; r < NT; r += nq) {
-      s0 += red[r * 8 + j];
-      s1 += red[r * 8 + 4 + j];
-    }
-    const float p1 = exp_scale ? expf(pv1) : pv1;
-    const double wgt = -(double)1.0f * F.entropy_scale * F.weight;
-    double g[2] = {(double)1.0f * s0 + wgt * 0.0, (double)1.0f * s1 + wgt * (double)(1.0f / p1)};
-    const float pv[2] = {pv0, p1};
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (F.grad[c] == nullptr) continue;
-      if (F.transform[c] == MI_TRANSFORM_EXP) g[c] *= (double)pv[c];
-      F.grad[c][(int64_t)i * F.grad_stride[c]] = (float)g[c];
-    }
-  }
-  if ((int64_t)tid < F.nflags) F.flags_mirror[tid] = fw;
-  for (int64_t i = tid + NT; i < F.nflags; i += NT) F.flags_mirror[i] = ld_agent_u32(F.flags + i);
-  if (tid == 0) {
-    if (F.step_counter != nullptr) {
-      const uint64_t c0 = *F.step_counter;
-      *F.step_snapshot = c0;
-      *F.step_counter = c0 + 1u;
-    }
-    __hip_atomic_store(F.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(F.counters + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  MI_LF_STAMP(6);
-  if (F.adam.num > 0) {
-    // the optimizer step over the gradients just written (every block has read the parameters
-    // for its draw before arriving): the training step ends inside this launch
-    __syncthreads();
-    adam_block<NT>(F.adam);
-  }
-  MI_LF_STAMP(7);
-}
-
 // Phase timestamps (MI_LINEAR_TIMING builds only, tools/linear_timing.py): wall clock at 8 points of
 // every wave of k_linear_mfma, into a buffer behind the launch's workspace.
 #ifndef MI_LINEAR_TIMING
@@ -571,16 +276,13 @@ __device__ __forceinline__ void draw_theta(const mi_linear& L, int64_t kbase, in
 // ONESTAGE: every block stages one row block (small N, e.g. a 65536-row minibatch): no stage
 // loop, no prefetch and no software pipeline over tiles -- a third of the code, which matters
 // when each wave runs through it once (the cold instruction fetch dominates such launches).
-// FINISH (ONESTAGE launches with gradients only): the launch also runs the ELBO forward
-// (lin_finish): partials are stored agent-coherent and the last blocks reduce them.
-template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW, bool GRADS, bool ONESTAGE,
-          bool FINISH>
+template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW, bool GRADS, bool ONESTAGE>
 __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int wt, int gy,
                                                           int64_t stages_per_block,
                                                           int64_t ntile,
                                                           float* __restrict__ part,
                                                           uint32_t* __restrict__ flags,
-                                                          int rows_half, const LinFinish fin) {
+                                                          int rows_half) {
   using S = MfShape<PT, NT>;
   constexpr int kMfThreads = NT;
   constexpr int kMfWaves = S::NW;
@@ -588,7 +290,6 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   unsigned long long ts_[8] = {};
 #endif
   MI_LIN_STAMP(0);
-  if constexpr (FINISH) MI_LF_STAMP(0);
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
@@ -938,9 +639,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   MI_LIN_STAMP(6);
   if (!combine || rs == 0) {
     if (h == 0 && k0 + c < K) {
-      st_part<FINISH>(&part[tile_id * K + k0 + c], val[16 * PT]);
+      part[tile_id * K + k0 + c] = val[16 * PT];
       if (per_particle_sigma && grads)
-        st_part<FINISH>(&part[((int64_t)(1 + P) * ntile + tile_id) * K + k0 + c], val[16 * PT + 1]);
+        part[((int64_t)(1 + P) * ntile + tile_id) * K + k0 + c] = val[16 * PT + 1];
     }
     if (grads) {
 #pragma unroll
@@ -950,7 +651,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 #pragma unroll
         for (int t = 0; t < PT; ++t) {
           const int p = 32 * t + c;
-          if (p < P) st_part<FINISH>(&part[((int64_t)(1 + p) * ntile + tile_id) * K + kk], val[r * PT + t]);
+          if (p < P) part[((int64_t)(1 + p) * ntile + tile_id) * K + kk] = val[r * PT + t];
         }
       }
     }
@@ -974,14 +675,14 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
         else eval_gamma(L.prior.constant[0], L.prior.constant[1], thf[s], e);
         plp += e.lp;
         pfl |= (e.param_bad ? MI_FLAG_PARAM : 0u) | (e.support_bad ? MI_FLAG_SUPPORT : 0u);
-        if (grads) st_part<FINISH>(&part[((int64_t)(1 + p) * ntile + ptile) * K + kk], (float)(L.prior.scale * (double)e.d[2]));
+        if (grads) part[((int64_t)(1 + p) * ntile + ptile) * K + kk] = (float)(L.prior.scale * (double)e.d[2]);
       }
     }
     plp += __shfl_xor(plp, 32, kWave);   // the particle's two feature parities
     if (h == 0 && kk < K) {
       // the reduction scales the value row by the site's scale
-      st_part<FINISH>(&part[ptile * K + kk], (float)((double)plp * L.prior.scale / L.site_scale));
-      if (per_particle_sigma && grads) st_part<FINISH>(&part[((int64_t)(1 + P) * ntile + ptile) * K + kk], 0.0f);
+      part[ptile * K + kk] = (float)((double)plp * L.prior.scale / L.site_scale);
+      if (per_particle_sigma && grads) part[((int64_t)(1 + P) * ntile + ptile) * K + kk] = 0.0f;
     }
     publish_flags(L.prior.flags, pfl);
   }
@@ -1002,7 +703,6 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       L.rows.counter[0] = batch_no + 1;
     }
   }
-  if constexpr (FINISH) lin_finish<NT>(L, fin, part, ntile, flags, xs);
 }
 
 }  // namespace mi
@@ -1133,139 +833,48 @@ int launch_check(const mi_linear* site, const Geometry& g) {
 }
 
 // Compute units of the current device (cached).
-int device_cus() {
-  static int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
-      return 0;
-    return n;
-  }();
-  return cus;
-}
-
-// The ELBO-finishing launch (mi_linear_elbo_forward) of `site` and `elbo`: 0 and the plan (its
-// counters / work pointers still unset) when this launch can run the whole ELBO forward, else
-// MI_EUNSUPPORTED. *work_doubles: the chunk sums it keeps in the ELBO workspace.
-int finish_plan(const mi_linear* site, const mi_elbo* E, const Geometry& g, mi::LinFinish& F,
-                int64_t* work_doubles) {
-  if (E == nullptr || !g.mfma || g.stages_per_block != 1 || !site->compute_grads ||
-      site->draw.operand == 0 || launch_check(site, g) != 0)
-    return MI_EUNSUPPORTED;
-  if (getenv("MININF_AMD_LINEAR_ELBO") != nullptr && atoi(getenv("MININF_AMD_LINEAR_ELBO")) == 0)
-    return MI_EUNSUPPORTED;
-  const MfVariant v = kMfVariants[g.variant];
-  const int NT = v.threads;
-  if (NT != 256 || v.minw < 2) return MI_EUNSUPPORTED;   // (kFinishVariant)
-  // the whole grid resident at once (the helpers wait for every other block): waves per SIMD
-  // at least the variant's minimum, four SIMDs per compute unit
-  const int cus = device_cus();
-  const int64_t resident = (int64_t)cus * 4 * v.minw * mi::kWave / NT;
-  const int64_t grid = g.gx * g.gy;
-  if (cus < 1 || grid > resident) return MI_EUNSUPPORTED;
-  const int64_t K = site->K, P = site->P;
-  if (E->K != K || E->num_terms != 0 || E->num_reduce != 0 || E->num_factors != 1 || K > NT)
-    return MI_EUNSUPPORTED;
-  const mi_factor& Q = E->factors[0];
-  const mi_draw& D = site->draw;
-  if (Q.family != MI_NORMAL || Q.draw_kind != MI_DRAW_SOURCES || Q.num_sources != 1 || Q.n != P ||
-      Q.eps != nullptr || !(Q.weight > 0.0) || Q.param[1] != D.scale || Q.source[0].stride_k != 1 ||
-      Q.source[0].stride_i != K || Q.stream_id != D.stream_id || Q.seed != D.seed ||
-      Q.particle_offset != D.particle_offset || Q.element_offset != D.element_offset)
-    return MI_EUNSUPPORTED;
-  if (E->nflags < 0 || (E->flags_mirror != nullptr && E->flags == nullptr)) return MI_EINVAL;
-  int kp = 1;
-  while (kp < K) kp <<= 1;
-  const int nv = g.nv;
-  const int64_t npairs = (int64_t)nv * K;
-  // segment chunks: 16 loads per helper thread (one round of memory latency)
-  const int64_t per_chunk = (int64_t)16 * (NT / kp);
-  const int64_t nsc = ceil_div(g.ntile, per_chunk);
-  if (nsc > mi::kFinChunks) return MI_EUNSUPPORTED;
-  // the tail's feature quads split evenly over the block's threads
-  const int64_t nq = P / 4;
-  if (P % 4 != 0 || (nq & (nq - 1)) != 0 || NT % nq != 0) return MI_EUNSUPPORTED;
-  // the tail's LDS inside the X staging buffer: the job sums, the slab's sums, the column sums
-  const int64_t xs_bytes = (int64_t)((NT >= 512 ? 256 : 128) / g.pt) * (32 * g.pt + 4) * 4;
-  if ((int64_t)NT * 8 * 8 > xs_bytes || npairs * 4 > xs_bytes) return MI_EUNSUPPORTED;
-  F = mi::LinFinish{};
-  F.jobs = (int)(nv * nsc);
-  F.helpers = (int)std::min<int64_t>(F.jobs, grid);
-  F.nsc = (int)nsc;
-  F.nv = nv;
-  F.kp = kp;
-  F.segc = ceil_div(g.ntile, nsc);
-  F.entropy_scale = E->entropy_scale;
-  F.weight = Q.weight;
-  for (int j = 0; j < 2; ++j) {
-    F.grad[j] = Q.grad[j];
-    F.grad_stride[j] = Q.grad_stride[j];
-    F.transform[j] = Q.transform[j];
-  }
-  F.step_counter = E->step_counter;
-  F.step_snapshot = E->step_snapshot;
-  F.flags = E->flags;
-  F.flags_mirror = E->flags_mirror;
-  F.nflags = E->flags_mirror != nullptr ? E->nflags : 0;
-  *work_doubles = npairs * nsc;
-  return 0;
-}
-
 // per-(tile, particle) partials, 256-byte aligned so the finalize scratch behind them is too
 size_t partial_bytes(const mi_linear* site, const Geometry& g) {
   return ((size_t)g.nv * (size_t)g.ntile * (size_t)site->K * sizeof(float) + 255) / 256 * 256;
 }
 
-// The variants with an ELBO-finishing instance: the default ones (mf_variant), 256 threads.
-template <int NT, int MINW>
-constexpr bool kFinishVariant = NT == 256 && MINW >= 2;
-
 template <int FAMILY, int PT, int NT, bool FLUSH64, int MINW>
 void launch_mfma(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
-                 hipStream_t s, const mi::LinFinish* fin) {
+                 hipStream_t s) {
   const dim3 grid((unsigned)(g.gx * g.gy));
   const bool one = g.stages_per_block == 1;
-  const mi::LinFinish none{};
-#define MI_LAUNCH_MFMA(GRADS, ONE, FIN)                                                          \
-  hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, GRADS, ONE, FIN>), grid,  \
+#define MI_LAUNCH_MFMA(GRADS, ONE)                                                               \
+  hipLaunchKernelGGL((mi::k_linear_mfma<FAMILY, PT, NT, FLUSH64, MINW, GRADS, ONE>), grid,       \
                      dim3(NT), 0, s, L, g.wt, (int)g.gy, g.stages_per_block, g.ntile, part, flags, \
-                     L.rows.counter != nullptr ? mi_feistel_half(L.rows.n) : 0,                  \
-                     fin != nullptr ? *fin : none)
-  if constexpr (kFinishVariant<NT, MINW>) {
-    if (fin != nullptr) {   // (host-checked: one stage per block, gradients)
-      MI_LAUNCH_MFMA(true, true, true);
-      return;
-    }
-  }
+                     L.rows.counter != nullptr ? mi_feistel_half(L.rows.n) : 0)
   if (L.compute_grads) {
-    if (one) MI_LAUNCH_MFMA(true, true, false); else MI_LAUNCH_MFMA(true, false, false);
+    if (one) MI_LAUNCH_MFMA(true, true); else MI_LAUNCH_MFMA(true, false);
   } else {
-    if (one) MI_LAUNCH_MFMA(false, true, false); else MI_LAUNCH_MFMA(false, false, false);
+    if (one) MI_LAUNCH_MFMA(false, true); else MI_LAUNCH_MFMA(false, false);
   }
 #undef MI_LAUNCH_MFMA
 }
 
 template <int FAMILY, int PT>
 void launch_mfma_variant(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
-                         hipStream_t s, const mi::LinFinish* fin) {
+                         hipStream_t s) {
   switch (g.variant) {
-    case 1: launch_mfma<FAMILY, PT, 512, false, 1>(L, g, part, flags, s, fin); break;
-    case 2: launch_mfma<FAMILY, PT, 256, false, 1>(L, g, part, flags, s, fin); break;
-    case 3: launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s, fin); break;
-    case 4: launch_mfma<FAMILY, PT, 256, PT == 1, 2>(L, g, part, flags, s, fin); break;
-    default: launch_mfma<FAMILY, PT, 512, PT == 1, 1>(L, g, part, flags, s, fin); break;
+    case 1: launch_mfma<FAMILY, PT, 512, false, 1>(L, g, part, flags, s); break;
+    case 2: launch_mfma<FAMILY, PT, 256, false, 1>(L, g, part, flags, s); break;
+    case 3: launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s); break;
+    case 4: launch_mfma<FAMILY, PT, 256, PT == 1, 2>(L, g, part, flags, s); break;
+    default: launch_mfma<FAMILY, PT, 512, PT == 1, 1>(L, g, part, flags, s); break;
   }
 }
 
 template <int FAMILY>
-void launch(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags, hipStream_t s,
-            const mi::LinFinish* fin = nullptr) {
+void launch(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 grid((unsigned)g.gx, (unsigned)g.gy);
   if (g.mfma) {
     if (g.pt == 1)
-      launch_mfma_variant<FAMILY, 1>(L, g, part, flags, s, fin);
+      launch_mfma_variant<FAMILY, 1>(L, g, part, flags, s);
     else
-      launch_mfma_variant<FAMILY, 2>(L, g, part, flags, s, fin);
+      launch_mfma_variant<FAMILY, 2>(L, g, part, flags, s);
     return;
   }
   if (L.P <= 8)
@@ -1308,13 +917,6 @@ int mi_linear_workspace_bytes(const mi_linear* site, size_t* bytes) {
   return 0;
 }
 
-int mi_linear_forward_timed(const mi_linear* site, void* workspace, size_t workspace_bytes,
-                            float* total, float* dslots, uint32_t* flags, void* start_event,
-                            void* stop_event, void* stream) {
-  return mi_linear_forward_deferred(site, workspace, workspace_bytes, total, dslots, flags,
-                                    start_event, stop_event, stream, nullptr);
-}
-
 int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t workspace_bytes,
                                float* total, float* dslots, uint32_t* flags, void* start_event,
                                void* stop_event, void* stream, mi_reduce* reduce) {
@@ -1347,7 +949,7 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
       return to_code(e);
   }
 #endif
-  if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
+  if (start_event != nullptr && (e = hipEventRecordWithFlags(static_cast<hipEvent_t>(start_event), s, hipEventRecordExternal)) != hipSuccess)
     return to_code(e);
   if (site->family == MI_NORMAL)
     launch<MI_NORMAL>(*site, g, part, flags, s);
@@ -1355,7 +957,7 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
     launch<MI_BERNOULLI_LOGITS>(*site, g, part, flags, s);
   e = hipGetLastError();
   if (e != hipSuccess) return to_code(e);
-  if (stop_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s)) != hipSuccess)
+  if (stop_event != nullptr && (e = hipEventRecordWithFlags(static_cast<hipEvent_t>(stop_event), s, hipEventRecordExternal)) != hipSuccess)
     return to_code(e);
   const double scale = site->site_scale;
   if (reduce != nullptr && g.ntile <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize
@@ -1375,77 +977,10 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
                             (double)site->grad_scale, total, nullptr, dslots, scratch, s);
 }
 
-int mi_linear_elbo_supported(const mi_linear* site, const mi_elbo* elbo, int* supported,
-                             size_t* elbo_workspace_bytes) {
-  if (!valid(site) || elbo == nullptr || supported == nullptr) return MI_EINVAL;
-  mi::LinFinish F{};
-  int64_t work = 0;
-  const int rc = finish_plan(site, elbo, geometry(site), F, &work);
-  if (rc == MI_EINVAL) return rc;
-  *supported = rc == 0 ? 1 : 0;
-  if (elbo_workspace_bytes != nullptr)
-    *elbo_workspace_bytes = rc == 0 ? MI_ELBO_COUNTER_BYTES + (size_t)work * sizeof(double) : 0;
-  return 0;
-}
-
-int mi_linear_elbo_forward(const mi_linear* site, const mi_elbo* elbo, void* workspace,
-                           size_t workspace_bytes, float* total, float* dslots, uint32_t* flags,
-                           void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                           const mi_adam* adam, void* start_event, void* stop_event,
-                           void* stream) {
-  if (!valid(site) || elbo == nullptr || total == nullptr || flags == nullptr || dslots == nullptr ||
-      loss == nullptr || elbo_workspace == nullptr)
-    return MI_EINVAL;
-  if (const int arc = mi::fused_adam_check(adam); arc != 0) return arc;
-  size_t need = 0;
-  mi_linear_workspace_bytes(site, &need);
-  if (workspace == nullptr || workspace_bytes < need) return MI_EWORKSPACE;
-  const Geometry g = geometry(site);
-  mi::LinFinish F{};
-  int64_t work = 0;
-  const int rc = finish_plan(site, elbo, g, F, &work);
-  if (rc != 0) return rc;
-  if (elbo->factors[0].source[0].ptr != dslots) return MI_EUNSUPPORTED;
-  if (elbo_workspace_bytes < MI_ELBO_COUNTER_BYTES + (size_t)work * sizeof(double)) return MI_EWORKSPACE;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e;
-  if (!(site->options & MI_GROUP_FLAGS_ZEROED)) {
-    e = hipMemsetAsync(flags, 0, sizeof(uint32_t), s);
-    if (e == hipSuccess && site->prior.present != 0)
-      e = hipMemsetAsync(site->prior.flags, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return to_code(e);
-  }
-  F.counters = static_cast<unsigned*>(elbo_workspace) + mi::kLinFinishCounterWord;
-  F.work = reinterpret_cast<double*>(static_cast<char*>(elbo_workspace) + MI_ELBO_COUNTER_BYTES);
-  F.loss = loss;
-  F.total = total;
-  F.dslots = dslots;
-  if (adam != nullptr) F.adam = *adam;
-  if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
-    return to_code(e);
-  float* part = static_cast<float*>(workspace);
-  if (site->family == MI_NORMAL)
-    launch<MI_NORMAL>(*site, g, part, flags, s, &F);
-  else
-    launch<MI_BERNOULLI_LOGITS>(*site, g, part, flags, s, &F);
-  e = hipGetLastError();
-  if (e != hipSuccess) return to_code(e);
-  if (stop_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s)) != hipSuccess)
-    return to_code(e);
-  return 0;
-}
-
-#if MI_FINISH_TIMING
-int mi_linear_finish_timing(unsigned long long* buffer) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(mi::mi_linfin_tbuf), &buffer, sizeof(buffer)) == hipSuccess
-             ? 0 : MI_EINVAL;
-}
-#endif
-
 int mi_linear_forward(const mi_linear* site, void* workspace, size_t workspace_bytes, float* total,
                       float* dslots, uint32_t* flags, void* stream) {
-  return mi_linear_forward_timed(site, workspace, workspace_bytes, total, dslots, flags, nullptr,
-                                 nullptr, stream);
+  return mi_linear_forward_deferred(site, workspace, workspace_bytes, total, dslots, flags, nullptr,
+                                    nullptr, stream, nullptr);
 }
 
 }  // extern "C"

@@ -23,7 +23,6 @@
 #include "beta_grad.hpp"
 #include "common.hpp"
 #include "entropy.hpp"
-#include "fin_timing.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -560,251 +559,8 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast(const mi_group G,
 // Partial sums: fp32 over at most 64 terms (as k_site_bcast), carried in fp64.
 typedef const __attribute__((address_space(4))) float smem_float;
 
-// ---- the ELBO forward finished by the BCAST launch (mi_group_elbo_forward) -------------------
-// The README model's step (README.md:40-69: theta ~ Beta(2, 2), x ~ Bernoulli(theta)[n], guide
-// Beta(c1, c0)) is this one launch plus the guide's draw: the site's partial slab (value: one
-// segment per chunk and particle; slot: the rank-one layout), the Beta draws' implicit-gradient
-// factors (the side job, same launch) and then mi_elbo_forward's reduction and tail. Here the
-// launch's last blocks run that tail (as linear.hip lin_finish for the regression):
-//   1. every block stores agent-coherent and takes an arrival ticket; the last `helpers` arrivals
-//      wait for the rest (bounded spin) and each sums one (particle chunk, segment chunk) job of
-//      the value slab into fp64;
-//   2. the last job of each particle chunk adds the chunk's job sums in a fixed order and writes
-//      its particles' totals and slot gradients (rank-one: f_k sum_c u_c + e_k), the chunk's loss
-//      share g0 sum_k total_k and its tail sums sum_k g_k dgrad_k;
-//   3. the last particle chunk adds the chunks' shares in a fixed order, adds the Beta entropy,
-//      writes the loss, the sums the backward reads (mi_factor.saved), the final gradients
-//      (MI_ELBO_FINAL_GRADS), the flag mirror and the generator step.
-struct BcastFinish {
-  unsigned* counters;     // [0] arrivals, [16] chunks done, [32 + kc] jobs done of chunk kc
-  double* work;           // [nkc][nsc][256] job sums, then [nkc][4] chunk shares
-  int helpers;            // blocks that stay to run the jobs: min(jobs, grid)
-  int jobs;               // nkc * nsc
-  int nsc;                // segment chunks
-  int nkc;                // particle chunks of 256
-  int64_t segc;           // segments per chunk
-  float* loss;
-  float* total;           // [K]
-  float* slot_grad;       // [K]
-  double site_scale;
-  double entropy_scale;
-  double weight;          // the factor's entropy weight
-  const float* c1;        // the factor's concentrations (one element)
-  const float* c0;
-  float* grad[2];         // d loss / d u_j (transform EXP) or d param_j, upstream 1
-  int32_t transform[2];
-  const double* dgrad;    // [K][2] (the side job's output)
-  double* saved;          // [4]: the forward's sums for mi_elbo_backward
-  uint64_t* step_counter;
-  uint64_t* step_snapshot;
-  const uint32_t* flags;
-  uint32_t* flags_mirror;
-  int64_t nflags;
-  mi_adam adam;           // num 0: no optimizer step in the launch
-};
-
-#if MI_FINISH_TIMING
-__device__ unsigned long long* mi_bcastfin_tbuf;
-#define MI_BF_STAMP(i) MI_FIN_STAMP(mi_bcastfin_tbuf, i)
-#else
-#define MI_BF_STAMP(i) do { } while (0)
-#endif
-
-template <bool COHERENT>
-MI_DEV void st_coh(float* p, float v) {
-  if constexpr (COHERENT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool COHERENT>
-MI_DEV void st_coh(double* p, double v) {
-  if constexpr (COHERENT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <typename T>
-MI_DEV T ld_coh(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Fixed-order block sum of three doubles (kBcastThreads lanes); the result on thread 0.
-MI_DEV void block_sum3(double (&v)[3], double (*red)[3]) {
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-#pragma unroll
-  for (int q = 0; q < 3; ++q) v[q] = wave_sum(v[q]);
-  __syncthreads();
-  if (lane == 0)
-#pragma unroll
-    for (int q = 0; q < 3; ++q) red[wave][q] = v[q];
-  __syncthreads();
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      double t = 0.0;
-      for (int w = 0; w < kBcastThreads / kWave; ++w) t += red[w][q];
-      v[q] = t;
-    }
-}
-
-MI_DEV void bcast_finish(const mi_group& G, const BcastFinish& F, const float* part, int64_t nseg,
-                         uint32_t* flags) {
-  __shared__ int role;
-  __shared__ double red[kBcastThreads];
-  __shared__ double red3[kBcastThreads / kWave][3];
-  const int tid = threadIdx.x;
-  const int64_t K = G.K;
-  MI_BF_STAMP(1);
-  __builtin_amdgcn_s_waitcnt(0);   // this thread's (agent-coherent) stores are complete
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned nb = gridDim.x;
-    const unsigned t = atomicAdd(F.counters, 1u);
-    MI_BF_STAMP(2);
-    int r = (t + (unsigned)F.helpers >= nb) ? (int)(t + (unsigned)F.helpers - nb) : -1;
-    if (r >= 0) {
-      // the blocks not yet arrived are running or about to be dispatched (they never wait); the
-      // count reaches nb -- bounded anyway, reported through the site's flag word
-      unsigned spins = 0;
-      while (__hip_atomic_load(F.counters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nb) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {
-          atomicOr(flags, MI_FLAG_INTERNAL);
-          break;
-        }
-      }
-    }
-    role = r;
-  }
-  __syncthreads();
-  const int h = role;
-  if (h < 0) return;
-  MI_BF_STAMP(3);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // jobs h, h + helpers, ... (a small launch has fewer blocks than jobs); a block completes a
-  // particle chunk's jobs -> its chunk stage; the block completing the last chunk -> the tail
-  bool final_block = false;
-  for (int job = h; job < F.jobs && !final_block; job += F.helpers) {
-    // ---- 1. job: particles [kc * 256, +256) over segments [sc * segc, +segc) ----------------
-    const int kc = job / F.nsc, sc = job - kc * F.nsc;
-    const int64_t k = (int64_t)kc * kBcastThreads + tid;
-    const int64_t kk = k < K ? k : K - 1;
-    {
-      const int64_t s0 = (int64_t)sc * F.segc, s1 = min(nseg, s0 + F.segc);
-      double acc = 0.0;
-      int64_t s = s0;
-      for (; s + 16 <= s1; s += 16) {
-        float x[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) x[j] = ld_coh(part + (s + j) * K + kk);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc += (double)x[j];
-      }
-      for (; s < s1; ++s) acc += (double)ld_coh(part + s * K + kk);
-      st_coh<true>(&F.work[((int64_t)kc * F.nsc + sc) * kBcastThreads + tid], acc);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned t = atomicAdd(F.counters + 32 + kc, 1u);
-      role = t == (unsigned)F.nsc - 1u ? 1 : -1;
-    }
-    __syncthreads();
-    if (role < 0) continue;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // ---- 2. the chunk's particles: totals, rank-one slot gradients, loss share, tail sums ------
-    const float* slot = part + nseg * K;   // value 1: u[0 .. nseg), then f[K], e[K]
-    double tot = 0.0;
-    for (int c = 0; c < F.nsc; ++c) tot += ld_coh(&F.work[((int64_t)kc * F.nsc + c) * kBcastThreads + tid]);
-    const float fk = ld_coh(slot + nseg + kk), ek = ld_coh(slot + nseg + K + kk);
-    const double dg0 = ld_coh(F.dgrad + 2 * kk), dg1 = ld_coh(F.dgrad + 2 * kk + 1);
-    double usum = 0.0;   // sum_c u_c in a fixed order: lanes over segments, then the block tree
-    for (int64_t c = tid; c < nseg; c += kBcastThreads) usum += (double)ld_coh(slot + c);
-    red[tid] = usum;
-    __syncthreads();
-    for (int half = kBcastThreads / 2; half > 0; half >>= 1) {
-      if (tid < half) red[tid] += red[tid + half];
-      __syncthreads();
-    }
-    const double U = red[0];
-    double v3[3] = {0.0, 0.0, 0.0};
-    if (k < K) {
-      const float tf = (float)(tot * F.site_scale);
-      const float gv = (float)(((double)fk * U + (double)ek) * (double)G.grad_scale);
-      F.total[k] = tf;
-      F.slot_grad[k] = gv;
-      v3[0] = (double)G.grad_scale * (double)tf;
-      if (gv != 0.0f) {   // a zero upstream never meets the factor (as mi_elbo_forward's tails)
-        v3[1] = (double)gv * dg0;
-        v3[2] = (double)gv * dg1;
-      }
-    }
-    block_sum3(v3, red3);
-    if (tid == 0) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        st_coh<true>(&F.work[(int64_t)F.nkc * F.nsc * kBcastThreads + kc * 4 + q], v3[q]);
-      __builtin_amdgcn_s_waitcnt(0);
-      __hip_atomic_store(F.counters + 32 + kc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned t = atomicAdd(F.counters + 16, 1u);
-      role = t == (unsigned)F.nkc - 1u ? 1 : -1;
-    }
-    __syncthreads();
-    final_block = role > 0;
-  }
-  MI_BF_STAMP(4);
-  if (!final_block) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  MI_BF_STAMP(5);
-  // ---- 3. the loss, the Beta factor's sums and final gradients, the step, the mirror ---------
-  const uint32_t fw = (int64_t)tid < F.nflags ? ld_coh(F.flags + tid) : 0u;
-  if (tid == 0) {
-    double sh = 0.0, s0 = 0.0, s1 = 0.0;
-    const double* shares = F.work + (int64_t)F.nkc * F.nsc * kBcastThreads;
-    for (int c = 0; c < F.nkc; ++c) {
-      sh += ld_coh(shares + c * 4);
-      s0 += ld_coh(shares + c * 4 + 1);
-      s1 += ld_coh(shares + c * 4 + 2);
-    }
-    const float a = *F.c1, b = *F.c0;
-    const double H = F.weight * beta_entropy(a, b);
-    *F.loss = (float)(sh - F.entropy_scale * H);
-    double h0, h1;
-    beta_entropy_grad(a, b, h0, h1);
-    F.saved[0] = s0;
-    F.saved[1] = s1;
-    F.saved[2] = h0;
-    F.saved[3] = h1;
-    // the gradients k_elbo_backward writes from `saved` for an upstream of 1
-    const double w = -(double)1.0f * F.entropy_scale * F.weight;
-    double g[2] = {(double)1.0f * s0 + w * h0, (double)1.0f * s1 + w * h1};
-    const float pv[2] = {a, b};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (F.grad[j] == nullptr) continue;
-      if (F.transform[j] == MI_TRANSFORM_EXP) g[j] *= (double)pv[j];
-      F.grad[j][0] = (float)g[j];
-    }
-    if (F.step_counter != nullptr) {
-      const uint64_t c0 = *F.step_counter;
-      *F.step_snapshot = c0;
-      *F.step_counter = c0 + 1u;
-    }
-    __hip_atomic_store(F.counters, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(F.counters + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if ((int64_t)tid < F.nflags) F.flags_mirror[tid] = fw;
-  for (int64_t i = tid + kBcastThreads; i < F.nflags; i += kBcastThreads)
-    F.flags_mirror[i] = ld_coh(F.flags + i);
-  MI_BF_STAMP(6);
-  if (F.adam.num > 0) {
-    // the optimizer step over the gradients thread 0 wrote: the training step ends here
-    __syncthreads();
-    adam_block<kBcastThreads>(F.adam);
-  }
-  MI_BF_STAMP(7);
-}
-
 // One workgroup of a group's side job (mi_side): the mi_beta_dgrad factors of 256 (draw, component)
 // pairs, one per thread -- latency-bound fp64 chains that run beside the site workgroups.
-template <bool COHERENT = false>
 MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
   const int64_t t = b * kBcastThreads + threadIdx.x;
   if (t >= 2 * S.K * S.N) return;
@@ -814,7 +570,7 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
   const float tot = a + bb;  // concentration.sum(-1) in fp32, dirichlet.py:18
   const double psi_t = digamma((double)tot);
   const float xv = S.x[e];
-  st_coh<COHERENT>(&S.out[t],
+  S.out[t] = (
                    j == 0 ? dirichlet_grad(xv, a, tot, digamma((double)a), psi_t) * (double)(1.0f - xv)
                           : -dirichlet_grad(1.0f - xv, bb, tot, digamma((double)bb), psi_t) * (double)xv);
 }
@@ -830,35 +586,27 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // SUFF (MININF_AMD_BCAST_SUFFSTAT=1, a measurement of the floor, not the default): the
 // per-(particle, element) FMA loop replaced by its closed form l_k * sum_i x_i -- the same value
 // in exact arithmetic (C2's per-eval arithmetic is reducible).
-// FINISH: the launch also runs the ELBO forward (bcast_finish): every store another block reads
-// is agent-coherent, and every block (padding and side-job blocks too) takes an arrival ticket.
-template <int FAMILY, int kSmemP, int kSmemChunk, bool SUFF = false, bool FINISH = false>
+template <int FAMILY, int kSmemP, int kSmemChunk, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
                                                                    int mode,
-                                                                   uint32_t* __restrict__ flags,
-                                                                   const BcastFinish fin = {}) {
+                                                                   uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
   // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below); bit 2: L2
   // prefetch of the chunk
-  if constexpr (FINISH) MI_BF_STAMP(0);
   const int rank1 = mode & 1;
   const bool balance = (mode & 2) != 0;
   const int64_t chunks = nseg - 1;
   const int64_t padded = (chunks + 7) / 8 * 8;
   const int64_t b = blockIdx.x;
   if (b >= padded * gy) {   // workgroups past the chunks: the side job (mi_side)
-    beta_side_block<FINISH>(G.side, b - padded * gy);
-    if constexpr (FINISH) bcast_finish(G, fin, part, nseg, flags);
+    beta_side_block(G.side, b - padded * gy);
     return;
   }
   const int64_t c = (b / (8 * gy)) * 8 + b % 8;
   const int64_t kblock = (b / 8) % gy;
-  if (c >= chunks) {   // padding
-    if constexpr (FINISH) bcast_finish(G, fin, part, nseg, flags);
-    return;
-  }
+  if (c >= chunks) return;   // padding
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
   const int64_t i0 = c * kSmemChunk;
@@ -1012,13 +760,13 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int64_t extra = nseg - 1;
   uint32_t fl_prior = 0u;
   float* slot_part = part + (int64_t)(1 + slot_a) * nseg * K;   // (slot_a >= 0)
-  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0) st_coh<FINISH>(&slot_part[c], s_a);   // u[c]
+  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0) slot_part[c] = s_a;   // u[c]
 #pragma unroll
   for (int p = 0; p < kSmemP; ++p) {
     const int64_t k = kbase + p * kBcastThreads;
     if (k >= K) continue;
-    st_coh<FINISH>(&part[c * K + k], (float)acc[p]);
-    if (slot_a >= 0 && !rank1) st_coh<FINISH>(&slot_part[c * K + k], w * (s_a * dl[p]));
+    part[c * K + k] = (float)acc[p];
+    if (slot_a >= 0 && !rank1) slot_part[c * K + k] = w * (s_a * dl[p]);
     if (c == 0) {
       const float l = lg[p];
       const float t = expf(-fabsf(l));
@@ -1037,22 +785,21 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
         prior_d = pe.d[2];
         fl_prior |= (pe.param_bad ? MI_FLAG_PARAM : 0u) | (pe.support_bad ? MI_FLAG_SUPPORT : 0u);
       }
-      st_coh<FINISH>(&part[extra * K + k], (float)(-n * softplus) + prior_lp);
+      part[extra * K + k] = (float)(-n * softplus) + prior_lp;
       if (slot_a >= 0) {
         const float e = w * (float)(-n * sig * (double)dl[p]) + w * prior_d;
         if (rank1) {
-          st_coh<FINISH>(&slot_part[nseg + k], w * dl[p]);       // f[k]
-          st_coh<FINISH>(&slot_part[nseg + K + k], e);           // e[k]
+          slot_part[nseg + k] = w * dl[p];       // f[k]
+          slot_part[nseg + K + k] = e;           // e[k]
         } else {
-          st_coh<FINISH>(&slot_part[extra * K + k], e);
+          slot_part[extra * K + k] = e;
         }
       }
     }
   }
-  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0 && c == 0) st_coh<FINISH>(&slot_part[extra], 0.0f);
+  if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0 && c == 0) slot_part[extra] = 0.0f;
   publish_flags(flags, fl);
   if (G.prior.present != 0) publish_flags(G.prior.flags, fl_prior);
-  if constexpr (FINISH) bcast_finish(G, fin, part, nseg, flags);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1516,8 +1263,7 @@ bool smem_rank1(const mi_group* g, const Plan& p) {
 }
 
 template <int FAM>
-void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s,
-                 const mi::BcastFinish* fin = nullptr) {
+void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 block(mi::kBcastThreads);
   // p.grid = (chunks + side blocks, particle blocks): the kernel takes them as one XCD-aware
   // dimension (see k_site_bcast_smem)
@@ -1529,15 +1275,6 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
                     (env_int("MININF_AMD_BCAST_PREFETCH", 0) ? 4 : 0);
 #define MI_SMEM(P, CH) \
   hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, rank1, flags)
-  if (fin != nullptr) {   // (host-checked: the default variant)
-    if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
-      hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096, true, true>), grid, block, bcast_lds(),
-                         s, G, part, p.nseg, gy, rank1, flags, *fin);
-    else
-      hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096, false, true>), grid, block,
-                         bcast_lds(), s, G, part, p.nseg, gy, rank1, flags, *fin);
-    return;
-  }
   switch (smem_variant()) {
     case 1: MI_SMEM(8, 4096); break;
     case 2: MI_SMEM(4, 8192); break;
@@ -1595,69 +1332,6 @@ int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites
   return to_code(hipGetLastError());
 }
 
-namespace {
-
-// Counter words of the mi_elbo workspace (clear of mi_elbo_forward's and the linear finish's).
-constexpr int64_t kBcastFinishCounterWord = MI_ELBO_COUNTER_BYTES / sizeof(unsigned) - 128;
-
-// The ELBO-finishing launch (mi_group_elbo_forward) of `group` and `elbo`: 0 and the plan when
-// this launch can run the whole ELBO forward, else MI_EUNSUPPORTED.
-int bcast_finish_plan(const mi_group* group, const mi_elbo* E, const Plan& p, mi::BcastFinish& F,
-                      int64_t* work_doubles) {
-  if (env_int("MININF_AMD_GROUP_ELBO", 1) == 0) return MI_EUNSUPPORTED;
-  const mi_group& G = *group;
-  if (E == nullptr || p.shape != kBcast || !bcast_smem(group) || smem_variant() != 0 ||
-      G.num_sites != 1 || G.num_slots != 1 || !G.compute_grads || !smem_rank1(group, p) ||
-      G.side.out == nullptr || G.draw.operand != 0 ||
-      (G.sites[0].family != MI_BERNOULLI_LOGITS && G.sites[0].family != MI_BERNOULLI_PROBS))
-    return MI_EUNSUPPORTED;
-  if (G.prior.present != 0) {
-    int ok = 0;
-    mi_group_prior_supported(group, &ok);
-    if (!ok) return MI_EUNSUPPORTED;
-  }
-  const int64_t K = G.K;
-  if (E->K != K || E->num_terms != 0 || E->num_reduce != 0 || E->num_factors != 1) return MI_EUNSUPPORTED;
-  const mi_factor& Q = E->factors[0];
-  if (Q.family != MI_BETA || Q.draw_kind != MI_DRAW_SOURCES || Q.n != 1 || Q.num_sources != 1 ||
-      Q.source[0].stride_k != 1 || Q.dgrad != G.side.out || Q.saved == nullptr ||
-      Q.param[0] == nullptr || Q.param[1] == nullptr || !(Q.weight > 0.0) || G.side.N != 1 ||
-      G.side.K != K)
-    return MI_EUNSUPPORTED;
-  if (E->nflags < 0 || (E->flags_mirror != nullptr && E->flags == nullptr)) return MI_EINVAL;
-  const int64_t nkc = ceil_div(K, mi::kBcastThreads);
-  const int64_t nsc = ceil_div(p.nseg, 16);   // 16 loads per helper thread
-  const int64_t chunks = p.nseg - 1;
-  const int64_t grid = ceil_div(chunks, 8) * 8 * p.grid.y + ((int64_t)p.grid.x - chunks);
-  if (nkc > 64) return MI_EUNSUPPORTED;
-  F = mi::BcastFinish{};
-  F.jobs = (int)(nkc * nsc);
-  F.helpers = (int)std::min<int64_t>({(int64_t)F.jobs, grid, (int64_t)1024});
-  F.nsc = (int)nsc;
-  F.nkc = (int)nkc;
-  F.segc = 16;
-  F.site_scale = G.sites[0].scale;
-  F.entropy_scale = E->entropy_scale;
-  F.weight = Q.weight;
-  F.c1 = Q.param[0];
-  F.c0 = Q.param[1];
-  for (int j = 0; j < 2; ++j) {
-    F.grad[j] = Q.grad[j];
-    F.transform[j] = Q.transform[j];
-  }
-  F.dgrad = Q.dgrad;
-  F.saved = Q.saved;
-  F.step_counter = E->step_counter;
-  F.step_snapshot = E->step_snapshot;
-  F.flags = E->flags;
-  F.flags_mirror = E->flags_mirror;
-  F.nflags = E->flags_mirror != nullptr ? E->nflags : 0;
-  *work_doubles = nkc * nsc * mi::kBcastThreads + nkc * 4;
-  return 0;
-}
-
-}  // namespace
-
 extern "C" {
 
 int mi_abi_version(char* target, size_t target_bytes) {
@@ -1705,15 +1379,8 @@ int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
 
 int mi_group_forward(const mi_group* group, void* workspace, size_t workspace_bytes, float* total,
                      double* site_lp, float* slot_grad, uint32_t* flags, void* stream) {
-  return mi_group_forward_timed(group, workspace, workspace_bytes, total, site_lp, slot_grad, flags,
-                                nullptr, nullptr, stream);
-}
-
-int mi_group_forward_timed(const mi_group* group, void* workspace, size_t workspace_bytes,
-                           float* total, double* site_lp, float* slot_grad, uint32_t* flags,
-                           void* start_event, void* stop_event, void* stream) {
   return mi_group_forward_deferred(group, workspace, workspace_bytes, total, site_lp, slot_grad,
-                                   flags, start_event, stop_event, stream, nullptr);
+                                   flags, nullptr, nullptr, stream, nullptr);
 }
 
 int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t workspace_bytes,
@@ -1770,7 +1437,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
     }
   }
   if (start_event != nullptr) {
-    e = hipEventRecord(static_cast<hipEvent_t>(start_event), s);
+    e = hipEventRecordWithFlags(static_cast<hipEvent_t>(start_event), s, hipEventRecordExternal);
     if (e != hipSuccess) return to_code(e);
   }
   switch (p.shape) {
@@ -1840,7 +1507,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   e = hipGetLastError();
   if (e != hipSuccess) return to_code(e);
   if (stop_event != nullptr) {
-    e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s);
+    e = hipEventRecordWithFlags(static_cast<hipEvent_t>(stop_event), s, hipEventRecordExternal);
     if (e != hipSuccess) return to_code(e);
   }
   if (draw_partials != nullptr && !(G.options & MI_GROUP_DRAW_PARTIALS)) {
@@ -1872,71 +1539,6 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   return mi_launch_finalize(part, prows, G.K, reduced_lp, G.num_slots, scales,
                             (double)G.grad_scale, total, site_lp, slot_grad, scratch, s,
                             rank1_mask);
-}
-
-#if MI_FINISH_TIMING
-int mi_group_finish_timing(unsigned long long* buffer) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(mi::mi_bcastfin_tbuf), &buffer, sizeof(buffer)) == hipSuccess
-             ? 0 : MI_EINVAL;
-}
-#endif
-
-int mi_group_elbo_supported(const mi_group* group, const mi_elbo* elbo, int* supported,
-                            size_t* elbo_workspace_bytes) {
-  if (!validate_group(group) || elbo == nullptr || supported == nullptr) return MI_EINVAL;
-  mi::BcastFinish F{};
-  int64_t work = 0;
-  const int rc = bcast_finish_plan(group, elbo, make_plan(group), F, &work);
-  if (rc == MI_EINVAL) return rc;
-  *supported = rc == 0 ? 1 : 0;
-  if (elbo_workspace_bytes != nullptr)
-    *elbo_workspace_bytes = rc == 0 ? MI_ELBO_COUNTER_BYTES + (size_t)work * sizeof(double) : 0;
-  return 0;
-}
-
-int mi_group_elbo_forward(const mi_group* group, const mi_elbo* elbo, void* workspace,
-                          size_t workspace_bytes, float* total, float* slot_grad, uint32_t* flags,
-                          void* elbo_workspace, size_t elbo_workspace_bytes, float* loss,
-                          const mi_adam* adam, void* start_event, void* stop_event,
-                          void* stream) {
-  if (!validate_group(group) || elbo == nullptr || total == nullptr || slot_grad == nullptr ||
-      flags == nullptr || loss == nullptr || elbo_workspace == nullptr)
-    return MI_EINVAL;
-  if (const int arc = mi::fused_adam_check(adam); arc != 0) return arc;
-  const Plan p = make_plan(group);
-  if (workspace == nullptr || workspace_bytes < ::workspace_bytes(group, p)) return MI_EWORKSPACE;
-  mi::BcastFinish F{};
-  int64_t work = 0;
-  const int rc = bcast_finish_plan(group, elbo, p, F, &work);
-  if (rc != 0) return rc;
-  if (elbo->factors[0].source[0].ptr != slot_grad) return MI_EUNSUPPORTED;
-  if (elbo_workspace_bytes < MI_ELBO_COUNTER_BYTES + (size_t)work * sizeof(double)) return MI_EWORKSPACE;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  hipError_t e = hipSuccess;
-  if (!(group->options & MI_GROUP_FLAGS_ZEROED)) {
-    e = hipMemsetAsync(flags, 0, sizeof(uint32_t) * group->num_sites, s);
-    if (e == hipSuccess && group->prior.present != 0)
-      e = hipMemsetAsync(group->prior.flags, 0, sizeof(uint32_t), s);
-    if (e != hipSuccess) return to_code(e);
-  }
-  F.counters = static_cast<unsigned*>(elbo_workspace) + kBcastFinishCounterWord;
-  F.work = reinterpret_cast<double*>(static_cast<char*>(elbo_workspace) + MI_ELBO_COUNTER_BYTES);
-  F.loss = loss;
-  F.total = total;
-  F.slot_grad = slot_grad;
-  if (adam != nullptr) F.adam = *adam;
-  if (start_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(start_event), s)) != hipSuccess)
-    return to_code(e);
-  float* part = static_cast<float*>(workspace);
-  if (group->sites[0].family == MI_BERNOULLI_PROBS)
-    launch_smem<MI_BERNOULLI_PROBS>(*group, p, part, flags, s, &F);
-  else
-    launch_smem<MI_BERNOULLI_LOGITS>(*group, p, part, flags, s, &F);
-  e = hipGetLastError();
-  if (e != hipSuccess) return to_code(e);
-  if (stop_event != nullptr && (e = hipEventRecord(static_cast<hipEvent_t>(stop_event), s)) != hipSuccess)
-    return to_code(e);
-  return 0;
 }
 
 int mi_reduce_launch(const mi_reduce* r, void* stream) {

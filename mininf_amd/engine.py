@@ -22,6 +22,7 @@ import ctypes
 import dataclasses
 import functools
 import os
+import sys
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -1380,8 +1381,6 @@ class _ElboPlan:
         self.cat_holders = [dict() for _ in categorical]
         self.flags: Optional[torch.Tensor] = None
         self.state = None
-        self.fused_linear = False   # the linear launch ran the ELBO forward (mi_linear_elbo_forward)
-        self.fused_group = False    # the group launch ran it (mi_group_elbo_forward)
         self.tensor_inputs: Optional[List[bool]] = None
         self.deferred_count = 0
         self.absorbed = absorbed or {}
@@ -1518,14 +1517,6 @@ class _ElboPlan:
             self.flags = zeroed[:words]
         else:
             self.flags = torch.zeros(words, dtype=torch.int32, device=self.device)
-        if self._linear_elbo_candidate():
-            loss = self._forward_linear_elbo()
-            if loss is not None:
-                return loss
-        if self._group_elbo_candidate():
-            loss = self._forward_group_elbo()
-            if loss is not None:
-                return loss
         cursor = len(self.categorical) + sum(len(l.flag_sites) for l in self.linears)
         # absorbed Beta draws whose implicit-gradient factors a site launch can carry (mi_side)
         side_jobs = [plan for plan in self.absorbed.values()
@@ -1670,7 +1661,7 @@ class _ElboPlan:
         # be handed to the allocations made before the launch (the optimizer's own descriptor).
         keep = (self, E, ws, loss, self.state, self.final, deferred, buffers)
         if self.final is None or not _defer_step(launch, "mi_elbo_forward", self.final, keep,
-                                                 self._elbo_adam(E)):
+                                                 self._elbo_adam(E), stream=(self.device, stream)):
             nat.check(launch(None), "mi_elbo_forward")
         return loss
 
@@ -1710,97 +1701,6 @@ class _ElboPlan:
             return _elbo_adam_device(desc, device) if ok.value else None
         return adapt
 
-    def _linear_elbo_candidate(self) -> bool:
-        """
-        The step is one linear site over the guide's one Normal factor that its launch draws
-        (examples/minibatch.md:76-88): the launch may run the whole ELBO forward
-        (mi_linear_elbo_forward; the library decides; opt-in, MININF_AMD_LINEAR_ELBO=1: measured
-        slower than the two-launch path).
-        """
-        if len(self.linears) != 1 or self.launchers or self.categorical or self.fallback or \
-                self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
-            return False
-        linear = self.linears[0]
-        return (linear.draw is not None and not linear.draw.done and linear.needs_grads() and
-                ("lin_theta", 0) in self.skip_lin and
-                os.environ.get("MININF_AMD_LINEAR_ELBO", "0") == "1" and
-                os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
-
-    def _forward_linear_elbo(self) -> Optional[torch.Tensor]:
-        """
-        The linear site's launch with the ELBO forward finished by its last blocks: one kernel
-        for the whole forward (and, with the final gradients, the whole backward). None (nothing
-        launched) when the library does not take this step.
-        """
-        device, lib = self.device, nat.lib()
-        linear, holder = self.linears[0], self.lin_holders[0]
-        flags = self.flags[:len(linear.flag_sites)]
-        L = linear.describe(True)
-        L.options |= nat.GROUP_FLAGS_ZEROED
-        if linear.prior is not None:   # its word after the site's
-            L.prior.flags = flags.data_ptr() + 4
-        size = ctypes.c_size_t()
-        nat.check(lib.mi_linear_workspace_bytes(ctypes.byref(L), ctypes.byref(size)),
-                  "mi_linear_workspace_bytes")
-        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
-        total = torch.empty(self.K, dtype=torch.float32, device=device)
-        nslots = linear.P + (1 if L.scale else 0)
-        dslots = torch.empty((nslots, self.K), dtype=torch.float32, device=device)
-        buffers = []
-        if nslots > linear.P and ("lin_sigma", 0) not in self.skip_lin:
-            buffers.append(dslots[linear.P:])
-        E = self._describe([], buffers, fill=False)   # (the launch writes the factor's scale)
-        self._describe_absorbed(E, [], [dslots])
-        if self.step_words is not None:
-            E.step_counter = self.step_words[0].data_ptr()
-            E.step_snapshot = self.step_words[1].data_ptr()
-        if self.mirror is not None:
-            E.flags = self.flags.data_ptr()
-            E.flags_mirror = self.mirror.data_ptr()
-            E.nflags = min(self.flags.numel(), self.mirror.numel())
-        final = self._factor_grads(E)
-        E.options |= nat.ELBO_FINAL_GRADS
-        supported, need = ctypes.c_int(0), ctypes.c_size_t()
-        nat.check(lib.mi_linear_elbo_supported(ctypes.byref(L), ctypes.byref(E),
-                                               ctypes.byref(supported), ctypes.byref(need)),
-                  "mi_linear_elbo_supported")
-        if not supported.value:
-            return None
-        elbo_need = ctypes.c_size_t()
-        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(elbo_need)),
-                  "mi_elbo_workspace_bytes")   # (the backward of a non-unit upstream uses it)
-        ws = _elbo_workspace(device, max(need.value, elbo_need.value))
-        loss = torch.empty((), dtype=torch.float32, device=device)
-        start = stop = None
-        if KERNEL_TIMER is not None:
-            start, stop = KERNEL_TIMER.pair(linear)
-        head = (ctypes.byref(L), ctypes.byref(E), workspace.data_ptr(), size.value,
-                total.data_ptr(), dslots.data_ptr(), flags.data_ptr(), ws.data_ptr(), ws.numel(),
-                loss.data_ptr())
-        tail = (None if start is None else start.cuda_event,
-                None if stop is None else stop.cuda_event, nat.stream_handle(device))
-
-        def launch(adam):
-            return lib.mi_linear_elbo_forward(*head, None if adam is None else ctypes.byref(adam),
-                                              *tail)
-        if not _defer_step(launch, "mi_linear_elbo_forward", final,
-                           (self, L, E, workspace, total, dslots, ws, loss, final)):
-            code = launch(None)
-            if code == nat.MI_EUNSUPPORTED:
-                return None
-            nat.check(code, "mi_linear_elbo_forward")
-        guide.take_draw(linear.draw)
-        linear.drew_theta = True
-        if L.rows.counter:
-            linear.batch.rows_taken()
-            linear.drew_rows = True
-        linear.reduce, linear.workspace = None, workspace
-        holder["flags"] = flags
-        self.final = final
-        self.fused_linear = True
-        self.state = (E, [], [], [dslots], [], [])
-        return loss
-
     def fusions(self) -> Dict[str, int]:
         """
         Which fast paths this evaluation took (structural patterns the planner recognised; a model
@@ -1810,9 +1710,7 @@ class _ElboPlan:
         (mi_linear.draw) / their minibatch rows (mi_rows) themselves; fused_draws: Normal guide
         factors drawn in registers by the site programs (mi_draw); deferred_reductions: site
         reductions finished by the ELBO forward; final_grads: the forward wrote the guide
-        gradients (no backward launch for loss.backward()); linear_elbo / group_elbo: the site
-        launch ran the whole ELBO forward (mi_linear_elbo_forward / mi_group_elbo_forward);
-        optimizer_step: the Adam step ran in the held launch's last block (no launch of its own).
+        gradients (no backward launch for loss.backward()); optimizer_step: the Adam step ran in the held launch's last block (no launch of its own).
         """
         return {
             "folded_priors": sum(l.prior is not None for l in self.launchers) +
@@ -1822,114 +1720,8 @@ class _ElboPlan:
             "fused_draws": sum(p.kind == nat.DRAW_PARTIALS for p in self.absorbed.values()),
             "deferred_reductions": self.deferred_count,
             "final_grads": int(getattr(self, "final", None) is not None),
-            "linear_elbo": int(self.fused_linear),
-            "group_elbo": int(self.fused_group),
             "optimizer_step": 0,   # set when the optimizer step joins the held launch
         }
-
-    def _group_elbo_candidate(self) -> bool:
-        """
-        The step is one site group over the guide's one one-element Beta factor whose draws only
-        that group reads (the README model, README.md:40-69): its launch may run the whole ELBO
-        forward (mi_group_elbo_forward; the library decides; opt-in, MININF_AMD_GROUP_ELBO=1: measured
-        slower than the two-launch path).
-        """
-        if len(self.launchers) != 1 or self.linears or self.categorical or self.fallback or \
-                self.recompute or len(self.factors) != 1 or 0 not in self.absorbed:
-            return False
-        plan = self.absorbed[0]
-        return (self.factors[0].family == nat.BETA and plan.kind == nat.DRAW_SOURCES and
-                plan.drawn is not None and plan.drawn.conc is not None and
-                plan.drawn.dgrad is None and self.factors[0].n == 1 and
-                os.environ.get("MININF_AMD_BETA_SIDE", "1") != "0" and
-                os.environ.get("MININF_AMD_GROUP_ELBO", "0") == "1" and
-                os.environ.get("MININF_AMD_FINAL_GRADS", "1") != "0")
-
-    def _forward_group_elbo(self) -> Optional[torch.Tensor]:
-        """
-        The site group's launch with the ELBO forward finished by its last blocks (the Beta
-        draws' implicit-gradient factors as the launch's side job): one kernel after the guide's
-        draw. None (nothing launched) when the library does not take this step.
-        """
-        device, lib = self.device, nat.lib()
-        launcher, holder = self.launchers[0], self.holders[0]
-        plan = self.absorbed[0]
-        K, N = launcher.K, launcher.N
-        if not any(op.mode != nat.GRAD_NONE for op in launcher.operands):
-            return None
-        flags = self.flags[:len(launcher.flag_sites)]
-        launcher.exp_pending = None
-        group, grads = launcher.describe(True, fuse_exp=True)
-        if launcher.exp_pending is not None or any(g is not None for g in grads):
-            return None   # (dense operands or a fused draw: not the BCAST shape)
-        group.options |= nat.GROUP_FLAGS_ZEROED
-        if launcher.prior is not None:   # its word after the group's own
-            group.prior.flags = flags.data_ptr() + 4 * len(launcher.sites)
-        x = plan.drawn.base.reshape(self.K, plan.drawn.N)
-        conc = plan.drawn.conc
-        side_out = torch.empty((x.shape[0], x.shape[1], 2), dtype=torch.float64, device=device)
-        sd = group.side
-        sd.x, sd.c1, sd.c1_stride = x.data_ptr(), conc.data_ptr(), 2
-        sd.c0, sd.c0_stride = conc.data_ptr() + 4, 2
-        sd.K, sd.N, sd.out = x.shape[0], x.shape[1], side_out.data_ptr()
-        size = ctypes.c_size_t()
-        nat.check(lib.mi_group_workspace_bytes(ctypes.byref(group), ctypes.byref(size)),
-                  "mi_group_workspace_bytes")
-        workspace = torch.empty(max(1, size.value), dtype=torch.uint8, device=device)
-        total = torch.empty(K, dtype=torch.float32, device=device)
-        slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
-        plan.side_dgrad = side_out
-        E = self._describe([], [], fill=False)   # (the draw wrote the concentrations)
-        self._describe_absorbed(E, [(grads, slot_grad, workspace)], [])
-        if self.step_words is not None:
-            E.step_counter = self.step_words[0].data_ptr()
-            E.step_snapshot = self.step_words[1].data_ptr()
-        if self.mirror is not None:
-            E.flags = self.flags.data_ptr()
-            E.flags_mirror = self.mirror.data_ptr()
-            E.nflags = min(self.flags.numel(), self.mirror.numel())
-        final = self._factor_grads(E)
-        E.options |= nat.ELBO_FINAL_GRADS
-        supported, need = ctypes.c_int(0), ctypes.c_size_t()
-        nat.check(lib.mi_group_elbo_supported(ctypes.byref(group), ctypes.byref(E),
-                                              ctypes.byref(supported), ctypes.byref(need)),
-                  "mi_group_elbo_supported")
-        if not supported.value:
-            plan.side_dgrad = None
-            return None
-        elbo_need = ctypes.c_size_t()
-        nat.check(lib.mi_elbo_workspace_bytes(ctypes.byref(E), ctypes.byref(elbo_need)),
-                  "mi_elbo_workspace_bytes")   # (the backward of a non-unit upstream uses it)
-        ws = _elbo_workspace(device, max(need.value, elbo_need.value))
-        loss = torch.empty((), dtype=torch.float32, device=device)
-        start = stop = None
-        if KERNEL_TIMER is not None:
-            start, stop = KERNEL_TIMER.pair(launcher)
-        guide.join_side()
-        head = (ctypes.byref(group), ctypes.byref(E), workspace.data_ptr(), size.value,
-                total.data_ptr(), slot_grad.data_ptr(), flags.data_ptr(), ws.data_ptr(),
-                ws.numel(), loss.data_ptr())
-        tail = (None if start is None else start.cuda_event,
-                None if stop is None else stop.cuda_event, nat.stream_handle(device))
-
-        def launch(adam):
-            return lib.mi_group_elbo_forward(*head, None if adam is None else ctypes.byref(adam),
-                                             *tail)
-        if not _defer_step(launch, "mi_group_elbo_forward", final,
-                           (self, group, E, workspace, total, slot_grad, side_out, ws, loss,
-                            final)):
-            code = launch(None)
-            if code == nat.MI_EUNSUPPORTED:
-                plan.side_dgrad = None
-                return None
-            nat.check(code, "mi_group_elbo_forward")
-        launcher.reduce, launcher.workspace, launcher.side_out = None, workspace, side_out
-        launcher.partials = None
-        holder["flags"], holder["site_lp"] = flags, None
-        self.final = final
-        self.fused_group = True
-        self.state = (E, [(grads, slot_grad, workspace)], [], [], [], [])
-        return loss
 
     def _reduce_ok(self) -> bool:
         """
@@ -2048,11 +1840,11 @@ def _is_unit_seed(u: torch.Tensor) -> bool:
 
 
 # ---- the step-finishing launch held for the optimizer --------------------------------------------
-# A finishing launch (mi_linear_elbo_forward / mi_group_elbo_forward) writes the loss and the guide
-# gradients of loss.backward() itself; the step's only other kernel is the optimizer's. The launch
-# is therefore held (not enqueued) until its first consumer: when that is the Adam step over its
-# gradients (mininf_amd.optim.Adam), the launch runs the update in its last block (ABI 14) and the
-# whole training step is ONE kernel. Any other consumer enqueues it first, as it would have been:
+# The ELBO forward that writes the final guide gradients of loss.backward() itself (mi_elbo_forward
+# with MI_ELBO_FINAL_GRADS) is the step's last kernel before the optimizer's. The launch is therefore
+# held (not enqueued) until its first consumer: when that is the Adam step over its gradients
+# (mininf_amd.optim.Adam), the launch runs the update in its last block (mi_elbo_forward_adam) and
+# the optimizer has no launch of its own. Any other consumer enqueues it first, as it would have been:
 # every native launch (_native.stream_handle), every torch operation on the loss (nn._Loss) or on
 # a held gradient (PendingGrad) other than metadata queries, the validation read, graph capture
 # boundaries (graph.StepGraph) and the distributed gradient reductions. MININF_AMD_DEFER_STEP=0
@@ -2063,19 +1855,41 @@ _PENDING: Optional["_PendingStep"] = None
 # queries that read no tensor data (they run before the launch without flushing it)
 _NO_FLUSH = frozenset({
     torch.Tensor.dim, torch.Tensor.size, torch.Tensor.numel, torch.Tensor.nelement,
-    torch.Tensor.is_contiguous, torch.Tensor.data_ptr, torch.Tensor.stride,
+    torch.Tensor.is_contiguous, torch.Tensor.stride,
     torch.Tensor.storage_offset, torch.Tensor.element_size, torch.Tensor.is_floating_point,
     torch.Tensor.is_complex, torch.Tensor.get_device, torch.Tensor.ndimension,
     torch.Tensor.requires_grad_})
 # tensor-valued properties (everything else read through a property is metadata)
 _DATA_PROPERTIES = frozenset({"data", "T", "mT", "H", "mH", "real", "imag", "grad", "_base"})
+# properties that hand the device address to another library (CuPy, numba, ...), which then reads
+# the data on its own: the launch that writes it must be enqueued first
+_RAW_POINTER_PROPERTIES = tuple(p for p in (torch.Tensor.__dict__.get("__cuda_array_interface__"),)
+                                if p is not None)
+
+
+def _called_from_package() -> bool:
+    """Whether the Python code asking (the first frame outside this module's flush machinery) is
+    mininf_amd's own: the package reads gradient addresses to describe launches that the stream
+    orders after the held one, so those reads need no flush."""
+    frame = sys._getframe(1)
+    while frame is not None and frame.f_globals.get("__name__") == __name__:
+        frame = frame.f_back
+    name = frame.f_globals.get("__name__", "") if frame is not None else ""
+    return name == "mininf_amd" or name.startswith("mininf_amd.")
 
 
 def _flushes(func) -> bool:
+    if func is torch.Tensor.data_ptr:
+        # a raw address read by user code (ctypes, a DDP-like hook, another kernel library) is a
+        # data use the stream does not see; the package's own descriptor reads are not
+        return not _called_from_package()
     if func in _NO_FLUSH:
         return False
     if getattr(func, "__name__", None) == "__get__":
-        return getattr(getattr(func, "__self__", None), "__name__", None) in _DATA_PROPERTIES
+        owner = getattr(func, "__self__", None)
+        if any(owner is p for p in _RAW_POINTER_PROPERTIES):
+            return True
+        return getattr(owner, "__name__", None) in _DATA_PROPERTIES
     return True
 
 
@@ -2096,8 +1910,13 @@ class PendingGrad(torch.Tensor):
                                      torch_function_flush(func, types, args, kwargs))
 
 
+def _current_stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 class _PendingStep:
-    def __init__(self, launch, what: str, grads: List[torch.Tensor], keep, adapter) -> None:
+    def __init__(self, launch, what: str, grads: List[torch.Tensor], keep, adapter,
+                 stream=None) -> None:
         self._launch = launch        # launch(optimizer argument or None) -> error code
         self.what = what
         # the site launches that finish the ELBO write the step's validation words themselves;
@@ -2107,6 +1926,13 @@ class _PendingStep:
         self.held: List[Tuple[torch.Tensor, torch.Tensor]] = []   # (param, PendingGrad)
         self._keep = keep            # the launch's buffers, alive until it has run
         self.adapt = adapter         # adapter(mi_adam descriptor) -> launch argument, or None
+        # (device, hipStream_t) the launch is enqueued on: the stream current at the forward
+        self.stream = stream
+
+    def other_stream(self) -> bool:
+        """Whether the stream current now is not the one the launch goes to (a consumer inside
+        ``torch.cuda.stream(side)``)."""
+        return self.stream is not None and _current_stream(self.stream[0]) != self.stream[1]
 
     def hold(self, var: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
         """``grad`` as the PendingGrad to assign to ``var.grad``."""
@@ -2116,6 +1942,13 @@ class _PendingStep:
 
     def run(self, adam=None) -> None:
         code = self._launch(adam)
+        if code == 0 and self.other_stream():
+            # the consumer's stream waits for the launch (a wait_stream recorded before this flush
+            # could not have seen it)
+            device, handle = self.stream
+            done = torch.cuda.Event()
+            done.record(torch.cuda.ExternalStream(handle, device=device))
+            torch.cuda.current_stream(device).wait_event(done)
         self._keep = None
         for var, held in self.held:   # the gradients are ordinary tensors from here on
             if var.grad is held:
@@ -2154,6 +1987,11 @@ def attach_optimizer(adam, grads: Sequence[torch.Tensor]) -> bool:
     step = _PENDING
     if step is None or adam.num < 1 or not any(g.data_ptr() in step.grad_ptrs for g in grads):
         return False
+    if step.other_stream():
+        # an optimizer stepping on another stream than the forward's: the launch runs first (the
+        # current stream waits for it), the step on its own
+        flush_pending_step()
+        return False
     arg = step.adapt(adam)
     if arg is None:
         return False
@@ -2172,14 +2010,15 @@ def _small_adam(adam):
     return adam if numel <= _FUSED_ADAM_MAX_NUMEL else None
 
 
-def _defer_step(launch, what: str, grads, keep, adapter=_small_adam) -> bool:
-    """Hold ``launch`` for the optimizer (True), or False: the caller launches now."""
+def _defer_step(launch, what: str, grads, keep, adapter=_small_adam, stream=None) -> bool:
+    """Hold ``launch`` for the optimizer (True), or False: the caller launches now. ``stream``:
+    (device, hipStream_t) the launch goes to, for consumers on other streams."""
     global _PENDING
     if os.environ.get("MININF_AMD_DEFER_STEP", "1") == "0":
         return False
     flush_pending_step()
     _PENDING = _PendingStep(launch, what, [g for gs in grads for g in gs if g is not None], keep,
-                            adapter)
+                            adapter, stream)
     return True
 
 

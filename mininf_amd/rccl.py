@@ -20,6 +20,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from . import _native as native
+
 NCCL_UNIQUE_ID_BYTES = 128
 NCCL_SUM = 0                                      # ncclRedOp_t (rccl.h)
 _DTYPES = {torch.float32: 7, torch.float64: 8}    # ncclFloat32, ncclFloat64
@@ -92,7 +94,9 @@ class Communicator:
                 tensor.dtype not in _DTYPES:
             raise ValueError("all_reduce takes a contiguous float32/float64 tensor on the "
                              f"communicator's device {self.device}")
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        # through the launch hook: a held step-finishing launch (engine._PendingStep) that writes
+        # `tensor` -- a guide gradient passed here directly -- is enqueued before the collective
+        stream = native.stream_handle(self.device)
         _check(library().ncclAllReduce(tensor.data_ptr(), tensor.data_ptr(), tensor.numel(),
                                        _DTYPES[tensor.dtype], NCCL_SUM, self.comm, stream),
                "ncclAllReduce")

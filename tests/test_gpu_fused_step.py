@@ -1,10 +1,8 @@
 """
-The optimizer step inside the step's last launch (ABI 14): the launch that writes the final guide
-gradients -- the ELBO forward (mi_elbo_forward_adam, the default) or, opt-in, the site launch that
-finishes the ELBO itself (mi_linear_elbo_forward for the minibatch regression,
-examples/minibatch.md:76-88; mi_group_elbo_forward for the README model, README.md:40-69) -- is held
-until the Adam step over its gradients, which then runs in that launch's last block
-(csrc/adam_math.hpp, torch's fused-Adam arithmetic).
+The optimizer step inside the step's last launch (ABI 14): the ELBO forward that writes the final
+guide gradients (mi_elbo_forward_adam; the minibatch regression, examples/minibatch.md:76-88, and
+the README model, README.md:40-69) is held until the Adam step over its gradients, which then runs
+in that launch's last block (csrc/adam_math.hpp, torch's fused-Adam arithmetic).
 
 * parameters and losses are BIT-identical to the held-off path (MININF_AMD_DEFER_STEP=0: the
   finishing launch, then mi_adam_step) over several steps, eager and captured, and mi_adam_step
@@ -106,16 +104,6 @@ def _hierarchical(device, validate=False, n=4096, K=128):
 
 
 MODELS = {"regression": _regression, "coin": _coin, "hierarchical": _hierarchical}
-FINISH = {"regression": ("MININF_AMD_LINEAR_ELBO", "mi_linear_elbo_forward"),
-          "coin": ("MININF_AMD_GROUP_ELBO", "mi_group_elbo_forward")}
-PATHS = ["elbo", "finish"]
-
-
-def _path(monkeypatch, name, path):
-    """The held launch: the ELBO forward (default) or the site launch finishing the ELBO."""
-    env, fn = FINISH[name]
-    monkeypatch.setenv(env, "1" if path == "finish" else "0")
-    return fn if path == "finish" else "mi_elbo_forward_adam"
 
 
 def _train(device, monkeypatch, name, held, steps=4, between=None, optimizer_cls=Adam,
@@ -138,33 +126,26 @@ def _train(device, monkeypatch, name, held, steps=4, between=None, optimizer_cls
         loss_fn.last_fusions
 
 
-@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_step_joins_the_held_launch(device, monkeypatch, name, path):
-    fn = _path(monkeypatch, name, path)
+def test_step_joins_the_held_launch(device, monkeypatch, name):
     adam = _spy(monkeypatch, "mi_adam_step")
-    fused = _spy(monkeypatch, fn)
+    fused = _spy(monkeypatch, "mi_elbo_forward_adam")
     losses, params, fusions = _train(device, monkeypatch, name, held=True)
     assert adam == [], "the optimizer step ran in the held launch"
     assert len(fused) == 4
-    if path == "finish":
-        assert all(call[10] is not None for call in fused)
-        assert fusions["linear_elbo" if name == "regression" else "group_elbo"] == 1
     assert fusions["optimizer_step"] == 1
     adam.clear()
     fused.clear()
     ref_losses, ref_params, ref_fusions = _train(device, monkeypatch, name, held=False)
     assert len(adam) == 4 and ref_fusions["optimizer_step"] == 0
-    assert all(call[10] is None for call in fused) if path == "finish" else fused == []
+    assert fused == []
     assert torch.equal(losses, ref_losses)
     for a, b in zip(params, ref_params):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name, path):
-    _path(monkeypatch, name, path)
+def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name):
     ref_losses, ref_params, _ = _train(device, monkeypatch, name, held=False, steps=9)
     monkeypatch.setenv("MININF_AMD_DEFER_STEP", "1")
     module, loss_fn, approx, conditioned = MODELS[name](device, validate=True)
@@ -187,11 +168,9 @@ def test_captured_joined_steps_match_held_off_steps(device, monkeypatch, name, p
         assert torch.equal(a.detach(), b)
 
 
-@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", ["regression", "coin"])
-def test_consumers_between_backward_and_step(device, monkeypatch, name, path):
+def test_consumers_between_backward_and_step(device, monkeypatch, name):
     """Gradient clipping reads the held gradients: the launch runs first, the step on its own."""
-    _path(monkeypatch, name, path)
 
     def clip(module):
         torch.nn.utils.clip_grad_norm_(module.parameters(), 0.5)
@@ -249,7 +228,6 @@ def test_validated_step_joins_the_held_launch(device, monkeypatch, name):
     """With validation on, the loss reads the step's validation words before returning: that read
     waits for the site launches only -- the held ELBO forward (which writes no word) stays held and
     the optimizer step still joins it. Results equal the held-off path bit for bit."""
-    _path(monkeypatch, name, "elbo")
     adam = _spy(monkeypatch, "mi_adam_step")
     losses, params, fusions = _train(device, monkeypatch, name, held=True, validate=True)
     assert adam == [] and fusions["optimizer_step"] == 1
@@ -259,49 +237,63 @@ def test_validated_step_joins_the_held_launch(device, monkeypatch, name):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("validate", [False, True])
-def test_fused_draw_factor_steps_in_its_final_gradient_blocks(device, monkeypatch, validate):
-    """A fused-draw factor (10^3+ elements) is updated by the ELBO forward blocks that write its
-    final gradients, the one-element factor by the last block: no optimizer launch, parameters,
-    moments and losses bit-identical to the held-off path; the step counts advance once per
-    step (the last of the factor's blocks to read a count advances it). Opt-in
-    (MININF_AMD_ELBO_FIN_ADAM=1: measured slower than Adam's own launch on C5)."""
-    monkeypatch.setenv("MININF_AMD_ELBO_FIN_ADAM", "1")
-    adam = _spy(monkeypatch, "mi_adam_step")
-    fused = _spy(monkeypatch, "mi_elbo_forward_adam")
-    losses, params, fusions = _train(device, monkeypatch, "hierarchical", held=True, steps=5,
-                                     validate=validate)
-    assert adam == [] and fusions["optimizer_step"] == 1 and fusions["fused_draws"] == 1
-    assert len(fused) == 5 and all(call[4] is not None for call in fused)
-    ref_losses, ref_params, _ = _train(device, monkeypatch, "hierarchical", held=False, steps=5,
-                                       validate=validate)
+@pytest.mark.parametrize("name", ["regression", "coin"])
+def test_allocator_reuse_between_backward_and_step(device, monkeypatch, name):
+    """The round-4 fault's cause, pinned: between loss.backward() and
+    optimizer.step() the caching allocator hands out every free block of the sizes the held
+    launch's buffers have (the deferred reductions' [K] / [slots, K] outputs, partial slabs,
+    workspaces: 512 B .. 16 MB), filled with NaN and kept until after the step. Had the held
+    launch dropped one of its buffers, the fill would land in memory it reads, or its stores in a
+    NaN tensor: the steps are bit-identical to the held-off path and every NaN tensor is intact."""
+    def churn(junk):
+        def between(module):
+            for nbytes in [1 << j for j in range(9, 25)] * 3:
+                junk.append(torch.full((nbytes // 4,), float("nan"), device=device))
+        return between
+
+    junk: list = []
+    losses, params, fusions = _train(device, monkeypatch, name, held=True, between=churn(junk))
+    assert fusions["optimizer_step"] == 1
+    torch.cuda.synchronize()
+    assert all(bool(torch.isnan(t).all()) for t in junk), "a held launch wrote into freed memory"
+    ref_junk: list = []
+    ref_losses, ref_params, _ = _train(device, monkeypatch, name, held=False,
+                                       between=churn(ref_junk))
     assert torch.equal(losses, ref_losses)
     for a, b in zip(params, ref_params):
         assert torch.equal(a, b)
 
 
-def test_fused_draw_factor_steps_captured(device, monkeypatch):
-    """The same step captured (several steps per replay): the readers' words reset every step."""
-    monkeypatch.setenv("MININF_AMD_ELBO_FIN_ADAM", "1")
-    ref_losses, ref_params, _ = _train(device, monkeypatch, "hierarchical", held=False, steps=9)
-    monkeypatch.setenv("MININF_AMD_DEFER_STEP", "1")
-    module, loss_fn, approx, conditioned = _hierarchical(device, validate=True)
-    optimizer = Adam(module.parameters(), lr=0.02)
+def test_consumer_on_another_stream_waits_for_the_held_launch(device, monkeypatch):
+    """a consumer that reads the held gradients on a side stream after
+    side.wait_stream(main) -- recorded before anything flushed the held launch -- is ordered
+    after the launch (the flush makes the current stream wait), and an optimizer stepping on that
+    stream does not join it: results equal the held-off path."""
+    def run(held):
+        monkeypatch.setenv("MININF_AMD_DEFER_STEP", "1" if held else "0")
+        module, loss_fn, approx, conditioned = _coin(device)
+        optimizer = Adam(module.parameters(), lr=0.02)
+        side = torch.cuda.Stream()
+        grads, losses = [], []
+        for _ in range(3):
+            optimizer.zero_grad(set_to_none=True)
+            loss = loss_fn(conditioned(), approx())
+            loss.backward()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                grads.append([q.grad.clone() for q in module.parameters()])
+                optimizer.step()
+            torch.cuda.current_stream().wait_stream(side)
+            losses.append(loss.detach())
+        torch.cuda.synchronize()
+        assert engine.pending_step() is None
+        return torch.stack(losses).cpu(), grads, [q.detach().clone() for q in module.parameters()]
 
-    def step():
-        optimizer.zero_grad(set_to_none=True)
-        loss = loss_fn(conditioned(), approx())
-        loss.backward()
-        optimizer.step()
-        return loss
-
-    adam = _spy(monkeypatch, "mi_adam_step")
-    graph = StepGraph(step, warmup=3, repeat=3)
-    assert adam == []
-    losses = [float(graph()) for _ in range(2)]
-    graph.check()
-    assert losses[0] == float(ref_losses[5]) and losses[1] == float(ref_losses[8])
-    for a, b in zip(module.parameters(), ref_params):
-        assert torch.equal(a.detach(), b)
-    for state in optimizer.state.values():   # (every tensor's count, both factors)
-        assert float(state["step"]) == 9.0
+    losses, grads, params = run(True)
+    ref_losses, ref_grads, ref_params = run(False)
+    assert torch.equal(losses, ref_losses)
+    for a, b in zip(grads, ref_grads):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    for a, b in zip(params, ref_params):
+        assert torch.equal(a, b)

@@ -49,12 +49,32 @@ def test_metadata_does_not_flush_data_does():
     held = engine.pending_step().hold(torch.zeros(4, requires_grad=True), g)
     assert isinstance(held, engine.PendingGrad)
     _ = (held.shape, held.dtype, held.device, held.is_sparse, held.dim(), held.numel(),
-         held.is_contiguous(), held.data_ptr(), held.stride(), held.requires_grad)
+         held.is_contiguous(), held.stride(), held.requires_grad)
+    assert nat.ptr(held) == g.data_ptr()   # the package's own descriptor reads: no flush
     assert launch.calls == []
     assert torch.equal(held.clone(), torch.full((4,), 7.0))
     assert launch.calls == [None]
     held.sum()
     assert launch.calls == [None]   # once
+
+
+def test_raw_address_read_by_user_code_flushes():
+    """data_ptr() outside the package (ctypes, a DDP-like hook, CuPy) is a data use the stream
+    cannot see: the held launch is enqueued first."""
+    g = torch.zeros(4)
+    launch = _hold([g], [g])
+    held = engine.pending_step().hold(torch.zeros(4, requires_grad=True), g)
+    assert held.data_ptr() == g.data_ptr()
+    assert launch.calls == [None]
+
+
+def test_cuda_array_interface_flushes():
+    g = torch.zeros(4)
+    launch = _hold([g], [g])
+    held = engine.pending_step().hold(torch.zeros(4, requires_grad=True), g)
+    with pytest.raises((TypeError, AttributeError, RuntimeError)):
+        held.__cuda_array_interface__   # (a CPU tensor here: torch refuses after the flush)
+    assert launch.calls == [None]
 
 
 def test_loss_class_flushes_on_float():
@@ -120,8 +140,8 @@ def test_a_new_hold_flushes_the_previous_one():
 
 def test_failed_launch_raises_at_the_consumer():
     g = torch.zeros(1)
-    assert engine._defer_step(lambda adam: -3, "mi_linear_elbo_forward", [[g]], ())
-    with pytest.raises(nat.NativeError, match="mi_linear_elbo_forward failed: unsupported"):
+    assert engine._defer_step(lambda adam: -3, "mi_elbo_forward", [[g]], ())
+    with pytest.raises(nat.NativeError, match="mi_elbo_forward failed: unsupported"):
         engine.flush_pending_step()
 
 
@@ -141,6 +161,5 @@ def test_validation_read_flushes():
 
 def test_adam_descriptor_pointer_argument():
     # the ctypes prototypes take the descriptor by pointer (NULL: no optimizer step)
-    for name in ("mi_linear_elbo_forward", "mi_group_elbo_forward"):
-        argtypes = nat._SIGNATURES[name][1]
-        assert argtypes[10] is ctypes.POINTER(nat.Adam)
+    argtypes = nat._SIGNATURES["mi_elbo_adam_supported"][1]
+    assert argtypes[1] is ctypes.POINTER(nat.ElboAdam)
