@@ -1,7 +1,7 @@
 """
 Microbenchmark of the Bernoulli BCAST site kernel (C2's k_site_bcast_smem / k_site_bcast) through
 the engine's group launcher, over particle and element counts: mean kernel time (HIP events
-recorded by mi_group_forward_timed around the site kernel) and packed-FMA rate.
+recorded by mi_group_forward_deferred around the site kernel) and packed-FMA rate.
 
     python tools/bcast_bench.py           (MININF_AMD_BCAST_SMEM / _TUNE select the kernel)
 """

@@ -74,9 +74,9 @@ def main():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             b.record()
-            nat.check(lib.mi_linear_forward_timed(
+            nat.check(lib.mi_linear_forward_deferred(
                 ctypes.byref(L), work.data_ptr(), size.value, total.data_ptr(), dslots.data_ptr(),
-                flags.data_ptr(), a.cuda_event, b.cuda_event, stream), "fwd")
+                flags.data_ptr(), a.cuda_event, b.cuda_event, stream, None), "fwd")
             if rep >= 3:
                 times.append((a, b))
         torch.cuda.synchronize()
