@@ -243,6 +243,59 @@ void emit_site_eval2(std::ostringstream& o, const mi_group& g, int s, const std:
   o << in << "}\n";
 }
 
+
+// ---- accumulator forms (fused-draw packed loop) ----------------------------------------------
+// In the fused-draw row loop every site's per-element log density enters only the row's sum, so
+// instead of evaluating the full density per element (eval_*2: every role's derivative, the
+// constant terms, a select and an add per element) the loop accumulates what the density is
+// affine in, per element pair:
+//   Normal(loc, sigma) with sigma constant or per-particle: t = obs ? v - loc : 0, Sum t^2 (and
+//     Sum t when a per-particle role takes a slot gradient); per element the gradients are
+//     +-sigma^-2 t, one packed FMA into the dense target. The row's log density is
+//     -sigma^-2 / 2 Sum t^2 + n_obs (-log sigma - log sqrt(2 pi)), n_obs per lane being
+//     loop-invariant (the masks and the lane's validity do not change with the particle).
+//   Bernoulli(logits l): lp = v l - max(l, 0) - log(1 + exp(-|l|)) on the hardware exp / log / rcp,
+//     Sum obs ? lp : 0; d/dl = v - sigmoid(l).
+// Same formulas as device_math.hpp's eval_normal2 / eval_bernoulli_logits2 up to rounding order
+// (the constant terms are added once per row, not per element; log1p(t) is log(fl(1 + t)) without
+// eval_bernoulli_logits2's first-order correction for the rounding of 1 + t: an absolute error
+// below 2^-24 per element, far inside the 1e-5 relative tolerance of every ELBO and gradient).
+// The accumulator form applies when every site of the group qualifies (acc_form).
+bool acc_site(const mi_group& g, int s, int draw) {
+  const mi_site& st = g.sites[s];
+  if (st.mask != nullptr && kind_of(st.mask_stride_k, st.mask_stride_i) != kShared) return false;
+  auto op_kind = [&](int q) {
+    const int o = st.operand[q];
+    return o < 0 ? kConst : kind_of(g.operands[o].stride_k, g.operands[o].stride_i);
+  };
+  auto grad_of = [&](int q) {
+    const int o = st.operand[q];
+    return (o < 0 || !g.compute_grads) ? (int)MI_GRAD_NONE : (int)g.operands[o].grad_mode;
+  };
+  if (st.family == MI_NORMAL) {
+    const Kind ks = op_kind(1);
+    if (!(ks == kConst || ks == kParticle || ks == kBroadcast)) return false;
+    if (st.operand[0] >= 0 && st.operand[0] == st.operand[2]) return false;
+    for (int q = 0; q < 3; ++q)
+      if (st.operand[q] >= 0 && (st.operand[q] == st.operand[1]) && q != 1) return false;
+    if (grad_of(1) == MI_GRAD_DENSE) return false;
+    return true;
+  }
+  if (st.family == MI_BERNOULLI_LOGITS) {
+    if (grad_of(2) != MI_GRAD_NONE) return false;   // (a gradient w.r.t. the observed value)
+    return true;
+  }
+  return false;
+}
+
+bool acc_form(const mi_group& g, int draw) {
+  if (std::getenv("MININF_AMD_ACC_FORM") != nullptr && std::atoi(std::getenv("MININF_AMD_ACC_FORM")) == 0)
+    return false;
+  for (int s = 0; s < g.num_sites; ++s)
+    if (!acc_site(g, s, draw)) return false;
+  return true;
+}
+
 std::string generate(const mi_group& g, const PlanInfo& plan) {
   const bool row = plan.row;
   const int E = plan.elems;
@@ -496,6 +549,153 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   };
 
 
+  // ---- accumulator forms (acc_form): per-site code of the fused-draw packed loop -------------
+  auto site_str = [&](int s) { return std::to_string(s); };
+  auto role_expr = [&](int s, int q) -> std::string {
+    const mi_site& st = g.sites[s];
+    if (st.operand[q] < 0) return "c" + site_str(s) + "_" + std::to_string(q);
+    return operand_var(g, st.operand[q]);
+  };
+  auto site_obs = [&](int s, const std::string& valid) -> std::string {
+    const mi_site& st = g.sites[s];
+    std::string obs = valid;
+    if (st.mask != nullptr) obs = (valid == "true") ? mask_var(st, s) : "(" + valid + " && " + mask_var(st, s) + ")";
+    return obs;
+  };
+  auto role_grad = [&](int s, int q) -> int {
+    const int op = g.sites[s].operand[q];
+    if (op < 0 || !g.compute_grads || !role_used(g.sites[s].family, q)) return MI_GRAD_NONE;
+    return g.operands[op].grad_mode;
+  };
+  auto normal_scale_const = [&](int s) { return g.sites[s].operand[1] < 0; };
+  auto normal_needs_q1 = [&](int s) {
+    return role_grad(s, 0) == MI_GRAD_PARTICLE || role_grad(s, 2) == MI_GRAD_PARTICLE;
+  };
+  // loop-invariant per lane: observed-element counts, constant-scale factors, the constant
+  // parameters' checks
+  auto emit_acc_prologue = [&](const std::string& valid) {
+    const char* in = "    ";
+    for (int st = 0; st < g.num_sites; ++st) {
+      const std::string S = site_str(st);
+      o << in << "float cn" << S << " = 0.0f;\n#pragma unroll\n" << in << "for (int e = 0; e < " << E
+        << "; ++e) cn" << S << " += (" << site_obs(st, valid) << ") ? 1.0f : 0.0f;\n";
+      if (g.sites[st].family == MI_NORMAL && normal_scale_const(st)) {
+        const std::string sig = role_expr(st, 1);
+        o << in << "const float iv" << S << " = mi::rcp(" << sig << "), iq" << S << " = iv" << S << " * iv" << S
+          << ";\n" << in << "const float lc" << S << " = -(logf(" << sig << ") + mi::kHalfLog2Pi);\n"
+          << in << "pb" << S << " |= !(" << sig << " > 0.0f);\n";
+      }
+    }
+  };
+  // one row (particle k): the pairs' accumulations, then the row's lp<s> / sl<j> scalars
+  auto emit_acc_row = [&](const std::string& valid) {
+    const char* in2 = "      ";
+    for (int st = 0; st < g.num_sites; ++st) {
+      const std::string S = site_str(st);
+      if (g.sites[st].family == MI_NORMAL) {
+        if (!normal_scale_const(st)) {   // per-particle sigma: this row's factors
+          const std::string sig = role_expr(st, 1);
+          o << in2 << "const float iv" << S << " = mi::rcp(" << sig << "), iq" << S << " = iv" << S
+            << " * iv" << S << ";\n" << in2 << "const float lc" << S << " = -(logf(" << sig
+            << ") + mi::kHalfLog2Pi);\n" << in2 << "pb" << S << " |= !(" << sig << " > 0.0f);\n";
+        }
+        o << in2 << "mi::f2 qa" << S << " = mi::splat2(-0.0f);\n";
+        if (normal_needs_q1(st)) o << in2 << "mi::f2 qb" << S << " = mi::splat2(-0.0f);\n";
+        o << in2 << "const float kl" << S << " = scale" << S << " * iq" << S << ";\n";
+      } else {
+        o << in2 << "mi::f2 qa" << S << " = mi::splat2(-0.0f);\n";
+        if (role_grad(st, 0) == MI_GRAD_PARTICLE) o << in2 << "mi::f2 qb" << S << " = mi::splat2(-0.0f);\n";
+      }
+    }
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << in2 << "mi::f2 g" << op << "[" << E / 2 << "];\n";
+    o << in2 << "#pragma unroll\n" << in2 << "for (int h = 0; h < " << E / 2 << "; ++h) {\n";
+    const std::string in3 = std::string(in2) + "  ";
+    for (int op = 0; op < g.num_operands; ++op)
+      if (dense_grad(op)) o << in3 << "g" << op << "[h] = mi::splat2(-0.0f);\n";
+    for (int st = 0; st < g.num_sites; ++st) {
+      const std::string S = site_str(st);
+      const mi_site& site = g.sites[st];
+      const std::string obs = site_obs(st, valid);
+      const bool all = obs == "true";
+      const std::string o0 = at_pair(obs, 0), o1 = at_pair(obs, 1);
+      auto sel = [&](const std::string& x) {
+        return all ? x : "mi::f2{" + o0 + " ? " + x + ".x : 0.0f, " + o1 + " ? " + x + ".y : 0.0f}";
+      };
+      const std::string V = pair_role(role_expr(st, 2));
+      o << in3 << "{\n";
+      if (site.family == MI_NORMAL) {
+        const std::string L = pair_role(role_expr(st, 0));
+        o << in3 << "  const mi::f2 lv = " << L << ", vv = " << V << ";\n";
+        o << in3 << "  const mi::f2 df = vv - lv;\n";
+        o << in3 << "  const mi::f2 t = " << sel("df") << ";\n";
+        o << in3 << "  qa" << S << " = mi::fma2(t, t, qa" << S << ");\n";
+        if (normal_needs_q1(st)) o << in3 << "  qb" << S << " = qb" << S << " + t;\n";
+        o << in3 << "  pb" << S << " |= (lv.x != lv.x) | (lv.y != lv.y);\n";
+        o << in3 << "  sb" << S << " |= (" << o0 << " & (vv.x != vv.x)) | (" << o1 << " & (vv.y != vv.y));\n";
+        if (role_grad(st, 0) == MI_GRAD_DENSE)
+          o << in3 << "  g" << site.operand[0] << "[h] = mi::fma2(mi::splat2(kl" << S << "), t, g"
+            << site.operand[0] << "[h]);\n";
+        if (role_grad(st, 2) == MI_GRAD_DENSE)
+          o << in3 << "  g" << site.operand[2] << "[h] = mi::fma2(mi::splat2(-kl" << S << "), t, g"
+            << site.operand[2] << "[h]);\n";
+      } else {   // MI_BERNOULLI_LOGITS
+        const std::string L = pair_role(role_expr(st, 0));
+        o << in3 << "  const mi::f2 l = " << L << ", vv = " << V << ";\n";
+        o << in3 << "  const mi::f2 t = mi::f2{mi::fast_exp(-fabsf(l.x)), mi::fast_exp(-fabsf(l.y))};\n";
+        o << in3 << "  const mi::f2 u = 1.0f + t;\n";
+        o << in3 << "  const mi::f2 r = mi::f2{mi::rcp(u.x), mi::rcp(u.y)};\n";
+        o << in3 << "  const mi::f2 lu = mi::f2{__builtin_amdgcn_logf(u.x), __builtin_amdgcn_logf(u.y)};\n";
+        o << in3 << "  const mi::f2 a = mi::fma2(l, vv, -mi::f2{fmaxf(l.x, 0.0f), fmaxf(l.y, 0.0f)});\n";
+        o << in3 << "  const mi::f2 lp = mi::fma2(lu, mi::splat2(-0.69314718055994531f), a);\n";
+        o << in3 << "  qa" << S << " = qa" << S << " + " << sel("lp") << ";\n";
+        if (role_grad(st, 0) != MI_GRAD_NONE) {
+          o << in3 << "  const mi::f2 tr = t * r;\n";
+          o << in3 << "  const mi::f2 dd = vv - mi::f2{l.x >= 0.0f ? r.x : tr.x, l.y >= 0.0f ? r.y : tr.y};\n";
+          o << in3 << "  const mi::f2 ds = " << sel("dd") << ";\n";
+          if (role_grad(st, 0) == MI_GRAD_DENSE)
+            o << in3 << "  g" << site.operand[0] << "[h] = mi::fma2(mi::splat2(scale" << S << "), ds, g"
+              << site.operand[0] << "[h]);\n";
+          else
+            o << in3 << "  qb" << S << " = qb" << S << " + ds;\n";
+        }
+        o << in3 << "  pb" << S << " |= (l.x != l.x) | (l.y != l.y);\n";
+        o << in3 << "  sb" << S << " |= (" << o0 << " & !((vv.x == 0.0f) | (vv.x == 1.0f))) | (" << o1
+          << " & !((vv.y == 0.0f) | (vv.y == 1.0f)));\n";
+      }
+      o << in3 << "}\n";
+    }
+    o << in2 << "}\n";
+    // the row's values: lp<s> per site, sl<j> per slot
+    for (int st = 0; st < g.num_sites; ++st) {
+      const std::string S = site_str(st);
+      if (g.sites[st].family == MI_NORMAL)
+        o << in2 << "const float lp" << S << " = fmaf(-0.5f * iq" << S << ", qa" << S << ".x + qa" << S
+          << ".y, cn" << S << " * lc" << S << ");\n";
+      else
+        o << in2 << "const float lp" << S << " = qa" << S << ".x + qa" << S << ".y;\n";
+    }
+    if (g.compute_grads)
+      for (int j = 0; j < g.num_slots; ++j) {
+        o << in2 << "float sl" << j << " = -0.0f;\n";
+        for (int st = 0; st < g.num_sites; ++st) {
+          const std::string S = site_str(st);
+          const mi_site& site = g.sites[st];
+          for (int q = 0; q < 3; ++q) {
+            if (role_grad(st, q) != MI_GRAD_PARTICLE || g.operands[site.operand[q]].slot != j) continue;
+            if (site.family == MI_NORMAL) {
+              if (q == 0) o << in2 << "sl" << j << " = fmaf(kl" << S << ", qb" << S << ".x + qb" << S << ".y, sl" << j << ");\n";
+              else if (q == 2) o << in2 << "sl" << j << " = fmaf(-kl" << S << ", qb" << S << ".x + qb" << S << ".y, sl" << j << ");\n";
+              else o << in2 << "sl" << j << " = fmaf(scale" << S << ", (iq" << S << " * (qa" << S << ".x + qa" << S
+                     << ".y) - cn" << S << ") * iv" << S << ", sl" << j << ");\n";
+            } else if (q == 0) {
+              o << in2 << "sl" << j << " = fmaf(scale" << S << ", qb" << S << ".x + qb" << S << ".y, sl" << j << ");\n";
+            }
+          }
+        }
+      }
+  };
+
   // Row loop with a fused guide draw (mi_draw): lane `lane` owns the element quads
   // base/4 + qq * 64 + lane (qq < E / 4), i.e. elements base + qq * 256 + lane * 4 + j, so that one
   // Philox call yields the lane's four normals of a quad -- exactly the eps of mi_normal_rsample for
@@ -542,7 +742,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << "] : 0.0f;\n";
     // Two copies of the particle loop: a segment that is neither ragged nor past the end has
     // every element valid, and its unmasked sites need no per-element select.
+    const bool acc = packed && acc_form(g, draw);
     auto emit_k_loop = [&](const std::string& valid) {
+    if (acc) emit_acc_prologue(valid);
     if (plan.unroll > 1) o << "#pragma unroll " << plan.unroll << "\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
@@ -578,8 +780,11 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     for (int st = 0; st < g.num_sites; ++st)
       if (mask_is(st, kParticle))
         o << in << "  const bool mp" << st << " = mk" << st << "[k * msk" << st << "] != 0;\n";
-    zero_accumulators("      ");
     const char* in2 = "      ";
+    if (acc) {
+      emit_acc_row(valid);
+    } else {
+    zero_accumulators("      ");
     if (packed) {   // element pairs on the packed fp32 instructions
       for (int op = 0; op < g.num_operands; ++op)
         if (dense_grad(op)) o << in2 << "mi::f2 g" << op << "[" << E / 2 << "];\n";
@@ -598,6 +803,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
         if (dense_grad(op)) o << inner << "g" << op << "[e] = 0.0f;\n";
       for (int st = 0; st < g.num_sites; ++st) emit_site_eval(o, g, st, valid, inner.c_str());
       o << in2 << "}\n";
+    }
     }
     // g<op>[e] of either form
     auto gel = [&](int op, const char* e) {
