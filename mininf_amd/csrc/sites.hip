@@ -663,19 +663,19 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
     float xc[kGroup];
 #pragma unroll
     for (int e = 0; e < kGroup; ++e) xc[e] = xs[e];
+    // the first block index of each later quarter of the chunk (no division inside the loop)
+    const int q1 = (nfull / 4 + kBlock - 1) & ~(kBlock - 1), q2 = (nfull / 2 + kBlock - 1) & ~(kBlock - 1),
+              q3 = (3 * nfull / 4 + kBlock - 1) & ~(kBlock - 1);
+    if (balance) __builtin_amdgcn_s_setprio(3);
     for (; j < nfull; j += kBlock) {
       // Progress-balanced priority: a wave drops one priority level per quarter of its chunk, so
       // the SIMD's arbiter (priority, then age) lets the waves behind it catch up; the waves of a
       // SIMD then finish together instead of the oldest first, which would leave the last one
       // issuing alone (at half the VALU rate) through the kernel's tail.
       if (balance) {
-        const int quarter = (4 * j) / nfull;
-        if (quarter != (4 * (j - kBlock)) / nfull || j == 0) {
-          if (quarter == 0) __builtin_amdgcn_s_setprio(3);
-          else if (quarter == 1) __builtin_amdgcn_s_setprio(2);
-          else if (quarter == 2) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
-        }
+        if (j == q1) __builtin_amdgcn_s_setprio(2);
+        else if (j == q2) __builtin_amdgcn_s_setprio(1);
+        else if (j == q3) __builtin_amdgcn_s_setprio(0);
       }
       f32x2 in[2][kSmemP];
 #pragma unroll

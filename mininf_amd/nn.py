@@ -353,13 +353,21 @@ def _accumulate_final_grads(loss: torch.Tensor, unit: torch.Tensor) -> bool:
     -- ``p.grad = g``, or ``p.grad += g`` -- without starting the autograd engine (its device
     thread hand-off is most of an eager backward's host time). False (nothing done): let autograd
     run. MININF_AMD_DIRECT_GRADS=0 disables it.
+
+    Autograd also runs when ``loss.retain_grad()`` was called (it sets ``loss.grad``), and while a
+    ``torch.distributed`` process group is initialised: hooks on the AccumulateGrad nodes
+    themselves (DDP's reducer, ``grad_acc.register_hook``) are not visible on the parameter, and
+    only the engine runs them. A single-process user of node-level hooks sets
+    MININF_AMD_DIRECT_GRADS=0.
     """
     fn = loss.grad_fn
     plan = getattr(fn, "plan", None)
     tensor_inputs = getattr(plan, "tensor_inputs", None)
     if plan is None or getattr(plan, "final", None) is None or plan.state is None or \
-            tensor_inputs is None or loss._backward_hooks or \
+            tensor_inputs is None or loss._backward_hooks or loss.retains_grad or \
             os.environ.get("MININF_AMD_DIRECT_GRADS", "1") == "0":
+        return False
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
         return False
     # next_functions: one entry per tensor input of _ElboFn.apply (None inputs have none)
     nexts = fn.next_functions
@@ -461,7 +469,12 @@ class EvidenceLowerBoundLoss(nn.Module):
 
     def _zeroed_flags(self, device: torch.device) -> torch.Tensor:
         """Zeroed validation words for one eager step: a row no earlier step wrote (a used block
-        is never zeroed again: it is dropped, and lives on only while a joint still reads it)."""
+        is never zeroed again: it is dropped, and lives on only while a joint still reads it).
+        Inside a graph capture the words come from the graph's own pool (a fill every replay): a
+        row of a block allocated outside the capture would not be zeroed by replays, and the block
+        could be freed while the graph still writes into it."""
+        if torch.cuda.is_current_stream_capturing():
+            return torch.zeros(self.FLAG_WORDS, dtype=torch.int32, device=device)
         pool = self._flag_pool
         if pool is None or pool.device != device or self._flag_next >= pool.shape[0]:
             pool = self._flag_pool = torch.zeros((self.FLAG_POOL, self.FLAG_WORDS),
