@@ -473,7 +473,7 @@ class EvidenceLowerBoundLoss(nn.Module):
         Inside a graph capture the words come from the graph's own pool (a fill every replay): a
         row of a block allocated outside the capture would not be zeroed by replays, and the block
         could be freed while the graph still writes into it."""
-        if torch.cuda.is_current_stream_capturing():
+        if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
             return torch.zeros(self.FLAG_WORDS, dtype=torch.int32, device=device)
         pool = self._flag_pool
         if pool is None or pool.device != device or self._flag_next >= pool.shape[0]:
