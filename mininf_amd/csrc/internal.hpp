@@ -17,3 +17,15 @@ size_t mi_finalize_scratch_bytes(int64_t nseg, int64_t K, int nv);
 int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites, int num_slots,
                        const double* scale, double slot_scale, float* total, double* site_lp,
                        float* slot_grad, double* scratch, hipStream_t stream, int rank1 = 0);
+
+// Record a caller's timing event on `stream`: under stream capture as an external event node
+// (hipEventRecordExternal: every replay of the graph records it, so a replayed kernel can be timed),
+// otherwise as a plain record (the external flag is for captures only).
+inline hipError_t mi_record_event(void* event, hipStream_t stream) {
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(stream, &status);
+  if (e != hipSuccess) return e;
+  return status == hipStreamCaptureStatusActive
+             ? hipEventRecordWithFlags(static_cast<hipEvent_t>(event), stream, hipEventRecordExternal)
+             : hipEventRecord(static_cast<hipEvent_t>(event), stream);
+}

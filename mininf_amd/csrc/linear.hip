@@ -949,7 +949,7 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
       return to_code(e);
   }
 #endif
-  if (start_event != nullptr && (e = hipEventRecordWithFlags(static_cast<hipEvent_t>(start_event), s, hipEventRecordExternal)) != hipSuccess)
+  if (start_event != nullptr && (e = mi_record_event(start_event, s)) != hipSuccess)
     return to_code(e);
   if (site->family == MI_NORMAL)
     launch<MI_NORMAL>(*site, g, part, flags, s);
@@ -957,7 +957,7 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
     launch<MI_BERNOULLI_LOGITS>(*site, g, part, flags, s);
   e = hipGetLastError();
   if (e != hipSuccess) return to_code(e);
-  if (stop_event != nullptr && (e = hipEventRecordWithFlags(static_cast<hipEvent_t>(stop_event), s, hipEventRecordExternal)) != hipSuccess)
+  if (stop_event != nullptr && (e = mi_record_event(stop_event, s)) != hipSuccess)
     return to_code(e);
   const double scale = site->site_scale;
   if (reduce != nullptr && g.ntile <= MI_REDUCE_MAX_SEG) {   // the caller runs the finalize

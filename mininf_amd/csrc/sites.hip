@@ -1437,7 +1437,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
     }
   }
   if (start_event != nullptr) {
-    e = hipEventRecordWithFlags(static_cast<hipEvent_t>(start_event), s, hipEventRecordExternal);
+    e = mi_record_event(start_event, s);
     if (e != hipSuccess) return to_code(e);
   }
   switch (p.shape) {
@@ -1507,7 +1507,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   e = hipGetLastError();
   if (e != hipSuccess) return to_code(e);
   if (stop_event != nullptr) {
-    e = hipEventRecordWithFlags(static_cast<hipEvent_t>(stop_event), s, hipEventRecordExternal);
+    e = mi_record_event(stop_event, s);
     if (e != hipSuccess) return to_code(e);
   }
   if (draw_partials != nullptr && !(G.options & MI_GROUP_DRAW_PARTIALS)) {
