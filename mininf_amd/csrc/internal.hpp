@@ -18,14 +18,20 @@ int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites
                        const double* scale, double slot_scale, float* total, double* site_lp,
                        float* slot_grad, double* scratch, hipStream_t stream, int rank1 = 0);
 
-// Record a caller's timing event on `stream`: under stream capture as an external event node
-// (hipEventRecordExternal: every replay of the graph records it, so a replayed kernel can be timed),
-// otherwise as a plain record (the external flag is for captures only).
+// Record a caller's timing event on `stream`. Under stream capture the record becomes an event
+// record node of the graph, appended after the capture's current dependencies (every replay of
+// the graph then records it, so a replayed kernel can be timed); otherwise a plain record.
 inline hipError_t mi_record_event(void* event, hipStream_t stream) {
   hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
-  hipError_t e = hipStreamIsCapturing(stream, &status);
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(stream, &status, nullptr, &graph, &deps, &ndeps);
   if (e != hipSuccess) return e;
-  return status == hipStreamCaptureStatusActive
-             ? hipEventRecordWithFlags(static_cast<hipEvent_t>(event), stream, hipEventRecordExternal)
-             : hipEventRecord(static_cast<hipEvent_t>(event), stream);
+  if (status != hipStreamCaptureStatusActive)
+    return hipEventRecord(static_cast<hipEvent_t>(event), stream);
+  hipGraphNode_t node = nullptr;
+  e = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, static_cast<hipEvent_t>(event));
+  if (e != hipSuccess) return e;
+  return hipStreamUpdateCaptureDependencies(stream, &node, 1, hipStreamSetCaptureDependencies);
 }

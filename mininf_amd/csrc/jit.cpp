@@ -131,7 +131,8 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
   s << "|" << g.num_slots << "|" << g.compute_grads
     << (plan.row && g.N < 64L * plan.elems ? "|small" : "") << "|draw" << g.draw.operand
     << (g.draw.loc_stride == 0 ? "b" : "") << (g.draw.scale_stride == 0 ? "b" : "")
-    << (g.draw.scale_exp != nullptr ? "x" : "");
+    << (g.draw.scale_exp != nullptr ? "x" : "")
+    << (g.prior.present != 0 ? "|prior" + std::to_string(g.prior.family) : "");
   return Signature{s.str()};
 }
 
@@ -303,6 +304,8 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   const int nsite_values = plan.combined ? 1 : g.num_sites;
   const int nv = nsite_values + (g.compute_grads ? g.num_slots : 0);
   const bool packed = use_packed(g, plan);
+  // a folded prior site (mi_prior): evaluated at the block-row flush (combined values only)
+  const bool prior = g.prior.present != 0 && row && plan.block_rows && plan.combined;
   std::ostringstream o;
   auto is = [&](int op, Kind k) { return kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == k; };
   auto mask_is = [&](int s, Kind k) {
@@ -437,12 +440,38 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << ") bsum[(" << v << " * 4 + (threadIdx.x >> 6)) * " << tile_rows << " + lane] = t; }\n";
       o << in << "  __syncthreads();\n";
       o << in << "  if (threadIdx.x < " << tile_rows << " && (int)threadIdx.x <= r) {\n";
-      for (int v = 0; v < nv; ++v)
+      if (prior) {
+        // the folded prior site (mi_prior) on site 0's per-particle parameter: its log density
+        // and d/dparameter enter the particle's value and the parameter's slot once, from the
+        // writer threads of block column 0 (the prior's scale equals site 0's)
+        const int po = g.sites[0].operand[0];
+        o << in << "    float pv = 0.0f, pd = 0.0f;\n";
+        o << in << "    if (blockIdx.x == 0) {\n";
+        o << in << "      const float a = x" << po << "[((k - r) + (long)threadIdx.x) * sk" << po << "];\n";
+        o << in << "      mi::Elem pe;\n";
+        o << in << "      mi::" << (g.prior.family == MI_BETA ? "eval_beta" : g.prior.family == MI_NORMAL
+                                    ? "eval_normal" : "eval_gamma")
+          << "(G.prior.constant[0], G.prior.constant[1], a, pe);\n";
+        o << in << "      pv = (float)G.prior.scale * pe.lp;\n";
+        o << in << "      pd = (float)G.prior.scale * pe.d[2];\n";
+        o << in << "      const unsigned pf = (pe.param_bad ? " << MI_FLAG_PARAM << "u : 0u) | (pe.support_bad ? "
+          << MI_FLAG_SUPPORT << "u : 0u);\n";
+        o << in << "      if (pf != 0u) atomicOr(G.prior.flags, pf);\n";
+        o << in << "    }\n";
+      }
+      for (int v = 0; v < nv; ++v) {
+        std::string extra;
+        if (prior && v == 0) extra = " + pv";
+        if (prior && g.compute_grads && v >= nsite_values &&
+            g.operands[g.sites[0].operand[0]].grad_mode == MI_GRAD_PARTICLE &&
+            v - nsite_values == g.operands[g.sites[0].operand[0]].slot)
+          extra = " + pd";
         o << in << "    part[((long)" << v << " * gridDim.x + blockIdx.x) * K + (k - r) + threadIdx.x] = "
           << "((bsum[(" << v << " * 4) * " << tile_rows << " + threadIdx.x] + bsum[(" << v
           << " * 4 + 1) * " << tile_rows << " + threadIdx.x]) + bsum[(" << v << " * 4 + 2) * "
           << tile_rows << " + threadIdx.x]) + bsum[(" << v << " * 4 + 3) * " << tile_rows
-          << " + threadIdx.x];\n";
+          << " + threadIdx.x]" << extra << ";\n";
+      }
       o << in << "  }\n";
       o << in << "  __syncthreads();\n";
     }
@@ -1030,6 +1059,8 @@ int mi_jit_launch(const mi_group& g, const PlanInfo& plan, float* part, int64_t 
 bool mi_jit_compile_check(const mi_group& g, const PlanInfo& plan, std::string* log) {
   return compile_only(generate(g, plan), nullptr, log);
 }
+
+bool mi_jit_enabled() { return !jit_disabled(); }
 
 size_t mi_jit_cache_size() {
   std::lock_guard<std::mutex> lock(g_mutex);

@@ -33,6 +33,9 @@ std::string mi_jit_source(const mi_group& g, const PlanInfo& plan);
 
 size_t mi_jit_cache_size();
 
+// Whether specialised kernels are compiled at all (MININF_AMD_JIT=0 disables them).
+bool mi_jit_enabled();
+
 // Compile (hiprtc only, no device needed) the specialised kernel for `g`; returns success and the
 // compiler log.
 bool mi_jit_compile_check(const mi_group& g, const PlanInfo& plan, std::string* log);

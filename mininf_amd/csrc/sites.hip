@@ -1362,10 +1362,14 @@ int mi_group_side_supported(const mi_group* group, int* supported) {
 int mi_group_prior_supported(const mi_group* group, int* supported) {
   if (!validate_group(group) || supported == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
-  // the BCAST kernel's one site, its per-particle parameter an operand (stride_i == 0)
+  // the BCAST kernel's one site, or a fused-draw site program's site 0 (evaluated at its
+  // block-row flush); either way on site 0's per-particle parameter, an operand (stride_i == 0)
   const int o = group->sites[0].operand[0];
-  *supported = (p.shape == kBcast && bcast_smem(group) && group->num_sites == 1 && o >= 0 &&
-                group->operands[o].stride_i == 0 &&
+  const bool host = (p.shape == kBcast && bcast_smem(group) && group->num_sites == 1) ||
+                    (p.shape == kRow && p.draw && draw_supported(group) && mi_jit_enabled() &&
+                     env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0);
+  *supported = (host && o >= 0 && group->operands[o].stride_i == 0 &&
+                group->operands[o].stride_k != 0 &&
                 group->prior.scale == group->sites[0].scale) ? 1 : 0;
   return 0;
 }
@@ -1414,7 +1418,7 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   if (group->prior.present != 0) {
     int ok = 0;
     mi_group_prior_supported(group, &ok);
-    if (!ok) return MI_EUNSUPPORTED;
+    if (!ok || (p.shape == kRow && !combined)) return MI_EUNSUPPORTED;
   }
   float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
   const bool smem = p.shape == kBcast && bcast_smem(group);

@@ -1039,7 +1039,10 @@ def fold_priors(launchers: List[_GroupLauncher]) -> List[_GroupLauncher]:
             continue
         value = prior.operands[roles[2][0]]
         for host in out:
-            if host is prior or len(host.sites) != 1 or host.prior is not None or host.per_site:
+            # the host's site 0 reads the prior's value as its per-particle parameter: a one-site
+            # BCAST launch (the README model) or a fused-draw site program (the missing-
+            # observations model's mu ~ Normal(0, 1) under z ~ Normal(mu, 1)); the library decides
+            if host is prior or host.prior is not None or host.per_site:
                 continue
             hsite, hroles, _ = host.sites[0]
             if hroles[0][0] < 0 or hsite.scale != site.scale:

@@ -82,6 +82,9 @@ def test_masked_hierarchical_fusions(device):
     loss_fn(cond, approx()).backward()
     f = loss_fn.last_fusions
     assert f["fused_draws"] == 1
+    # mu ~ Normal(0, 1) is evaluated by the fused-draw program's block-row flush (mi_prior): no
+    # launch of its own
+    assert f["folded_priors"] == 1
 
 
 def test_off_pattern_prior_over_two_sites_matches_oracle(device):
