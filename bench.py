@@ -16,6 +16,7 @@ torch-CPU semantics, oracle/cpu_port.py, on a bounded sample, N = 1 only).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -30,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 import mininf_amd  # noqa: E402
 import mininf_amd.optim  # noqa: E402
-from mininf_amd import engine, rccl  # noqa: E402
+from mininf_amd import _native as nat, engine, rccl  # noqa: E402
 from mininf_amd.distributed import GradientBucket  # noqa: E402
 from mininf_amd.graph import StepGraph  # noqa: E402
 from torch.distributions import Bernoulli, Beta, Normal  # noqa: E402
@@ -43,43 +44,64 @@ PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec
 
 class EventTimer:
     """
-    Collects (start, stop) HIP event pairs that the library records around the main site kernel of
-    each launch (engine.KERNEL_TIMER hook: the event arguments of mi_group_forward_deferred /
-    mi_linear_forward_deferred), keyed by the group's element count N so the dominant kernel can
-    be picked out. With ``captured_only`` the pairs come from a pool created before a graph
-    capture and are handed out only while the stream is capturing: the library records them as
-    external event nodes (hipEventRecordExternal), so every replay of the graph times the kernel
-    as it runs in the replayed step.
+    Times the main site kernel of each launch (engine.KERNEL_TIMER hook), keyed by the group's
+    element count N so the dominant kernel can be picked out.
+
+    * Eager steps: (start, stop) HIP event pairs the library records around the kernel
+      (mi_group_forward_deferred / mi_linear_forward_deferred).
+    * Captured steps (``captured_only``): span stamps -- each launch gets a slot of a device
+      buffer into which every workgroup of the kernel folds its start and end time on the device's
+      constant-rate clock (mi_group.stamps, s_memrealtime); slot span = last workgroup end minus
+      first workgroup start, read after each replay of the captured step. Unlike event-record
+      nodes in the graph (which add a dependency boundary on either side of the kernel), the
+      stamps leave the replayed step's structure unchanged.
     """
     def __init__(self):
         self.pairs = []
         self.active = False
         self.captured_only = False
-        self._pool = []
+        self.slots = []        # (N, K, slot index) handed out during a capture
+        self.buffer = None     # int64 [2 * slots] on the device
 
-    def prepare(self, n):
-        """n event pairs, materialised outside any capture."""
-        for _ in range(n):
-            start = torch.cuda.Event(enable_timing=True)
-            stop = torch.cuda.Event(enable_timing=True)
-            start.record()
-            stop.record()
-            self._pool.append((start, stop))
+    def prepare(self, n, device):
+        """A stamp buffer of n slots (allocated outside any capture)."""
+        self.buffer = torch.zeros(2 * n, dtype=torch.int64, device=device)
+        self.slots = []
+        self.reset()
+
+    def reset(self):
+        if self.buffer is not None:
+            self.buffer.view(-1, 2)[:, 0].fill_(torch.iinfo(torch.int64).max)
+            self.buffer.view(-1, 2)[:, 1].zero_()
 
     def pair(self, launcher):
-        if not self.active:
+        if not self.active or self.captured_only:
             return None, None
-        if self.captured_only:
-            if not torch.cuda.is_current_stream_capturing() or not self._pool:
-                return None, None
-            start, stop = self._pool.pop()
-        else:
-            start = torch.cuda.Event(enable_timing=True)
-            stop = torch.cuda.Event(enable_timing=True)
-            start.record()   # materialise the underlying hipEvent_t; re-recorded by the library
-            stop.record()
+        start = torch.cuda.Event(enable_timing=True)
+        stop = torch.cuda.Event(enable_timing=True)
+        start.record()   # materialise the underlying hipEvent_t; re-recorded by the library
+        stop.record()
         self.pairs.append((launcher.N, launcher.K, start, stop))
         return start, stop
+
+    def stamps(self, launcher):
+        if not (self.active and self.captured_only and torch.cuda.is_current_stream_capturing()):
+            return None
+        j = len(self.slots)
+        if self.buffer is None or 2 * j + 2 > self.buffer.numel():
+            return None
+        self.slots.append((launcher.N, launcher.K, j))
+        return self.buffer.data_ptr() + 16 * j
+
+    def spans_ms(self, khz):
+        """(N, K, span in ms) of every slot (after a replay)."""
+        raw = self.buffer.view(-1, 2).cpu()
+        out = []
+        for n, k, j in self.slots:
+            t0, t1 = int(raw[j, 0]), int(raw[j, 1])
+            if t1 > 0 and t1 >= t0:
+                out.append((n, k, (t1 - t0) / khz))
+        return out
 
     def times_ms(self, N):
         return [s.elapsed_time(e) for n, _, s, e in self.pairs if n == N]
@@ -572,26 +594,28 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     kernel_source = "eager steps (HIP events around the kernel)"
 
     def kernel_timed_replays(repeat, replays=16):
-        """The dominant kernel's duration AS REPLAYED: the step captured once more with an external
-        event-record node before and after each dominant launch (EventTimer.captured_only), then
-        replayed `replays` times after the timed region; every replay re-records every pair, read
-        after it. The same kernels, grid and step structure as the timed graph."""
+        """The dominant kernel's duration AS REPLAYED: the step captured once more with a span-stamp
+        slot per site launch (EventTimer.captured_only: every workgroup folds its start / end
+        clock into the slot), then replayed `replays` times after the timed region, the slots
+        reset before and read after each replay. The same kernels, grid and step structure as
+        the timed graph."""
         arm(f"{config}: kernel-timed graph replays")
-        timer.pairs = []
-        timer.prepare(8 * repeat)
+        timer.prepare(8 * repeat, device)
         timer.active, timer.captured_only = True, True
         try:
             timing_graph = StepGraph(full_step, warmup=1, repeat=repeat,
                                      capture_error_mode="thread_local" if sharded else "global")
         finally:
             timer.active, timer.captured_only = False, False
-        pairs, timer.pairs = timer.pairs, []
+        khz = ctypes.c_int(0)
+        nat.check(nat.lib().mi_wall_clock_khz(ctypes.byref(khz)), "mi_wall_clock_khz")
         samples = []
         for i in range(replays + 2):
+            timer.reset()
             timing_graph()
             wait_device(device)
             if i >= 2:   # (the first replays after a capture are not steady)
-                samples += [(n, k, s.elapsed_time(e)) for n, k, s, e in pairs]
+                samples += timer.spans_ms(khz.value)
         timing_graph.check()
         return samples
 
@@ -651,8 +675,9 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 del os.environ["MININF_AMD_BCAST_SUFFSTAT"]
         if not sharded or collective_in_graph:
             replay_samples = kernel_timed_replays(repeat)
-            kernel_source = (f"graph replays (external HIP event nodes around the kernel in a "
-                             f"capture of the same step, {repeat} steps per replay)")
+            kernel_source = (f"graph replays (span stamps: first workgroup start to last "
+                             f"workgroup end on the device clock, in a capture of the same step, "
+                             f"{repeat} steps per replay)")
         else:
             kernel_timed_steps()
 

@@ -181,7 +181,14 @@ typedef struct mi_group {
   mi_draw draw;          /* draw.operand == 0: no operand is a fused guide draw */
   mi_side side;          /* side.out == NULL: no side job */
   mi_prior prior;        /* prior.present == 0: no folded prior site */
+  /* non-NULL: the main site kernel folds its span into stamps[0] (min over workgroups of the start)
+   * and stamps[1] (max of the end), on the device's constant-rate clock (mi_wall_clock_khz);
+   * initialise them to (UINT64_MAX, 0). Timing only (bench.py); NULL in production launches. */
+  unsigned long long* stamps;
 } mi_group;
+
+/* Frequency of the clock the span stamps count (mi_group.stamps), in kHz. */
+int mi_wall_clock_khz(int* khz);
 
 /* Library identification: returns MI_ABI_VERSION and writes the offload target ("gfx950"). */
 int mi_abi_version(char* target, size_t target_bytes);
@@ -522,6 +529,7 @@ typedef struct mi_linear {
                              mi_normal_rsample_exp). `theta` is not read; every element of it is
                              written by the launch. dloc / dscale unused. Matrix-core kernel only,
                              P % 4 == 0 (else MI_EUNSUPPORTED: launch mi_normal_rsample first). */
+  unsigned long long* stamps; /* as mi_group.stamps: the site kernel's span (timing only) */
 } mi_linear;
 
 /* *supported = 1 when mi_linear_forward evaluates `site`'s folded prior (the matrix-core kernel). */

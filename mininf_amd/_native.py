@@ -91,7 +91,7 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
-        ("draw", Draw), ("side", Side), ("prior", Prior),
+        ("draw", Draw), ("side", Side), ("prior", Prior), ("stamps", c_vp),
     ]
 
 
@@ -114,6 +114,7 @@ class Linear(ctypes.Structure):
         ("site_scale", ctypes.c_double),
         ("compute_grads", ctypes.c_int32), ("pad0", ctypes.c_int32),
         ("row_index", c_vp), ("rows", Rows), ("prior", Prior), ("draw", Draw),
+        ("stamps", c_vp),
     ]
 
 
@@ -198,6 +199,7 @@ class ElboAdam(ctypes.Structure):
 # name -> (restype, argtypes). Mirrors include/mininf_amd.h one to one.
 _SIGNATURES = {
     "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "mi_wall_clock_khz": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mi_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 3),
     "mi_group_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Group),
                                                 ctypes.POINTER(ctypes.c_size_t)]),

@@ -171,6 +171,25 @@ MI_DEV float wave_sum_strided(float v, int width) {
   return v;
 }
 
+// Kernel span stamps (bench.py's timing of a replayed kernel): every workgroup of a launch folds
+// its start and end times on the device's constant-rate clock (s_memrealtime, 100 MHz) into
+// stamps[0] (minimum) and stamps[1] (maximum), so the launch's span is stamps[1] - stamps[0] --
+// first workgroup start to last workgroup end, inside the replayed step. stamps == NULL: nothing
+// (one uniform branch per workgroup). span_end is reached by every thread of the workgroup.
+MI_DEV unsigned long long span_begin(const unsigned long long* stamps) {
+  return stamps != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+
+MI_DEV void span_end(unsigned long long* stamps, unsigned long long t0) {
+  if (stamps == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_min(stamps, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_max(stamps + 1, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // OR-combine per-lane flag words across the wave and publish them with one atomic; must be called
 // with every lane of the wave active.
 MI_DEV void publish_flags(uint32_t* flags, uint32_t mine) {

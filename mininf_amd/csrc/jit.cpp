@@ -318,6 +318,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   if (plan.waves_per_eu > 0) o << "__attribute__((amdgpu_waves_per_eu(" << plan.waves_per_eu << ", 8))) ";
   o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
+  o << "  const unsigned long long span_t0 = mi::span_begin(G.stamps);\n";
   o << "  const int lane = threadIdx.x & 63;\n";
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
@@ -955,6 +956,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   for (int s = 0; s < g.num_sites; ++s)
     o << "  mi::publish_flags(flags + " << s << ", (pb" << s << " ? " << MI_FLAG_PARAM << "u : 0u) | (sb"
       << s << " ? " << MI_FLAG_SUPPORT << "u : 0u));\n";
+  o << "  mi::span_end(G.stamps, span_t0);\n";
   o << "}\n";
   std::string text = o.str();
   for (int s = 0; s < g.num_sites; ++s) {

@@ -290,6 +290,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   unsigned long long ts_[8] = {};
 #endif
   MI_LIN_STAMP(0);
+  const unsigned long long span_t0 = span_begin(L.stamps);
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
@@ -703,6 +704,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       L.rows.counter[0] = batch_no + 1;
     }
   }
+  span_end(L.stamps, span_t0);
 }
 
 }  // namespace mi

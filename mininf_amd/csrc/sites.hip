@@ -607,6 +607,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int64_t c = (b / (8 * gy)) * 8 + b % 8;
   const int64_t kblock = (b / 8) % gy;
   if (c >= chunks) return;   // padding
+  const unsigned long long t0 = span_begin(G.stamps);
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
   const int64_t i0 = c * kSmemChunk;
@@ -800,6 +801,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   if (rank1 && slot_a >= 0 && kblock == 0 && threadIdx.x == 0 && c == 0) slot_part[extra] = 0.0f;
   publish_flags(flags, fl);
   if (G.prior.present != 0) publish_flags(G.prior.flags, fl_prior);
+  span_end(G.stamps, t0);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -1342,6 +1344,14 @@ int mi_abi_version(char* target, size_t target_bytes) {
     target[n] = '\0';
   }
   return MI_ABI_VERSION;
+}
+
+int mi_wall_clock_khz(int* khz) {
+  if (khz == nullptr) return MI_EINVAL;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev);
+  return to_code(e);
 }
 
 int mi_struct_sizes(size_t* operand, size_t* site, size_t* group) {

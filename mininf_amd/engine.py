@@ -33,8 +33,10 @@ from .particles import ParticleTrace, SiteRecord
 
 
 # Optional instrumentation (bench.py): an object with `pair(launcher) -> (start, stop)` returning
-# torch.cuda.Event pairs (already created) that mi_group_forward_timed records around the main site
-# kernel of each launch.
+# torch.cuda.Event pairs (already created, or None) that mi_group_forward_deferred /
+# mi_linear_forward_deferred record around the main site kernel of each launch, and
+# `stamps(launcher) -> device address or None` of a (min start, max end) clock-stamp pair the
+# kernel's workgroups fold their span into (mi_group.stamps).
 KERNEL_TIMER = None
 
 FAMILY_CODES = {
@@ -434,8 +436,10 @@ class _GroupLauncher:
             if self.per_site else None
         slot_grad = torch.empty((max(1, group.num_slots), K), dtype=torch.float32, device=device)
         start = stop = None
+        group.stamps = None   # (a cached descriptor must not keep an earlier timing slot)
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
+            group.stamps = KERNEL_TIMER.stamps(self)
         reduce = nat.Reduce()
         nat.check(lib.mi_group_forward_deferred(
             ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
@@ -672,8 +676,10 @@ class _LinearLauncher:
         dslots = torch.empty((nslots, self.K), dtype=torch.float32, device=device) \
             if compute_grads else None
         start = stop = None
+        L.stamps = None
         if KERNEL_TIMER is not None:
             start, stop = KERNEL_TIMER.pair(self)
+            L.stamps = KERNEL_TIMER.stamps(self)
         reduce = nat.Reduce()
 
         def launch(L):
