@@ -181,6 +181,15 @@ typedef struct mi_group {
   mi_draw draw;          /* draw.operand == 0: no operand is a fused guide draw */
   mi_side side;          /* side.out == NULL: no side job */
   mi_prior prior;        /* prior.present == 0: no folded prior site */
+  /* pdraw.operand != 0: operand pdraw.operand - 1 is a per-particle operand (stride_i == 0) that is
+   * the guide's draw of a one-element Normal factor (the missing-observations model's mu,
+   * FactorizedDistribution.rsample, nn.py:133-145): value_k = loc[0] + eps_k * scale[0] with the
+   * eps of mi_normal_rsample for (particle_offset + k, element 0; same seed, step, stream --
+   * bit-identical), scale = expf(scale_exp[0]) when scale_exp is non-NULL (then also written to
+   * scale). The launch computes the values itself and writes them to the operand's data (column
+   * block 0) instead of a mi_normal_rsample launch before it. Fused-draw site programs only
+   * (mi_group_pdraw_supported; else MI_EUNSUPPORTED: launch mi_normal_rsample first). */
+  mi_draw pdraw;
   /* non-NULL: the main site kernel folds its span into stamps[0] (min over workgroups of the start)
    * and stamps[1] (max of the end), on the device's constant-rate clock (mi_wall_clock_khz);
    * initialise them to (UINT64_MAX, 0). Timing only (bench.py); NULL in production launches. */
@@ -205,6 +214,9 @@ int mi_group_side_supported(const mi_group* group, int* supported);
 /* *supported = 1 when mi_group_forward evaluates `group`'s folded prior site (mi_prior), else 0:
  * the caller then launches that site on its own. */
 int mi_group_prior_supported(const mi_group* group, int* supported);
+
+/* *supported = 1 when mi_group_forward makes `group`'s per-particle draw (mi_group.pdraw). */
+int mi_group_pdraw_supported(const mi_group* group, int* supported);
 
 /* Workspace needed by mi_group_forward for this descriptor. */
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes);

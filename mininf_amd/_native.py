@@ -91,7 +91,7 @@ class Group(ctypes.Structure):
         ("num_slots", ctypes.c_int32), ("compute_grads", ctypes.c_int32),
         ("grad_scale", ctypes.c_float), ("options", ctypes.c_int32),
         ("sites", Site * MAX_SITES), ("operands", Operand * MAX_OPERANDS),
-        ("draw", Draw), ("side", Side), ("prior", Prior), ("stamps", c_vp),
+        ("draw", Draw), ("side", Side), ("prior", Prior), ("pdraw", Draw), ("stamps", c_vp),
     ]
 
 
@@ -201,6 +201,8 @@ _SIGNATURES = {
     "mi_abi_version": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "mi_wall_clock_khz": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mi_struct_sizes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_size_t)] * 3),
+    "mi_group_pdraw_supported": (ctypes.c_int, [ctypes.POINTER(Group),
+                                                ctypes.POINTER(ctypes.c_int)]),
     "mi_group_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Group),
                                                 ctypes.POINTER(ctypes.c_size_t)]),
     "mi_group_forward": (ctypes.c_int, [ctypes.POINTER(Group), c_vp, ctypes.c_size_t, c_vp, c_vp,

@@ -41,6 +41,9 @@ const char kStddefStub[] =
 
 enum Kind { kConst = 0, kBroadcast = 1, kShared = 2, kParticle = 3, kDense = 4 };
 
+// LDS table of a program's per-particle draw (mi_group.pdraw): sites.hip kPdrawMax particles
+constexpr int kPdrawTable = 1024;
+
 Kind kind_of(int64_t sk, int64_t si) {
   if (sk == 0 && si == 0) return kBroadcast;
   if (sk == 0) return kShared;
@@ -132,7 +135,8 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
     << (plan.row && g.N < 64L * plan.elems ? "|small" : "") << "|draw" << g.draw.operand
     << (g.draw.loc_stride == 0 ? "b" : "") << (g.draw.scale_stride == 0 ? "b" : "")
     << (g.draw.scale_exp != nullptr ? "x" : "")
-    << (g.prior.present != 0 ? "|prior" + std::to_string(g.prior.family) : "");
+    << (g.prior.present != 0 ? "|prior" + std::to_string(g.prior.family) : "")
+    << (g.pdraw.operand != 0 ? "|pdraw" + std::to_string(g.pdraw.operand) : "");
   return Signature{s.str()};
 }
 
@@ -306,6 +310,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   const bool packed = use_packed(g, plan);
   // a folded prior site (mi_prior): evaluated at the block-row flush (combined values only)
   const bool prior = g.prior.present != 0 && row && plan.block_rows && plan.combined;
+  const int pdraw = g.pdraw.operand - 1;   // a per-particle draw made by the program (or -1)
   std::ostringstream o;
   auto is = [&](int op, Kind k) { return kind_of(g.operands[op].stride_k, g.operands[op].stride_i) == k; };
   auto mask_is = [&](int s, Kind k) {
@@ -448,7 +453,10 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
         const int po = g.sites[0].operand[0];
         o << in << "    float pv = 0.0f, pd = 0.0f;\n";
         o << in << "    if (blockIdx.x == 0) {\n";
-        o << in << "      const float a = x" << po << "[((k - r) + (long)threadIdx.x) * sk" << po << "];\n";
+        if (po == pdraw)
+          o << in << "      const float a = pdv[(k - r) + (long)threadIdx.x - k_begin];\n";
+        else
+          o << in << "      const float a = x" << po << "[((k - r) + (long)threadIdx.x) * sk" << po << "];\n";
         o << in << "      mi::Elem pe;\n";
         o << in << "      mi::" << (g.prior.family == MI_BETA ? "eval_beta" : g.prior.family == MI_NORMAL
                                     ? "eval_normal" : "eval_gamma")
@@ -767,9 +775,36 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       o << in << "float dal[" << E << "], das[" << E << "];\n#pragma unroll\n" << in
         << "for (int e = 0; e < " << E << "; ++e) dal[e] = das[e] = 0.0f;\n";
     for (int op = 0; op < g.num_operands; ++op)
-      if (is(op, kParticle))
+      if (is(op, kParticle) && op != pdraw)
         o << in << "float pn" << op << " = k_begin < k_end ? x" << op << "[k_begin * sk" << op
           << "] : 0.0f;\n";
+    if (pdraw >= 0) {
+      // the per-particle draw (mi_group.pdraw): this particle block's values into an LDS table,
+      // each by one thread -- the normals and fmaf of mi_normal_rsample for (particle, element 0)
+      // -- written to the operand by column block 0
+      const std::string P = std::to_string(pdraw);
+      o << in << "__shared__ float pdv[" << kPdrawTable << "];\n";
+      o << in << "{\n";
+      o << in << "  const unsigned long long pstep = G.pdraw.step + (G.pdraw.step_device != nullptr ? "
+           "*G.pdraw.step_device : 0ull);\n";
+      o << in << "  const float ploc = G.pdraw.loc[0];\n";
+      o << in << "  const float psd = G.pdraw.scale_exp != nullptr ? expf(G.pdraw.scale_exp[0]) : "
+           "G.pdraw.scale[0];\n";
+      o << in << "  if (G.pdraw.scale_exp != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && "
+           "threadIdx.x == 0) const_cast<float*>(G.pdraw.scale)[0] = psd;\n";
+      o << in << "  for (long j = threadIdx.x; j < k_end - k_begin; j += 256) {\n";
+      o << in << "    float pe[4];\n";
+      o << in << "    mi::guide_normals(G.pdraw.seed, pstep, G.pdraw.stream_id, (unsigned long long)"
+           "(G.pdraw.element_offset >> 2), (unsigned long long)(G.pdraw.particle_offset + k_begin + j), "
+           "pe);\n";
+      o << in << "    const float v = fmaf(pe[0], psd, ploc);\n";
+      o << in << "    pdv[j] = v;\n";
+      o << in << "    if (blockIdx.x == 0) const_cast<float*>(x" << P << ")[(k_begin + j) * sk" << P
+        << "] = v;\n";
+      o << in << "  }\n";
+      o << in << "  __syncthreads();\n";
+      o << in << "}\n";
+    }
     // Two copies of the particle loop: a segment that is neither ragged nor past the end has
     // every element valid, and its unmasked sites need no per-element select.
     const bool acc = packed && acc_form(g, draw);
@@ -804,7 +839,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     // per-particle operands: next row's values loaded one iteration ahead (a scalar load waited
     // on right away would stall the wave for its L2 round trip every row)
     for (int op = 0; op < g.num_operands; ++op)
-      if (is(op, kParticle))
+      if (is(op, kParticle) && op == pdraw)
+        o << in << "  const float p" << op << " = pdv[k - k_begin];\n";
+      else if (is(op, kParticle))
         o << in << "  const float p" << op << " = pn" << op << ";\n" << in << "  if (k + 1 < k_end) pn"
           << op << " = x" << op << "[(k + 1) * sk" << op << "];\n";
     for (int st = 0; st < g.num_sites; ++st)

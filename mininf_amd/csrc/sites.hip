@@ -1053,6 +1053,12 @@ bool validate_group(const mi_group* g) {
       ((g->prior.family != MI_BETA && g->prior.family != MI_NORMAL && g->prior.family != MI_GAMMA) ||
        g->prior.flags == nullptr || g->sites[0].operand[0] < 0))
     return false;
+  const int pdraw = g->pdraw.operand - 1;
+  if (pdraw >= g->num_operands || pdraw < -1 || (pdraw >= 0 && pdraw == draw)) return false;
+  if (pdraw >= 0 && (g->pdraw.loc == nullptr || g->pdraw.scale == nullptr ||
+                     g->pdraw.element_offset < 0 || (g->pdraw.element_offset & 3) != 0 ||
+                     g->operands[pdraw].stride_i != 0 || g->operands[pdraw].stride_k == 0))
+    return false;
   for (int o = 0; o < g->num_operands; ++o) {
     const mi_operand& op = g->operands[o];
     if (o == draw) continue;  // computed in the kernel
@@ -1065,6 +1071,10 @@ bool validate_group(const mi_group* g) {
 
 // A fused guide draw (mi_draw) needs the row layout with whole element quads per lane and plain
 // row-major [K, N] companions (see include/mininf_amd.h).
+// Largest particle block of a program that makes a per-particle draw (mi_group.pdraw): the
+// values live in an LDS table of the program (jit.cpp kPdrawTable).
+constexpr int64_t kPdrawMax = 1024;
+
 bool draw_supported(const mi_group* g) {
   const int draw = g->draw.operand - 1;
   if (draw < 0) return true;
@@ -1384,6 +1394,17 @@ int mi_group_prior_supported(const mi_group* group, int* supported) {
   return 0;
 }
 
+int mi_group_pdraw_supported(const mi_group* group, int* supported) {
+  if (!validate_group(group) || supported == nullptr) return MI_EINVAL;
+  const Plan p = make_plan(group);
+  // a fused-draw site program (row shape, block-row partials) whose particle block fits the
+  // program's LDS table of per-particle values
+  *supported = (p.shape == kRow && p.draw && draw_supported(group) && mi_jit_enabled() &&
+                env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0 &&
+                p.rows_per_block <= kPdrawMax) ? 1 : 0;
+  return 0;
+}
+
 int mi_group_workspace_bytes(const mi_group* group, size_t* bytes) {
   if (!validate_group(group) || bytes == nullptr) return MI_EINVAL;
   const Plan p = make_plan(group);
@@ -1429,6 +1450,11 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
     int ok = 0;
     mi_group_prior_supported(group, &ok);
     if (!ok || (p.shape == kRow && !combined)) return MI_EUNSUPPORTED;
+  }
+  if (group->pdraw.operand != 0) {
+    int ok = 0;
+    mi_group_pdraw_supported(group, &ok);
+    if (!ok) return MI_EUNSUPPORTED;
   }
   float* draw_partials = draw_partial_floats(group, p) != 0 ? prep : nullptr;
   const bool smem = p.shape == kBcast && bcast_smem(group);

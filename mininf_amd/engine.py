@@ -188,6 +188,9 @@ class _GroupLauncher:
         # a one-element prior site folded into this launch (mi_prior, fold_priors): (site, family
         # code, (constant, constant)); its validation word follows the group's own
         self.prior: Optional[Tuple[SiteRecord, int, Tuple[float, float]]] = None
+        # a deferred one-element Normal guide draw this launch makes itself (mi_group.pdraw,
+        # claim_group_draws): (the draw, the operand index that reads it)
+        self.pdraw: Optional[Tuple[guide.PendingDraw, int]] = None
 
     @property
     def flag_sites(self) -> List[SiteRecord]:
@@ -363,6 +366,10 @@ class _GroupLauncher:
             pr.present, pr.family = 1, self.prior[1]
             pr.constant[0], pr.constant[1] = self.prior[2]
             pr.scale = self.prior[0].scale
+        if self.pdraw is not None and not self.pdraw[0].done:
+            rec, index = self.pdraw
+            rec.describe(group.pdraw)
+            group.pdraw.operand = index + 1
         return group, grads
 
     def source(self) -> str:
@@ -441,12 +448,25 @@ class _GroupLauncher:
             start, stop = KERNEL_TIMER.pair(self)
             group.stamps = KERNEL_TIMER.stamps(self)
         reduce = nat.Reduce()
-        nat.check(lib.mi_group_forward_deferred(
-            ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
-            nat.ptr(site_lp), slot_grad.data_ptr(), flags.data_ptr(),
-            None if start is None else start.cuda_event, None if stop is None else stop.cuda_event,
-            nat.stream_handle(device), ctypes.byref(reduce) if defer else None),
-            "mi_group_forward_deferred")
+
+        def launch():
+            return lib.mi_group_forward_deferred(
+                ctypes.byref(group), workspace.data_ptr(), size.value, total.data_ptr(),
+                nat.ptr(site_lp), slot_grad.data_ptr(), flags.data_ptr(),
+                None if start is None else start.cuda_event,
+                None if stop is None else stop.cuda_event,
+                nat.stream_handle(device), ctypes.byref(reduce) if defer else None)
+        code = launch()
+        if group.pdraw.operand and code == nat.MI_EUNSUPPORTED:
+            # this launch does not make the per-particle draw: the draw's own launch first
+            rec = self.pdraw[0]
+            rec.launch()
+            guide.take_draw(rec)
+            group.pdraw = nat.Draw()
+            code = launch()
+        nat.check(code, "mi_group_forward_deferred")
+        if group.pdraw.operand:
+            guide.take_draw(self.pdraw[0])
         if self.exp_pending is not None:
             self.exp_pending.filled = True
             self.exp_pending = None
@@ -776,6 +796,9 @@ def claim_linear_draws(trace: ParticleTrace) -> Dict[int, guide.PendingDraw]:
             if rec is not None:
                 others[rec].append(t)
     claims = {}
+    # one-element draws (a global parameter's K draws, e.g. the missing-observations model's mu)
+    # stay pending for claim_group_draws: a fused-draw site program may make them itself
+    keep = {id(rec) for rec in guide._PENDING_DRAWS.values() if rec.z.shape[-1] == 1}
     for rec, sites in thetas.items():
         z = rec.z
         if len(sites) == 1 and all(
@@ -784,12 +807,57 @@ def claim_linear_draws(trace: ParticleTrace) -> Dict[int, guide.PendingDraw]:
                 for t in others.get(rec, [])):
             claims[id(sites[0])] = rec
             rec.claimed = True
-    claimed = set(map(id, claims.values()))
+    claimed = set(map(id, claims.values())) | keep
     for key, rec in list(guide._PENDING_DRAWS.items()):
         if id(rec) not in claimed:
             del guide._PENDING_DRAWS[key]
             rec.launch()
     return claims
+
+
+def claim_group_draws(trace: ParticleTrace, launchers: List["_GroupLauncher"]) -> None:
+    """
+    Deferred one-element Normal guide draws (a global parameter's K draws: the missing-
+    observations model's ``mu``, examples/missing-observations.md:33-45) that a fused-draw site
+    program makes itself (``mi_group.pdraw``): the draw is read only by that program, as one
+    per-particle operand (its sites, and a prior folded into it). The program computes the draws
+    from the same counter as ``mi_normal_rsample`` into a table of its own and writes them out, so
+    the draw has no launch of its own. Unclaimed draws are launched by the caller's flush.
+    """
+    pending = [rec for rec in guide._PENDING_DRAWS.values()
+               if not rec.claimed and not rec.done and rec.z.shape[-1] == 1]
+    if not pending:
+        return
+    lib = nat.lib()
+    for rec in pending:
+        key = _storage(rec.z)
+        # every site reading the draw must belong to one launcher (or be its folded prior)
+        readers = []
+        for site in trace.sites:
+            if any(isinstance(t, torch.Tensor) and guide.pending_draw(t) is rec for t in site.tensors):
+                readers.append(site)
+        hosts = [(l, i) for l in launchers for i, op in enumerate(l.operands)
+                 if op.view.tensor is not None and _storage(op.view.tensor) == key]
+        if len(hosts) != 1:
+            continue
+        host, index = hosts[0]
+        own = {id(site) for site, _, _ in host.sites}
+        if host.prior is not None:
+            own.add(id(host.prior[0]))
+        if host.draw is None or host.operands[index].view.si != 0 or \
+                any(id(site) not in own for site in readers):
+            continue
+        host.pdraw = (rec, index)
+        group, _ = host.describe(True, query=True)
+        if host.prior is not None:
+            group.prior.flags = _QUERY_ADDRESS
+        supported = ctypes.c_int(0)
+        nat.check(lib.mi_group_pdraw_supported(ctypes.byref(group), ctypes.byref(supported)),
+                  "mi_group_pdraw_supported")
+        if supported.value:
+            rec.claimed = True
+        else:
+            host.pdraw = None
 
 
 def release_unsafe_claims(linears: List["_LinearLauncher"], launchers: List["_GroupLauncher"],
@@ -2159,6 +2227,7 @@ def elbo(trace: ParticleTrace, g0: float, device: torch.device, factors: List[En
         _materialize_draws(trace, bad)
     launchers = fold_linear_priors(fold_priors(launchers), linears)
     release_unsafe_claims(linears, launchers, categorical)
+    claim_group_draws(trace, launchers)
     guide.flush_draws()   # draws made while planning (materialised lazy draws)
     fallback = [value for _, value in trace.fallback]
     absorbed = plan_absorption(factors, samples, launchers, linears, categorical, fallback)

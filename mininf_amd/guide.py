@@ -85,7 +85,7 @@ class _NormalRsampleFn(torch.autograd.Function):
         K = cfg.K
         z = torch.empty((K, N), dtype=torch.float32, device=loc.device)
         draw = PendingDraw(cfg, z, loc, loc_s, scale, scale_s, exp_source(scale))
-        if cfg.defer and cfg.noise is None and N % 4 == 0 and N <= DEFER_MAX_N and \
+        if cfg.defer and cfg.noise is None and (N % 4 == 0 or N == 1) and N <= DEFER_MAX_N and \
                 os.environ.get("MININF_AMD_DRAW_IN_LINEAR", "1") != "0":
             _PENDING_DRAWS[_storage_of(z)] = draw   # launched by flush_draws, or taken
         else:

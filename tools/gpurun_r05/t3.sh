@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU suite, default bench line, then rocprofv3 evidence on GRAPH-REPLAYED steps (kernel-trace
+# stats, FETCH_SIZE / WRITE_SIZE passes per config) for profiles/ (round tag r05).
+set -u
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+fatal() { [ "$1" -eq 124 ] || [ "$1" -eq 137 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+prof() { local t=$1; shift; local tag=$1; shift
+  timeout -s KILL "$t" rocprofv3 "$@" > "gpurun_out/$tag.log" 2>&1; local rc=$?; echo "$tag rc=$rc"
+  if fatal $rc; then exit $rc; fi; return $rc; }
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r05_t3_tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -2 gpurun_out/r05_t3_tests.log
+[ $rc -ne 0 ] && exit $rc
+fi
+timeout -k 10 400 python3 -u bench.py > gpurun_out/r05_t3_bench.json 2> gpurun_out/r05_t3_bench.err; rc=$?
+echo "bench rc=$rc"; fatal $rc && exit $rc
+B="python3 bench.py --no-cpu-baseline --no-other-configs --steps 48 --warmup 3 --warm-ms 20"
+for c in c2 c3 c4 c5; do
+  prof 240 stats_$c --kernel-trace --stats -d gpurun_out/stats_$c -o run --output-format csv -- $B --config $c || exit 1
+done
+P="python3 bench.py --no-cpu-baseline --no-other-configs --steps 16 --warmup 2 --warm-ms 0"
+for c in c2 c3 c4 c5; do
+  prof 150 fetch_$c --pmc FETCH_SIZE -d gpurun_out/fetch_$c -o run --output-format csv -- $P --config $c || exit 1
+  prof 150 write_$c --pmc WRITE_SIZE -d gpurun_out/write_$c -o run --output-format csv -- $P --config $c || exit 1
+done
+prof 150 fetch_c5cal --pmc FETCH_SIZE -d gpurun_out/fetch_c5cal -o run --output-format csv -- $P --config c5 --particles-per-gpu 64 || exit 1
+prof 150 write_c5cal --pmc WRITE_SIZE -d gpurun_out/write_c5cal -o run --output-format csv -- $P --config c5 --particles-per-gpu 64 || exit 1
+exit 0
