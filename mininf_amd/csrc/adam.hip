@@ -39,7 +39,7 @@ MI_DEV T pick_adam(const T (&arr)[N], int a) {
 
 MI_DEV mi_adam_tensor tensor_at(const mi_adam& A, int t) { return adam_tensor_at(A, t); }
 
-// NT: non-temporal 16-byte loads and stores (streamed once per step; MININF_AMD_ADAM_NT)
+// NT: non-temporal 16-byte loads and stores (measured slower on C5: the launch uses plain ones)
 typedef float f4v __attribute__((ext_vector_type(4)));
 MI_DEV float4 ld(const float4* p, bool nt) {
   if (!nt) return *p;
@@ -203,19 +203,12 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
       return MI_EINVAL;
     total += T.numel;
   }
-  // A few hundred workgroups over all tensors (MININF_AMD_ADAM_BLOCKS, default 512): measured on
-  // C5's 2 x 1e6 parameters (tools/adam_probe.py, profiles/r03_adam_sweep.log), 500 workgroups of
-  // 4096 elements run at 12.5 us, 980 of 2048 at 17 us; at least MININF_AMD_ADAM_CHUNK elements
-  // per workgroup and at most kAdamGroup^2 workgroups per tensor.
-  static const int64_t target_blocks = [] {
-    const char* v = std::getenv("MININF_AMD_ADAM_BLOCKS");
-    return std::max<int64_t>(1, v != nullptr ? std::atoll(v) : 512);
-  }();
-  static const int64_t min_chunk = [] {
-    const char* v = std::getenv("MININF_AMD_ADAM_CHUNK");
-    const int64_t n = v != nullptr ? std::atoll(v) : 4 * mi::kAdamThreads;
-    return std::max<int64_t>(4 * mi::kAdamThreads, n);
-  }();
+  // A few hundred workgroups over all tensors: measured on C5's 2 x 1e6 parameters
+  // (tools/adam_probe.py, profiles/r03_adam_sweep.log), 500 workgroups of 4096 elements run at
+  // 12.5 us, 980 of 2048 at 17 us; at least 4 * kAdamThreads elements per workgroup and at most
+  // kAdamGroup^2 workgroups per tensor.
+  constexpr int64_t target_blocks = 512;
+  constexpr int64_t min_chunk = 4 * mi::kAdamThreads;
   const int64_t even = (total + target_blocks - 1) / target_blocks;
   int blocks = 0;
   for (int t = 0; t < adam->num; ++t) {
@@ -229,28 +222,12 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
     blocks += (int)((T.numel + chunk - 1) / chunk);
   }
   for (int t = adam->num; t <= MI_ADAM_MAX_TENSORS; ++t) P.first[t] = blocks;
-  // variants (MININF_AMD_ADAM_NT=1: non-temporal accesses; MININF_AMD_ADAM_UNROLL=4: four quads
-  // per lane per pass)
-  static const int variant = [] {
-    const char* nt = std::getenv("MININF_AMD_ADAM_NT");
-    const char* un = std::getenv("MININF_AMD_ADAM_UNROLL");
-    return (nt != nullptr && nt[0] == '1' ? 1 : 0) | (un != nullptr && un[0] == '4' ? 2 : 0);
-  }();
-  // MININF_AMD_ADAM_COUNT: 2 count at the start (default; 12.5 us vs 14.2 us counting at the
-  // end, C5), 1 at the end, 0 never (timing probes only: the step does not advance)
-  static const int count = [] {
-    const char* v = std::getenv("MININF_AMD_ADAM_COUNT");
-    const int c = v != nullptr ? std::atoi(v) : 2;
-    return (c == 0 || c == 1) ? c : 2;
-  }();
+  // the step counts are advanced by the first workgroup (12.5 us vs 14.2 us counting at the end,
+  // C5; r03 sweeps also kept plain over non-temporal accesses and two quads per lane per pass)
+  constexpr int count = 2;
   const dim3 grid((unsigned)blocks), block(mi::kAdamThreads);
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (variant) {
-    case 1: hipLaunchKernelGGL((mi::k_adam_step<true, 2>), grid, block, 0, s, *adam, P, counters, count); break;
-    case 2: hipLaunchKernelGGL((mi::k_adam_step<false, 4>), grid, block, 0, s, *adam, P, counters, count); break;
-    case 3: hipLaunchKernelGGL((mi::k_adam_step<true, 4>), grid, block, 0, s, *adam, P, counters, count); break;
-    default: hipLaunchKernelGGL((mi::k_adam_step<false, 2>), grid, block, 0, s, *adam, P, counters, count); break;
-  }
+  hipLaunchKernelGGL((mi::k_adam_step<false, 2>), grid, block, 0, s, *adam, P, counters, count);
   return to_code(hipGetLastError());
 }
 

@@ -1367,16 +1367,9 @@ struct Layout {
   int64_t doubles;
 };
 
-// quads per lane of partial_lane_quads (MININF_AMD_ELBO_QUADS: 0 off, 1, 2 or 4)
-int env_quads() {
-  static const int v = [] {
-    const char* e = getenv("MININF_AMD_ELBO_QUADS");
-    // measured on C5 (two partial rows of 1e6): step 0.2427 ms with 2, 0.2457-0.2484 without
-    const int n = e != nullptr ? atoi(e) : 2;
-    return (n == 1 || n == 2 || n == 4) ? n : 0;
-  }();
-  return v;
-}
+// quads per lane of partial_lane_quads (measured on C5, two partial rows of 1e6: step 0.2427 ms
+// with 2, 0.2457-0.2484 without)
+constexpr int kQuads = 2;
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
@@ -1433,9 +1426,8 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
   slices = ceil_div(rows, rps);
   // a backward over a few partial rows, one lane per element: four elements per lane instead
   P.epl[a] = (!forward && F.draw_kind == MI_DRAW_PARTIALS && tk == 1 && slices == 1) ? 4 : 1;
-  // ... as 16-byte quads when the layout allows (MININF_AMD_ELBO_QUADS: quads per lane, 0 = off)
-  const int quads = env_quads();
-  if (P.epl[a] == 4 && quads > 0 && quad_layout(F)) P.epl[a] = -quads;
+  // ... as 16-byte quads when the layout allows
+  if (P.epl[a] == 4 && quad_layout(F)) P.epl[a] = -kQuads;
   P.ti[a] = ti;
   P.gx[a] = (int)(P.epl[a] == 4    ? ceil_div(F.n, (int64_t)ti * 4)
                   : P.epl[a] < 0 ? ceil_div(F.n >> 2, (int64_t)ti * -P.epl[a])
@@ -1451,36 +1443,12 @@ void add_absorbed(const mi_elbo* e, int f, bool forward, bool finish, mi::Absorb
   blocks += (int)(P.gx[a] * slices);
 }
 
-// particles per reducing block for long segment lists (MININF_AMD_ELBO_KRED: 16, 32 or 64)
-// particles per reducing block for very long segment lists over few particles
-// (MININF_AMD_ELBO_KRED_LONG: 8 or 16)
-int env_kred_long() {
-  static const int v = [] {
-    const char* e = getenv("MININF_AMD_ELBO_KRED_LONG");
-    const int n = e != nullptr ? atoi(e) : 16;
-    return (n == 8 || n == 16) ? n : 16;
-  }();
-  return v;
-}
-
-int env_kred() {
-  static const int v = [] {
-    const char* e = getenv("MININF_AMD_ELBO_KRED");
-    const int n = e != nullptr ? atoi(e) : 32;   // measured on MI355X (C2): 16 / 32 / 64
-    return (n == 16 || n == 32 || n == 64) ? n : 32;
-  }();
-  return v;
-}
-
-int env_lead() {
-  static const int v = [] {
-    const char* e = getenv("MININF_AMD_ELBO_LEAD");
-    // measured on MI355X (C5, steady clocks): 32 -> 0.2077-0.2079 ms, 16 -> 0.2091-0.2093
-    const int n = e != nullptr ? atoi(e) : 32;
-    return (n == 4 || n == 8 || n == 16 || n == 32) ? n : 32;
-  }();
-  return v;
-}
+// particles per reducing block for long segment lists (measured on MI355X, C2: 16 / 32 / 64)
+constexpr int kKred = 32;
+// particles per reducing block for very long segment lists over few particles (8 or 16)
+constexpr int kKredLong = 16;
+// lead blocks (measured on MI355X, C5, steady clocks: 32 -> 0.2077-0.2079 ms, 16 -> 0.2091-0.2093)
+constexpr int kLead = 32;
 
 Layout make_layout(const mi_elbo* e) {
   Layout L{};
@@ -1489,7 +1457,7 @@ Layout make_layout(const mi_elbo* e) {
   // 223-VGPR blocks fit two per CU, so a larger grid runs in several rounds
   L.fwd.lead_blocks = (int)std::max<int64_t>(
       1, std::min<int64_t>(mi::kElboMaxBlocks,
-                           ceil_div(std::max(e->K, longest_factor(e)), env_lead() * mi::kElboThreads)));
+                           ceil_div(std::max(e->K, longest_factor(e)), kLead * mi::kElboThreads)));
   int64_t longest = 1;
   for (int f = 0; f < e->num_factors; ++f)
     if (e->factors[f].draw_kind == MI_DRAW_NONE) longest = std::max(longest, e->factors[f].n);
@@ -1503,8 +1471,8 @@ Layout make_layout(const mi_elbo* e) {
     L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
     // long lists over few particles (a fused draw's block rows: ~1000 segments, K = 128): 16
     // particles x 16 segment groups per block, for more blocks and fewer serial loads per lane
-    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? env_kred_long()
-                    : (J.nseg >= 64 && env_kred() != mi::kRedKWide) ? env_kred()
+    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? kKredLong
+                    : (J.nseg >= 64 && kKred != mi::kRedKWide) ? kKred
                                                                      : mi::kRedKWide;
     nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
   }

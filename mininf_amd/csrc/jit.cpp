@@ -114,10 +114,8 @@ std::string mask_kind_tag(const mi_site& st) {
 
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
-  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s") << "w"
-    << plan.waves_per_eu << (plan.balance ? "b" : "") << "u" << plan.unroll
-    << (plan.block_rows ? "B" : "") << (use_packed(g, plan) ? "P" : "") << "t" << plan.tile_rows
-    << "|"
+  s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s")
+    << (plan.block_rows ? "B" : "") << (use_packed(g, plan) ? "P" : "") << "|"
     << g.num_operands << ":";
   for (int o = 0; o < g.num_operands; ++o) {
     const mi_operand& op = g.operands[o];
@@ -320,7 +318,6 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
 
   o << "#include \"device_math.hpp\"\n";
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
-  if (plan.waves_per_eu > 0) o << "__attribute__((amdgpu_waves_per_eu(" << plan.waves_per_eu << ", 8))) ";
   o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
   o << "  const unsigned long long span_t0 = mi::span_begin(G.stamps);\n";
@@ -328,10 +325,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
   // LDS of the row loops' particle sums: nv tiles of [tile_rows][65] floats per wave
-  // (plan.tile_rows overrides: 8 halves the LDS, which caps a 256-thread block at 4 waves / SIMD
-  // with 16 rows and two values)
-  const int tile_rows = plan.tile_rows == 8 || plan.tile_rows == 16 ? plan.tile_rows
-                                                                     : (nv <= 2 ? 16 : 8);
+  const int tile_rows = nv <= 2 ? 16 : 8;
   if (row)
     o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
       << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";
@@ -546,7 +540,6 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     row_loads("        ", "n", "k_begin");
     o << in << "}\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
-    if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     declare_dense("        ", "d");
     for (int op = 0; op < g.num_operands; ++op)
@@ -810,9 +803,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     const bool acc = packed && acc_form(g, draw);
     auto emit_k_loop = [&](const std::string& valid) {
     if (acc) emit_acc_prologue(valid);
-    if (plan.unroll > 1) o << "#pragma unroll " << plan.unroll << "\n";
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
-    if (plan.balance) o << in << "  mi::balance_priority(k - k_begin, k_end - k_begin);\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
     if (packed) {   // pairs: eps and z = loc + eps * scale on packed instructions
       o << in << "  mi::f2 ep2[" << E / 2 << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "

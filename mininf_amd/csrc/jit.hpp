@@ -12,12 +12,8 @@ struct PlanInfo {
   int elems;       // ROW: elements per lane per row; COL: unroll of the element loop
   int kw;          // COL: lanes per element group (power of two <= 64)
   bool combined;   // reduce one weighted log-joint value per particle instead of one per site
-  int waves_per_eu;  // occupancy target handed to the compiler (0 = compiler's choice)
-  bool balance;    // ROW: progress-balanced wave priority over the particle loop
-  int unroll;      // fused-draw row loop: particles unrolled per iteration (1 = none)
   bool block_rows; // fused-draw row loop: one partial row per block (gridDim.x rows), not per wave
   bool packed;     // fused-draw row loop: element pairs on packed fp32 math where the families allow
-  int tile_rows;   // row loops: particles per LDS tile flush (8 or 16; 0 = by the value count)
   unsigned grid_x;
   unsigned grid_y;
 };

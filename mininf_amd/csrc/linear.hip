@@ -748,26 +748,18 @@ bool use_mfma(const mi_linear* L) {
 }
 
 // Matrix-core launch variants: block size, fp64 carry of the dtheta accumulators across stages,
-// minimum waves per SIMD (register budget). MININF_AMD_LINEAR_TUNE forces one (tuning and tests).
+// minimum waves per SIMD (register budget). Measured on MI355X (tools/linear_bench.py, r02): one
+// feature tile (P <= 32) runs 256 threads at 4 waves/SIMD with fp32 dtheta accumulators over the
+// block's rows (C3 329 us vs 346 us for 512 threads with an fp64 carry), two tiles 256 threads at
+// 2 waves/SIMD (350 us vs 370 us).
 struct MfVariant {
   int threads;
   bool flush64;
   int minw;
 };
-constexpr MfVariant kMfVariants[] = {{512, true, 1}, {512, false, 1}, {256, false, 1},
-                                     {256, false, 4}, {256, true, 2}};
+constexpr MfVariant kMfVariants[] = {{256, false, 4}, {256, false, 2}};
 
-// Default per feature tiles (measured on MI355X, tools/linear_bench.py): one tile (P <= 32) runs
-// variant 3 (256 threads, 4 waves/SIMD, fp32 dtheta accumulators over the block's rows: C3 329 us
-// vs 346 us for variant 0), two tiles variant 4 (256 threads, 2 waves/SIMD: 350 us vs 370 us).
-int mf_variant(int pt) {
-  static const int forced = [] {
-    const char* e = getenv("MININF_AMD_LINEAR_TUNE");
-    const int n = e != nullptr ? atoi(e) : -1;
-    return (n >= 0 && n < (int)(sizeof(kMfVariants) / sizeof(kMfVariants[0]))) ? n : -1;
-  }();
-  return forced >= 0 ? forced : (pt == 1 ? 3 : 4);
-}
+int mf_variant(int pt) { return pt == 1 ? 0 : 1; }
 
 Geometry geometry(const mi_linear* L) {
   Geometry g{};
@@ -860,13 +852,10 @@ void launch_mfma(const mi_linear& L, const Geometry& g, float* part, uint32_t* f
 template <int FAMILY, int PT>
 void launch_mfma_variant(const mi_linear& L, const Geometry& g, float* part, uint32_t* flags,
                          hipStream_t s) {
-  switch (g.variant) {
-    case 1: launch_mfma<FAMILY, PT, 512, false, 1>(L, g, part, flags, s); break;
-    case 2: launch_mfma<FAMILY, PT, 256, false, 1>(L, g, part, flags, s); break;
-    case 3: launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s); break;
-    case 4: launch_mfma<FAMILY, PT, 256, PT == 1, 2>(L, g, part, flags, s); break;
-    default: launch_mfma<FAMILY, PT, 512, PT == 1, 1>(L, g, part, flags, s); break;
-  }
+  if (g.variant == 0)
+    launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s);
+  else
+    launch_mfma<FAMILY, PT, 256, false, 2>(L, g, part, flags, s);
 }
 
 template <int FAMILY>

@@ -212,11 +212,7 @@ int mi_mvn_tril_forward(const double* value, const double* loc, const double* sc
   if (value == nullptr || loc == nullptr || scale_tril == nullptr || log_prob == nullptr ||
       w == nullptr || u == nullptr)
     return MI_EINVAL;
-  static const bool lds = [] {   // MININF_AMD_MVN_LDS=0: read the factor from global memory
-    const char* v = std::getenv("MININF_AMD_MVN_LDS");
-    return v == nullptr || v[0] != '0';
-  }();
-  if (lds && n <= mi::kMvnLdsMaxN) {
+  if (n <= mi::kMvnLdsMaxN) {   // the factor staged in LDS; longer ones read from global memory
     const size_t bytes = sizeof(double) * (size_t)n * (size_t)(n + 1);
     hipLaunchKernelGGL(mi::k_mvn_tril<true>, dim3((unsigned)batch), dim3(mi::kMvnThreads), bytes,
                        static_cast<hipStream_t>(stream), value, loc, scale_tril, (int)n,

@@ -593,8 +593,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
                                                                    int mode,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
-  // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below); bit 2: L2
-  // prefetch of the chunk
+  // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below)
   const int rank1 = mode & 1;
   const bool balance = (mode & 2) != 0;
   const int64_t chunks = nseg - 1;
@@ -613,12 +612,6 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int64_t i0 = c * kSmemChunk;
   const int len = (int)min((int64_t)kSmemChunk, G.N - i0);
   uint32_t fl = 0u;
-  // mode bit 2: the chunk pulled into L2 by one vector load per 64-byte line at the start, so the
-  // scalar loads of the main loop hit L2 instead of waiting on HBM (the value is only consumed at
-  // the end: no wait inside the loop, one register)
-  const bool prefetch = (mode & 4) != 0;
-  float pf = 0.0f;
-  if (prefetch && (int)threadIdx.x * 16 < len) pf = xg[i0 + (int)threadIdx.x * 16];
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
   const int64_t K = G.K;
@@ -746,7 +739,6 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       }
     }
   }
-  if (prefetch && !(pf == 0.0f || pf == 1.0f)) fl |= MI_FLAG_SUPPORT;   // (checked again above)
   s_a = block_sum(s_a, scratch);
   if (SUFF) {
 #pragma unroll
@@ -1099,12 +1091,6 @@ int env_int(const char* name, int fallback) {
   return v != nullptr ? std::atoi(v) : fallback;
 }
 
-// Elements per lane per row of the ROW shape (4, 8 or 16).
-int row_elems() {
-  const int e = env_int("MININF_AMD_ROW_ELEMS", kRowElems);
-  return (e == 4 || e == 16) ? e : 8;
-}
-
 bool bcast_eligible(const mi_group* g) {
   if (g->num_sites != 1 || g->N < 1024 || g->K < 64) return false;
   const mi_site& st = g->sites[0];
@@ -1121,35 +1107,17 @@ bool bcast_eligible(const mi_group* g) {
   return true;
 }
 
-// Bernoulli BCAST sites over unmasked contiguous data run k_site_bcast_smem (MININF_AMD_BCAST_SMEM=0
-// selects the LDS kernel, for cross-checks).
+// Bernoulli BCAST sites over unmasked contiguous data run k_site_bcast_smem.
 bool bcast_smem(const mi_group* g) {
-  static const bool enabled = env_int("MININF_AMD_BCAST_SMEM", 1) != 0;
   const mi_site& st = g->sites[0];
-  return enabled && (st.family == MI_BERNOULLI_LOGITS || st.family == MI_BERNOULLI_PROBS) &&
+  return (st.family == MI_BERNOULLI_LOGITS || st.family == MI_BERNOULLI_PROBS) &&
          st.mask == nullptr && g->operands[st.operand[2]].stride_i == 1;
 }
 
-// k_site_bcast_smem launch variants: particles per lane, chunk length (MININF_AMD_BCAST_TUNE).
-struct SmemVariant {
-  int p;
-  int chunk;
-};
-constexpr SmemVariant kSmemVariants[] = {{4, 4096}, {8, 4096}, {4, 8192}, {8, 8192}, {8, 2048}};
-
-int smem_variant() {
-  static const int v = [] {
-    const int n = env_int("MININF_AMD_BCAST_TUNE", 0);
-    return (n >= 0 && n < (int)(sizeof(kSmemVariants) / sizeof(kSmemVariants[0]))) ? n : 0;
-  }();
-  return v;
-}
-
-// Dynamic LDS reserved by the BCAST launches (tuning: caps the workgroups per CU).
-unsigned bcast_lds() {
-  static const unsigned bytes = (unsigned)env_int("MININF_AMD_BCAST_LDS", 0);
-  return bytes;
-}
+// k_site_bcast_smem: particles per lane and chunk length (measured r02: the best of {4, 8} x
+// {2048, 4096, 8192})
+constexpr int kSmemP = 4;
+constexpr int kSmemChunk = 4096;
 
 struct Plan {
   Shape shape;
@@ -1169,13 +1137,12 @@ Plan make_plan(const mi_group* g) {
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     const bool smem = bcast_smem(g);
-    const SmemVariant v = kSmemVariants[smem_variant()];
-    const int64_t chunks = ceil_div(g->N, smem ? v.chunk : mi::kBcastChunk);
+    const int64_t chunks = ceil_div(g->N, smem ? kSmemChunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
     const int64_t side = (smem && g->side.out != nullptr)
                              ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
     p.grid = dim3((unsigned)(chunks + side),
-                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? v.p : mi::kBcastP)));
+                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? kSmemP : mi::kBcastP)));
     return p;
   }
   int dense = -1;
@@ -1192,15 +1159,13 @@ Plan make_plan(const mi_group* g) {
     p.shape = kRow;
     p.draw = g->draw.operand != 0;
     // fused draws: one Philox quad per lane and row keeps the register footprint at 4 waves/SIMD
-    p.elems = g->draw.operand != 0 ? (env_int("MININF_AMD_DRAW_ELEMS", 4) == 8 ? 8 : 4)
-                                   : row_elems();
+    p.elems = g->draw.operand != 0 ? 4 : kRowElems;
     p.nseg = ceil_div(g->N, 64 * p.elems);
     const int64_t gx = ceil_div(p.nseg, 4);
-    // fused draws: about one round of 4-wave blocks (MININF_AMD_DRAW_TARGET_BLOCKS) -- fewer,
-    // longer particle blocks write fewer d loc / d scale partial rows for the same balance
-    const int64_t target = p.draw ? env_int("MININF_AMD_DRAW_TARGET_BLOCKS", (int)kTargetBlocks)
-                                  : kTargetBlocks;
-    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64), ceil_div(target, gx)));
+    // about two rounds of 4-wave blocks (fused draws: fewer, longer particle blocks write fewer
+    // d loc / d scale partial rows for the same balance; r04/r05 sweeps kept this target)
+    int64_t gy = std::max<int64_t>(1, std::min<int64_t>(ceil_div(g->K, 64),
+                                                        ceil_div(kTargetBlocks, gx)));
     p.rows_per_block = ceil_div(g->K, gy);
     gy = ceil_div(g->K, p.rows_per_block);
     p.grid = dim3((unsigned)gx, (unsigned)gy);
@@ -1226,17 +1191,11 @@ PlanInfo plan_info(const Plan& p, bool combined) {
   PlanInfo info{};
   info.combined = combined;
   info.row = p.shape == kRow;
-  // Tuning knobs (measured defaults; the env overrides exist for sweeps).
-  info.elems = p.shape == kRow ? p.elems : std::max(1, env_int("MININF_AMD_COL_UNROLL",
-                                                                     kColUnroll));
-  info.waves_per_eu = env_int("MININF_AMD_WAVES_PER_EU", 0);
-  info.unroll = std::max(1, env_int("MININF_AMD_DRAW_UNROLL", 1));
+  info.elems = p.shape == kRow ? p.elems : kColUnroll;
   // fused draws: the block's four waves combine their particle sums (a quarter of the partial rows:
   // C5's 3907 segments become 977 rows, within the ELBO forward's fused reduction)
-  info.block_rows = info.row && p.draw && env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0;
-  info.packed = info.row && p.draw && env_int("MININF_AMD_PACKED", 1) != 0;
-  info.tile_rows = env_int("MININF_AMD_TILE_ROWS", 0);
-  info.balance = info.row && env_int("MININF_AMD_ROW_BALANCE", 0) != 0;   // measured: no gain on C5 (two rounds of waves, not a lone-wave tail)
+  info.block_rows = info.row && p.draw;
+  info.packed = info.row && p.draw;
   info.kw = p.kw;
   info.grid_x = p.grid.x;
   info.grid_y = p.grid.y;
@@ -1270,8 +1229,7 @@ size_t finalize_offset(const mi_group* g, const Plan& p) {
 // The slot value of a k_site_bcast_smem launch in the rank-one layout (mi_reduce.rank1): one
 // slot, and a segment list short enough for the one-launch finalize / the fused reduction.
 bool smem_rank1(const mi_group* g, const Plan& p) {
-  return g->num_slots == 1 && g->compute_grads && p.nseg >= 3 && p.nseg <= MI_REDUCE_MAX_SEG &&
-         env_int("MININF_AMD_BCAST_RANK1", 1) != 0;
+  return g->num_slots == 1 && g->compute_grads && p.nseg >= 3 && p.nseg <= MI_REDUCE_MAX_SEG;
 }
 
 template <int FAM>
@@ -1283,24 +1241,15 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   const int64_t side = (int64_t)p.grid.x - chunks;
   const int gy = (int)p.grid.y;
   const dim3 grid((unsigned)(ceil_div(chunks, 8) * 8 * gy + side));
-  const int rank1 = (smem_rank1(&G, p) ? 1 : 0) | (env_int("MININF_AMD_BCAST_BALANCE", 1) ? 2 : 0) |
-                    (env_int("MININF_AMD_BCAST_PREFETCH", 0) ? 4 : 0);
-#define MI_SMEM(P, CH) \
-  hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, P, CH>), grid, block, bcast_lds(), s, G, part, p.nseg, gy, rank1, flags)
-  switch (smem_variant()) {
-    case 1: MI_SMEM(8, 4096); break;
-    case 2: MI_SMEM(4, 8192); break;
-    case 3: MI_SMEM(8, 8192); break;
-    case 4: MI_SMEM(8, 2048); break;
-    default:
-      if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
-        hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, 4, 4096, true>), grid, block, bcast_lds(),
-                           s, G, part, p.nseg, gy, rank1, flags);
-      else
-        MI_SMEM(4, 4096);
-      break;
-  }
-#undef MI_SMEM
+  const int rank1 = (smem_rank1(&G, p) ? 1 : 0) | 2;   // bit 2: progress-balanced priorities
+  // MININF_AMD_BCAST_SUFFSTAT=1: the reducible-floor measurement of bench.py (sum_i x_i l_k as
+  // l_k sum_i x_i), never the default
+  if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
+    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, kSmemChunk, true>), grid, block, 0, s,
+                       G, part, p.nseg, gy, rank1, flags);
+  else
+    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, kSmemChunk>), grid, block, 0, s, G,
+                       part, p.nseg, gy, rank1, flags);
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
@@ -1386,8 +1335,7 @@ int mi_group_prior_supported(const mi_group* group, int* supported) {
   // block-row flush); either way on site 0's per-particle parameter, an operand (stride_i == 0)
   const int o = group->sites[0].operand[0];
   const bool host = (p.shape == kBcast && bcast_smem(group) && group->num_sites == 1) ||
-                    (p.shape == kRow && p.draw && draw_supported(group) && mi_jit_enabled() &&
-                     env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0);
+                    (p.shape == kRow && p.draw && draw_supported(group) && mi_jit_enabled());
   *supported = (host && o >= 0 && group->operands[o].stride_i == 0 &&
                 group->operands[o].stride_k != 0 &&
                 group->prior.scale == group->sites[0].scale) ? 1 : 0;
@@ -1400,7 +1348,6 @@ int mi_group_pdraw_supported(const mi_group* group, int* supported) {
   // a fused-draw site program (row shape, block-row partials) whose particle block fits the
   // program's LDS table of per-particle values
   *supported = (p.shape == kRow && p.draw && draw_supported(group) && mi_jit_enabled() &&
-                env_int("MININF_AMD_DRAW_BLOCK_ROWS", 1) != 0 &&
                 p.rows_per_block <= kPdrawMax) ? 1 : 0;
   return 0;
 }
@@ -1494,10 +1441,10 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
 #define MI_LAUNCH_BCAST(FAM)                                                                   \
   case FAM:                                                                                    \
     if (masked)                                                                                \
-      hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), bcast_lds(), s, \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, true>), p.grid, dim3(mi::kBcastThreads), 0, s,         \
                          G, prep, part, p.nseg, flags);                                        \
     else                                                                                       \
-      hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), bcast_lds(),   \
+      hipLaunchKernelGGL((mi::k_site_bcast<FAM, false>), p.grid, dim3(mi::kBcastThreads), 0,             \
                          s, G, prep, part, p.nseg, flags);                                     \
     break;
         MI_LAUNCH_BCAST(MI_BERNOULLI_LOGITS)

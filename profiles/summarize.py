@@ -44,6 +44,9 @@ FETCH_SCALE = {"c2": 1.0}
 # exactly once) and the known input bytes divided by the raw FETCH_SIZE give the factor:
 # y, b, the guide's loc and unconstrained scale (4 B each) and the shared mask (1 B), n = 1e6.
 C5_CAL_BYTES = 1_000_000 * (4 + 4 + 4 + 4 + 1)
+# C3 / C4 ("Next round" 2): the linear site kernel's scale from a K = 32 run of C3
+# (fetch_c3cal: one particle tile, so X [1e6, 32] and y [1e6] are each read exactly once)
+C3_CAL_BYTES = 1_000_000 * (32 * 4 + 4)
 OTHERS = r"k_elbo_forward|k_elbo_backward|k_adam_step|k_minibatch_rows|k_finalize"
 
 
@@ -95,8 +98,53 @@ def c5_calibration(raw: str):
     return C5_CAL_BYTES / (1024.0 * kb), kb
 
 
+def c3_calibration(raw: str):
+    """(scale, raw KB) of the linear kernel's FETCH_SIZE from C3's K = 32 run, or None."""
+    fetch = counters(raw, "fetch", "c3cal")
+    if not fetch:
+        return None
+    keys = [k for k in fetch if re.search(DOMINANT["c3"], k[0])]
+    if not keys:
+        return None
+    kb = per_launch(fetch[max(keys, key=lambda k: k[1])])
+    return C3_CAL_BYTES / (1024.0 * kb), kb
+
+
+def replay_durations(raw: str, round_tag: str) -> None:
+    """Average duration of each config's dominant kernel over the graph-replayed launches of the
+    stats run (the second half of its launches: the first are eager warm-up steps), next to the
+    bench line's span-stamp kernel_ms -- <round>_kernel_replay.json."""
+    out = {}
+    for cfg, pattern in DOMINANT.items():
+        src = os.path.join(raw, f"stats_{cfg}", "run_kernel_trace.csv")
+        if not os.path.exists(src):
+            continue
+        rows = [r for r in csv.DictReader(open(src)) if re.search(pattern, r["Kernel_Name"]) and
+                "true>" not in short(r["Kernel_Name"])[-8:]]
+        if not rows:
+            continue
+        grid = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
+        rows = [r for r in rows if int(r.get("Grid_Size", 0) or 0) == grid]
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+        tail = d[len(d) // 2:]
+        out[cfg] = {"kernel": short(rows[0]["Kernel_Name"]), "grid_size": grid, "launches": len(d),
+                    "replay_launches": len(tail), "replay_avg_us": sum(tail) / len(tail),
+                    "replay_min_us": min(tail), "replay_max_us": max(tail),
+                    "all_avg_us": sum(d) / len(d)}
+    with open(os.path.join(HERE, f"{round_tag}_kernel_replay.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
 def pmc(raw: str, round_tag: str) -> None:
     result = {}
+    cal3 = c3_calibration(raw)
+    if cal3 is not None:
+        FETCH_SCALE["c3"] = FETCH_SCALE["c4"] = cal3[0]
+        result["c3_calibration"] = {
+            "known_input_bytes": C3_CAL_BYTES, "raw_fetch_size_kb_at_k32": cal3[1],
+            "fetch_scale": cal3[0],
+            "note": "C3 at K = 32: one particle tile, X and y read once; the same scale is applied "
+                    "to C4 (the same kernel, its rows gathered through the minibatch index)"}
     cal = c5_calibration(raw)
     if cal is not None:
         FETCH_SCALE["c5"] = cal[0]
@@ -195,6 +243,7 @@ def main() -> None:
     raw = sys.argv[2] if len(sys.argv) > 2 else os.path.join(HERE, "..", "gpurun_out")
     for cfg in ("c2", "c3", "c4", "c5"):
         kernel_stats(raw, round_tag, cfg)
+    replay_durations(raw, round_tag)
     pmc(raw, round_tag)
     valu(raw, round_tag)
 

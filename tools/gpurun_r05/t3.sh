@@ -24,6 +24,7 @@ for c in c2 c3 c4 c5; do
   prof 150 fetch_$c --pmc FETCH_SIZE -d gpurun_out/fetch_$c -o run --output-format csv -- $P --config $c || exit 1
   prof 150 write_$c --pmc WRITE_SIZE -d gpurun_out/write_$c -o run --output-format csv -- $P --config $c || exit 1
 done
+prof 150 fetch_c3cal --pmc FETCH_SIZE -d gpurun_out/fetch_c3cal -o run --output-format csv -- $P --config c3 --particles-per-gpu 32 || exit 1
 prof 150 fetch_c5cal --pmc FETCH_SIZE -d gpurun_out/fetch_c5cal -o run --output-format csv -- $P --config c5 --particles-per-gpu 64 || exit 1
 prof 150 write_c5cal --pmc WRITE_SIZE -d gpurun_out/write_c5cal -o run --output-format csv -- $P --config c5 --particles-per-gpu 64 || exit 1
 exit 0
