@@ -110,6 +110,17 @@ def deferred() -> Optional[list]:
     return getattr(_STATE, "collector", None)
 
 
+def mirrors_flags() -> bool:
+    """
+    Whether the step being run copies its sticky validation words to the host: every step except
+    the first R - 1 of the R steps one StepGraph replay holds (their words are sticky, so the last
+    step's copy carries them; the others skip a host-mapped write at the end of their ELBO
+    forward).
+    """
+    position = getattr(_STATE, "capture_position", None)
+    return position is None or position[0] == position[1] - 1
+
+
 @contextlib.contextmanager
 def graph_safe(collector: list):
     """
@@ -295,10 +306,15 @@ class StepGraph:
                 # as the graph (particles.device_copy's cache may evict them)
                 with graph_safe(self._joints), _capture_safe_distributions(), \
                         particles.pin_device_copies() as self._pinned:
-                    for _ in range(repeat):
-                        # detached: holding the captured step's autograd graph would keep its
-                        # AccumulateGrad nodes (and their capture stream) alive past the capture
-                        self.output = _detached(step())
+                    try:
+                        for r in range(repeat):
+                            _STATE.capture_position = (r, repeat)
+                            # detached: holding the captured step's autograd graph would keep its
+                            # AccumulateGrad nodes (and their capture stream) alive past the
+                            # capture
+                            self.output = _detached(step())
+                    finally:
+                        _STATE.capture_position = None
                     _flush_held_launch()   # (a step without an optimizer leaves it held)
                     mirror = self._record_validation(count)
                 self.graph.capture_end()
@@ -346,7 +362,7 @@ class StepGraph:
                           j.flags.data_ptr() == sticky[0].flags.data_ptr() for j in sticky):
             self._flags_device = sticky[0].flags
             self._accumulator = None
-            mirror = sticky[0].mirror
+            mirror = sticky[-1].mirror   # (only the last step writes it: mirrors_flags)
         else:
             any_flags = False
             for joints in steps:

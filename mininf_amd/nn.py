@@ -546,7 +546,8 @@ class EvidenceLowerBoundLoss(nn.Module):
                     if self._mirror is None and not torch.cuda.is_current_stream_capturing():
                         self._mirror = torch.zeros(self.FLAG_WORDS, dtype=torch.int32,
                                                    pin_memory=True)
-                    flags, sticky, mirror = self._sticky_flags, True, self._mirror
+                    flags, sticky = self._sticky_flags, True
+                    mirror = self._mirror if graph.mirrors_flags() else None
                 else:
                     flags = self._zeroed_flags(device)
             else:   # the samplers reject host guides with the engine's device error

@@ -88,3 +88,18 @@ def test_eager_validation_words_are_fresh_zeroed_rows():
     assert len(set(ptrs)) == len(ptrs)   # (the first block is still alive through its rows)
     rows[0].fill_(7)                     # a step's kernels write its words ...
     assert not loss._zeroed_flags(device).any()   # ... and no later step sees them
+
+
+def test_only_the_last_captured_step_mirrors_the_validation_words():
+    """StepGraph(repeat=R) captures R steps whose sticky validation words are the same device
+    words: only the last step's ELBO forward copies them to the pinned host mirror
+    (graph.mirrors_flags); outside a capture every step does."""
+    from mininf_amd import graph
+    assert graph.mirrors_flags()
+    seen = []
+    for r in range(3):
+        graph._STATE.capture_position = (r, 3)
+        seen.append(graph.mirrors_flags())
+    graph._STATE.capture_position = None
+    assert seen == [False, False, True]
+    assert graph.mirrors_flags()
