@@ -18,3 +18,4 @@ for c in c2 c4 c5 c3; do
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
 timeout -k 10 120 python3 -u tools/graph_branch_probe.py > gpurun_out/branch_probe.log 2>&1; echo "branch rc=$?"; tail -1 gpurun_out/branch_probe.log
+timeout -k 10 120 tools/_timing/stream_probe > gpurun_out/stream_probe.log 2>&1; echo "stream rc=$?"; cat gpurun_out/stream_probe.log
