@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 15
+#define MI_ABI_VERSION 16
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -585,9 +585,11 @@ int mi_gather_rows(const void* base, int64_t base_stride_bytes, int64_t row_byte
  *   m = beta1 m + (1 - beta1) g;  v = beta2 v + (1 - beta2) g^2
  *   param -= lr / (1 - beta1^s) * m / (sqrt(v) / sqrt(1 - beta2^s) + eps);  *step = s
  * per tensor (its own step word, fp32 as torch keeps it). `counters`: MI_ADAM_COUNTER_WORDS uint32
- * words, zero before first use; every launch leaves them zero. */
+ * words, zero before first use, owned by one caller's launches on one stream: the completion
+ * counters (every launch leaves them zero), then a cache of the next step's bias corrections per
+ * tensor slot (ABI 16; a slot that does not match the step and betas is recomputed). */
 #define MI_ADAM_MAX_TENSORS 8
-#define MI_ADAM_COUNTER_WORDS (MI_ADAM_MAX_TENSORS * 33)
+#define MI_ADAM_COUNTER_WORDS (MI_ADAM_MAX_TENSORS * 33 + MI_ADAM_MAX_TENSORS * 16)
 typedef struct mi_adam_tensor {
   float* param;
   const float* grad;

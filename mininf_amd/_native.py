@@ -38,7 +38,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 15   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 16   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -168,7 +168,7 @@ class Elbo(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 8
-ADAM_COUNTER_WORDS = ADAM_MAX_TENSORS * 33
+ADAM_COUNTER_WORDS = ADAM_MAX_TENSORS * 33 + ADAM_MAX_TENSORS * 16
 
 
 class AdamTensor(ctypes.Structure):

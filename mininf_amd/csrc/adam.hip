@@ -10,6 +10,14 @@
 // Every block reads its tensor's step s and uses s + 1; the last block of the tensor to finish
 // (completion count, two levels: groups of kGroup blocks, then the tensor) stores s + 1, so no
 // block can read the advanced value.
+//
+// The bias corrections (two double pows, a few hundred dependent instructions) are computed once
+// per tensor and step: the tensor's first block computes those of the next step while its loads
+// are in flight and stores them in the counter words' cache (a slot per tensor and step parity,
+// keyed by step and betas); the next launch's blocks read them instead of each computing them
+// (tools/stream_probe.hip: the per-block pows cost 1.5 us of a 7 us update at 512 blocks, 5 us at
+// 2048). A slot that does not match (first step, a loaded step count, changed betas) falls back to
+// the pows -- the same function of the same inputs either way.
 #include "adam_math.hpp"
 #include "common.hpp"
 #include "internal.hpp"
@@ -22,6 +30,16 @@ namespace mi {
 
 constexpr int kAdamThreads = 256;
 constexpr int kAdamGroup = 32;
+
+// counter words after the completion counters: [tensor][step parity] slots of kCoefWords
+constexpr int kCoefWords = 8;   // step s + 1 (float), bc1, bc2_sqrt, -, beta1 (double), beta2
+constexpr int kCoefOffset = MI_ADAM_MAX_TENSORS * (1 + kAdamGroup);
+static_assert(kCoefOffset + MI_ADAM_MAX_TENSORS * 2 * kCoefWords <= MI_ADAM_COUNTER_WORDS,
+              "counter words");
+
+MI_DEV unsigned* coef_slot(unsigned* counters, int t, float s1) {
+  return counters + kCoefOffset + (t * 2 + ((int)s1 & 1)) * kCoefWords;
+}
 
 struct AdamPlan {
   int first[MI_ADAM_MAX_TENSORS + 1];   // first block of each tensor
@@ -132,7 +150,38 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
     __builtin_amdgcn_s_barrier();
     if (threadIdx.x == 0) started_last = last_block();
   }
-  const AdamCoef coef = adam_coef(A, s1);   // (adam_math.hpp: torch's fused Adam arithmetic)
+  // bias corrections: the cached ones of this step if the slot matches, else computed here
+  // (adam_math.hpp: torch's fused Adam arithmetic either way)
+  AdamCoef coef;
+  {
+    const unsigned* slot = coef_slot(counters, t, s1);
+    const bool hit = __uint_as_float(slot[0]) == s1 &&
+                     __hiloint2double(slot[5], slot[4]) == A.beta1 &&
+                     __hiloint2double(slot[7], slot[6]) == A.beta2;
+    if (hit) {
+      coef.bc1 = __uint_as_float(slot[1]);
+      coef.bc2_sqrt = __uint_as_float(slot[2]);
+      coef.step_size = (float)(A.lr / (double)coef.bc1);
+    } else {
+      coef = adam_coef(A, s1);
+    }
+  }
+  // the tensor's first block: the next step's corrections, into the other parity's slot (no block
+  // of this launch reads it)
+  if (b == 0 && threadIdx.x < 64) {
+    const float s2 = s1 + 1.0f;
+    const AdamCoef next = adam_coef(A, s2);
+    if (threadIdx.x == 0) {
+      unsigned* slot = coef_slot(counters, t, s2);
+      slot[1] = __float_as_uint(next.bc1);
+      slot[2] = __float_as_uint(next.bc2_sqrt);
+      slot[4] = (unsigned)__double2loint(A.beta1);
+      slot[5] = (unsigned)__double2hiint(A.beta1);
+      slot[6] = (unsigned)__double2loint(A.beta2);
+      slot[7] = (unsigned)__double2hiint(A.beta2);
+      slot[0] = __float_as_uint(s2);
+    }
+  }
   auto update = [&](float& param, float grad, float& m, float& v) {
     adam_update(A, coef, param, grad, m, v);
   };
@@ -203,11 +252,11 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
       return MI_EINVAL;
     total += T.numel;
   }
-  // A few hundred workgroups over all tensors: measured on C5's 2 x 1e6 parameters
-  // (tools/adam_probe.py, profiles/r03_adam_sweep.log), 500 workgroups of 4096 elements run at
-  // 12.5 us, 980 of 2048 at 17 us; at least 4 * kAdamThreads elements per workgroup and at most
-  // kAdamGroup^2 workgroups per tensor.
-  constexpr int64_t target_blocks = 512;
+  // About 1024 workgroups over all tensors (C5's 2 x 1e6 parameters: 1024 of 2048 elements; with
+  // per-block pows 500 of 4096 had run faster, 12.5 us against 17, profiles/r03_adam_sweep.log --
+  // tools/stream_probe.hip without them: 7.0 us at 512, 6.6 at 1024, 6.7 at 2048); at least
+  // 4 * kAdamThreads elements per workgroup and at most kAdamGroup^2 workgroups per tensor.
+  constexpr int64_t target_blocks = 1024;
   constexpr int64_t min_chunk = 4 * mi::kAdamThreads;
   const int64_t even = (total + target_blocks - 1) / target_blocks;
   int blocks = 0;

@@ -114,6 +114,13 @@ MI_DEV float keep_if(float x, bool keep) {
   return __uint_as_float(__float_as_uint(x) & m);
 }
 
+MI_DEV double keep_if_d(double x, bool keep) {
+  uint32_t m = keep ? 0xffffffffu : 0u;
+  asm volatile("" : "+v"(m));
+  const uint64_t u = (uint64_t)__double_as_longlong(x) & (((uint64_t)m << 32) | m);
+  return __longlong_as_double((long long)u);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Wavefront reductions.
 // ---------------------------------------------------------------------------------------------

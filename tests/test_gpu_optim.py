@@ -45,6 +45,35 @@ def test_matches_torch_fused_adam(device, kwargs):
         assert float(sa["step"]) == float(sb["step"])
 
 
+def test_cached_bias_corrections_follow_betas_and_loaded_steps(device):
+    """The launch caches the next step's bias corrections in its counter words (keyed by step
+    and betas): changed betas, a rewound step count and a reordered tensor list between steps
+    still give torch's fused Adam bit for bit."""
+    shapes = [(5,), (4096,), (300_000,)]
+    ours, ref = make(device, shapes), make(device, shapes)
+    opt = Adam(ours, lr=0.01)
+    opt_ref = torch.optim.Adam(ref, lr=0.01, fused=True)
+    gen = torch.Generator().manual_seed(3)
+    for step in range(9):
+        if step == 3:
+            for o in (opt, opt_ref):
+                o.param_groups[0]["betas"] = (0.8, 0.95)
+        if step == 5:   # rewind one tensor's step count (as a loaded checkpoint would)
+            opt.state[ours[1]]["step"].fill_(1.0)
+            opt_ref.state[ref[1]]["step"].fill_(1.0)
+        grads = [torch.randn(s, generator=gen).to(device) for s in shapes]
+        for k, (a, b, g) in enumerate(zip(ours, ref, grads)):
+            skip = step == 6 and k == 0   # the tensor slots shift for one step
+            a.grad = None if skip else g.clone()
+            b.grad = None if skip else g.clone()
+        opt.step()
+        opt_ref.step()
+        for a, b in zip(ours, ref):
+            assert torch.equal(a, b), step
+    for a, b in zip(ours, ref):
+        assert float(opt.state[a]["step"]) == float(opt_ref.state[b]["step"])
+
+
 def test_captured_steps_advance(device):
     params = make(device, [(4,), (100_000,)])
     ref = make(device, [(4,), (100_000,)])
