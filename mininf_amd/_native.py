@@ -16,7 +16,9 @@ import torch
 
 
 LIB_NAME = "libmininf_amd.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# MININF_AMD_LIB: another build of the library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("MININF_AMD_LIB") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 MAX_SITES = 4
 MAX_OPERANDS = 6

@@ -7,17 +7,17 @@
 // ADAM_MODE::ORIGINAL, no AMSGrad): hyper-parameters in double, the moments and the parameter in
 // float, bias corrections 1 - beta^step in double -- bit-identical to torch.optim.Adam(fused=True).
 //
-// Every block reads its tensor's step s and uses s + 1; the last block of the tensor to finish
-// (completion count, two levels: groups of kGroup blocks, then the tensor) stores s + 1, so no
+// Every block reads its tensor's step s and uses s + 1; the last block of the tensor to count
+// itself after its read (two levels: groups of kAdamGroup blocks, then the tensor) stores s + 1, so no
 // block can read the advanced value.
 //
 // The bias corrections (two double pows, a few hundred dependent instructions) are computed once
-// per tensor and step: the tensor's first block computes those of the next step while its loads
-// are in flight and stores them in the counter words' cache (a slot per tensor and step parity,
+// per tensor and step: the bookkeeping wave of the tensor's first block computes those of the next
+// step and stores them in the counter words' cache (a slot per tensor and step parity,
 // keyed by step and betas); the next launch's blocks read them instead of each computing them
-// (tools/stream_probe.hip: the per-block pows cost 1.5 us of a 7 us update at 512 blocks, 5 us at
-// 2048). A slot that does not match (first step, a loaded step count, changed betas) falls back to
-// the pows -- the same function of the same inputs either way.
+// (C5's update 12.63 -> 12.43 us, the step 182.5 -> 181.5 us, profiles/r05_adam_ab.json). A slot
+// that does not match (first step, a loaded step count, changed betas) falls back to the pows --
+// the same function of the same inputs either way.
 #include "adam_math.hpp"
 #include "common.hpp"
 #include "internal.hpp"
@@ -55,37 +55,104 @@ MI_DEV T pick_adam(const T (&arr)[N], int a) {
   return v;
 }
 
-MI_DEV mi_adam_tensor tensor_at(const mi_adam& A, int t) { return adam_tensor_at(A, t); }
-
-// NT: non-temporal 16-byte loads and stores (measured slower on C5: the launch uses plain ones)
-typedef float f4v __attribute__((ext_vector_type(4)));
-MI_DEV float4 ld(const float4* p, bool nt) {
-  if (!nt) return *p;
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
+// Every kernel argument a block needs, loaded in one batch at its start: the plan's block ranges and
+// chunks and the NT tensors' fields, each pinned to a register (an empty asm) so that the selection
+// of the block's tensor runs on registers. Left to itself the compiler turned the selects into
+// indexed loads of the argument segment -- two more dependent round trips before the block's first
+// data loads (the C5 update: ~3 us of a 12 us launch).
+template <typename V>
+MI_DEV V pin(V v) {
+  asm("" : "+s"(v));
+  return v;
 }
-MI_DEV void st(float4* p, const float4& v, bool nt) {
-  if (!nt) {
-    *p = v;
-    return;
+// (a pointer through its address, handed back in the global address space: global, not flat,
+// accesses)
+template <typename V>
+MI_DEV V* pin_ptr(V* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t a = pin(reinterpret_cast<uint64_t>(p));
+  return (V*)reinterpret_cast<__attribute__((address_space(1))) V*>(a);
+#else
+  return p;   // (host pass: never called)
+#endif
+}
+
+template <int NT>
+struct Picked {
+  mi_adam_tensor T;
+  int first, nblocks, t;
+  int64_t chunk;
+};
+
+template <int NT>
+MI_DEV Picked<NT> pick_tensor(const mi_adam& A, const AdamPlan& P) {
+  int first[NT + 1];
+  int64_t chunk[NT];
+  float* param[NT];
+  const float* grad[NT];
+  float* m[NT];
+  float* v[NT];
+  int64_t numel[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    first[q] = pin(P.first[q]);
+    chunk[q] = pin(P.chunk[q]);
+    param[q] = pin_ptr(A.tensors[q].param);
+    grad[q] = pin_ptr(A.tensors[q].grad);
+    m[q] = pin_ptr(A.tensors[q].exp_avg);
+    v[q] = pin_ptr(A.tensors[q].exp_avg_sq);
+    numel[q] = pin(A.tensors[q].numel);
   }
-  const f4v w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
-}
-
-template <bool NT, int U>
-__global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, const AdamPlan P,
-                                                             unsigned* __restrict__ counters,
-                                                             int count) {
+  first[NT] = pin(P.first[NT]);
+  const int num = pin(A.num);
   int t = 0;
 #pragma unroll
-  for (int q = 1; q < MI_ADAM_MAX_TENSORS; ++q)
-    if (q < A.num && (int)blockIdx.x >= P.first[q]) t = q;
-  const mi_adam_tensor T = tensor_at(A, t);
-  const int first = pick_adam(P.first, t);
-  const int nblocks = pick_adam(P.first, t + 1) - first;
-  const int64_t chunk = pick_adam(P.chunk, t);
+  for (int q = 1; q < NT; ++q)
+    if (q < num && (int)blockIdx.x >= first[q]) t = q;
+  Picked<NT> r;
+  // (the step word's address by the ordinary indexed argument load: its read must stay a scalar
+  // load, which the barrier's lgkmcnt wait covers -- see k_adam_step; it is off the data loads' path)
+  r.T = mi_adam_tensor{param[0], grad[0], m[0], v[0], nullptr, numel[0]};
+  r.first = first[0];
+  r.nblocks = first[1] - first[0];
+  r.chunk = chunk[0];
+#pragma unroll
+  for (int q = 1; q < NT; ++q) {
+    const bool on = q == t;
+    r.T.param = on ? param[q] : r.T.param;
+    r.T.grad = on ? grad[q] : r.T.grad;
+    r.T.exp_avg = on ? m[q] : r.T.exp_avg;
+    r.T.exp_avg_sq = on ? v[q] : r.T.exp_avg_sq;
+    r.T.numel = on ? numel[q] : r.T.numel;
+    r.first = on ? first[q] : r.first;
+    r.nblocks = on ? first[q + 1] - first[q] : r.nblocks;
+    r.chunk = on ? chunk[q] : r.chunk;
+  }
+  r.t = t;
+  r.T.step = A.tensors[t].step;
+  return r;
+}
+
+// The launch's workgroups are kAdamThreads streaming threads plus one bookkeeping wave: the
+// streaming waves update their elements; the extra wave counts the workgroup in the tensor's
+// completion count (device-scope atomics on shared words: the return of each is a memory round
+// trip, longer under contention) and, in the tensor's first workgroup, computes the next step's bias
+// corrections -- neither stalls a streaming wave (counted by streaming wave 0 and computed by
+// streaming lanes, they had held that wave's elements back: the C5 update ran 12.1 us in
+// tools/stream_probe.hip against 7.8 for the same arithmetic without them).
+constexpr int kAdamBlock = kAdamThreads + 64;
+
+// NT: tensor slots the launch selects from (A.num <= NT: fewer kernel-argument loads before the
+// block's first data loads)
+template <int U, int NT>
+__global__ __launch_bounds__(kAdamBlock) void k_adam_step(const mi_adam A, const AdamPlan P,
+                                                          unsigned* __restrict__ counters) {
+  const Picked<NT> pk = pick_tensor<NT>(A, P);
+  const mi_adam_tensor T = pk.T;
+  const int t = pk.t, first = pk.first, nblocks = pk.nblocks;
+  const int64_t chunk = pk.chunk;
   const int b = (int)blockIdx.x - first;
+  const bool books = threadIdx.x >= kAdamThreads;   // the bookkeeping wave
 
   const int64_t i0 = (int64_t)b * chunk;
   const int64_t i1 = min(T.numel, i0 + chunk);
@@ -106,80 +173,82 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
       const int64_t e = base + u * kStride;
       if (e + 3 < i1) {
         const int64_t q = e >> 2;
-        p[u] = ld(param + q, NT);
-        g[u] = ld(grad + q, NT);
-        m[u] = ld(exp_avg + q, NT);
-        v[u] = ld(exp_avg_sq + q, NT);
+        p[u] = param[q];
+        g[u] = grad[q];
+        m[u] = exp_avg[q];
+        v[u] = exp_avg_sq[q];
       }
     }
   };
   int64_t i = i0 + 4 * (int64_t)threadIdx.x;
-  // the first pass's loads go out before the bias corrections (two double pows, a few hundred
-  // dependent instructions): without the barrier the compiler hoists them ahead of every load
-  if (vec) load_pass(i);
+  // the first pass's loads go out before anything that waits (the step read, the bias corrections)
+  if (vec && !books) load_pass(i);
   __builtin_amdgcn_sched_barrier(0);
 
-  // bias corrections in double, then handed to the update as float (adam_math's opmath_t
-  // parameters)
   const float s1 = *T.step + 1.0f;
-  // The step advances once every workgroup of the tensor has read it: counted at the end
-  // (count 1), or right after the read (count 2: the atomic's return is awaited only at the end,
-  // behind this workgroup's own traffic); count 0 leaves the step alone (timing probes only).
-  auto last_block = [&]() {
-    unsigned* tc = counters + t * (1 + kAdamGroup);
-    const int groups = (nblocks + kAdamGroup - 1) / kAdamGroup;
-    bool done = true;
-    if (groups > 1) {
-      const int g = b / kAdamGroup;
-      const unsigned in_group = (unsigned)min(kAdamGroup, nblocks - g * kAdamGroup);
-      unsigned* gc = tc + 1 + g;
-      done = atomicAdd(gc, 1u) == in_group - 1u;
-      if (done) *gc = 0u;
+  // both parities' cached bias corrections, read with the step (one memory round trip, not two
+  // dependent ones: which slot applies depends on the step); named words, not an array (a private
+  // array indexed by the parity was placed in LDS through the thread's flat index)
+  const uint32_t* cw = counters + kCoefOffset + t * 2 * kCoefWords;
+  const uint32_t e0 = cw[0], e1 = cw[1], e2 = cw[2], e4 = cw[4], e5 = cw[5], e6 = cw[6], e7 = cw[7];
+  const uint32_t o0 = cw[8], o1 = cw[9], o2 = cw[10], o4 = cw[12], o5 = cw[13], o6 = cw[14],
+                 o7 = cw[15];
+  // The step advances once every workgroup of the tensor has read it: every wave's step read
+  // complete (lgkmcnt(0) only: the first pass's loads stay in flight), the barrier, then the
+  // bookkeeping wave counts the workgroup (two levels: groups of kAdamGroup, then the tensor); the
+  // tensor's last workgroup to count stores s + 1 (every workgroup has read s by then).
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  if (books) {
+    if (threadIdx.x == kAdamThreads) {
+      unsigned* tc = counters + t * (1 + kAdamGroup);
+      const int groups = (nblocks + kAdamGroup - 1) / kAdamGroup;
+      bool done = true;
+      if (groups > 1) {
+        const int gi = b / kAdamGroup;
+        const unsigned in_group = (unsigned)min(kAdamGroup, nblocks - gi * kAdamGroup);
+        unsigned* gc = tc + 1 + gi;
+        done = atomicAdd(gc, 1u) == in_group - 1u;
+        if (done) *gc = 0u;
+      }
+      if (done && atomicAdd(tc, 1u) == (unsigned)(groups > 1 ? groups : nblocks) - 1u) {
+        *tc = 0u;
+        *T.step = s1;
+      }
     }
-    if (done && atomicAdd(tc, 1u) == (unsigned)(groups > 1 ? groups : nblocks) - 1u) {
-      *tc = 0u;
-      return true;
+    // the tensor's first workgroup: the next step's corrections, into the other parity's slot (no
+    // workgroup of this launch reads it)
+    if (b == 0) {
+      const float s2 = s1 + 1.0f;
+      const AdamCoef next = adam_coef(A, s2);
+      if (threadIdx.x == kAdamThreads) {
+        unsigned* slot = coef_slot(counters, t, s2);
+        slot[1] = __float_as_uint(next.bc1);
+        slot[2] = __float_as_uint(next.bc2_sqrt);
+        slot[4] = (unsigned)__double2loint(A.beta1);
+        slot[5] = (unsigned)__double2hiint(A.beta1);
+        slot[6] = (unsigned)__double2loint(A.beta2);
+        slot[7] = (unsigned)__double2hiint(A.beta2);
+        slot[0] = __float_as_uint(s2);
+      }
     }
-    return false;
-  };
-  bool started_last = false;
-  if (count == 2) {
-    // every wave's step read complete (lgkmcnt(0) only: the first pass's loads stay in flight),
-    // then the barrier
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    if (threadIdx.x == 0) started_last = last_block();
+    return;
   }
   // bias corrections: the cached ones of this step if the slot matches, else computed here
   // (adam_math.hpp: torch's fused Adam arithmetic either way)
   AdamCoef coef;
   {
-    const unsigned* slot = coef_slot(counters, t, s1);
-    const bool hit = __uint_as_float(slot[0]) == s1 &&
-                     __hiloint2double(slot[5], slot[4]) == A.beta1 &&
-                     __hiloint2double(slot[7], slot[6]) == A.beta2;
+    const bool odd = ((int)s1 & 1) != 0;
+    const uint32_t k0 = odd ? o0 : e0, k1 = odd ? o1 : e1, k2 = odd ? o2 : e2;
+    const uint32_t k4 = odd ? o4 : e4, k5 = odd ? o5 : e5, k6 = odd ? o6 : e6, k7 = odd ? o7 : e7;
+    const bool hit = __uint_as_float(k0) == s1 && __hiloint2double(k5, k4) == A.beta1 &&
+                     __hiloint2double(k7, k6) == A.beta2;
     if (hit) {
-      coef.bc1 = __uint_as_float(slot[1]);
-      coef.bc2_sqrt = __uint_as_float(slot[2]);
+      coef.bc1 = __uint_as_float(k1);
+      coef.bc2_sqrt = __uint_as_float(k2);
       coef.step_size = (float)(A.lr / (double)coef.bc1);
     } else {
       coef = adam_coef(A, s1);
-    }
-  }
-  // the tensor's first block: the next step's corrections, into the other parity's slot (no block
-  // of this launch reads it)
-  if (b == 0 && threadIdx.x < 64) {
-    const float s2 = s1 + 1.0f;
-    const AdamCoef next = adam_coef(A, s2);
-    if (threadIdx.x == 0) {
-      unsigned* slot = coef_slot(counters, t, s2);
-      slot[1] = __float_as_uint(next.bc1);
-      slot[2] = __float_as_uint(next.bc2_sqrt);
-      slot[4] = (unsigned)__double2loint(A.beta1);
-      slot[5] = (unsigned)__double2hiint(A.beta1);
-      slot[6] = (unsigned)__double2loint(A.beta2);
-      slot[7] = (unsigned)__double2hiint(A.beta2);
-      slot[0] = __float_as_uint(s2);
     }
   }
   auto update = [&](float& param, float grad, float& m, float& v) {
@@ -201,9 +270,9 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
         const int64_t e = i + u * kStride;
         if (e + 3 < i1) {
           const int64_t q = e >> 2;
-          st(param + q, p[u], NT);
-          st(exp_avg + q, m[u], NT);
-          st(exp_avg_sq + q, v[u], NT);
+          param[q] = p[u];
+          exp_avg[q] = m[u];
+          exp_avg_sq[q] = v[u];
         }
       }
       load_pass(i + U * kStride);
@@ -219,13 +288,6 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam_step(const mi_adam A, con
     T.param[j] = pe;
     T.exp_avg[j] = me;
     T.exp_avg_sq[j] = ve;
-  }
-
-  if (count == 1) {
-    __syncthreads();   // every thread of the block has read the step
-    if (threadIdx.x == 0 && last_block()) *T.step = s1;
-  } else if (count == 2 && threadIdx.x == 0 && started_last) {
-    *T.step = s1;
   }
 }
 
@@ -252,11 +314,11 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
       return MI_EINVAL;
     total += T.numel;
   }
-  // About 1024 workgroups over all tensors (C5's 2 x 1e6 parameters: 1024 of 2048 elements; with
-  // per-block pows 500 of 4096 had run faster, 12.5 us against 17, profiles/r03_adam_sweep.log --
-  // tools/stream_probe.hip without them: 7.0 us at 512, 6.6 at 1024, 6.7 at 2048); at least
+  // About 512 workgroups over all tensors: measured on C5's 2 x 1e6 parameters (tools/adam_probe.py,
+  // graph replays; profiles/r05_adam_ab.json): 500 workgroups of 4096 elements 12.4 us, 1000 of
+  // 2048 17.6 us (15.9 with every block computing its own bias corrections); at least
   // 4 * kAdamThreads elements per workgroup and at most kAdamGroup^2 workgroups per tensor.
-  constexpr int64_t target_blocks = 1024;
+  constexpr int64_t target_blocks = 512;
   constexpr int64_t min_chunk = 4 * mi::kAdamThreads;
   const int64_t even = (total + target_blocks - 1) / target_blocks;
   int blocks = 0;
@@ -271,12 +333,15 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream) {
     blocks += (int)((T.numel + chunk - 1) / chunk);
   }
   for (int t = adam->num; t <= MI_ADAM_MAX_TENSORS; ++t) P.first[t] = blocks;
-  // the step counts are advanced by the first workgroup (12.5 us vs 14.2 us counting at the end,
-  // C5; r03 sweeps also kept plain over non-temporal accesses and two quads per lane per pass)
-  constexpr int count = 2;
-  const dim3 grid((unsigned)blocks), block(mi::kAdamThreads);
+  const dim3 grid((unsigned)blocks), block(mi::kAdamBlock);
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL((mi::k_adam_step<false, 2>), grid, block, 0, s, *adam, P, counters, count);
+  if (adam->num <= 2)
+    hipLaunchKernelGGL((mi::k_adam_step<2, 2>), grid, block, 0, s, *adam, P, counters);
+  else if (adam->num <= 4)
+    hipLaunchKernelGGL((mi::k_adam_step<2, 4>), grid, block, 0, s, *adam, P, counters);
+  else
+    hipLaunchKernelGGL((mi::k_adam_step<2, MI_ADAM_MAX_TENSORS>), grid, block, 0, s, *adam, P,
+                       counters);
   return to_code(hipGetLastError());
 }
 

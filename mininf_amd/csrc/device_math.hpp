@@ -178,6 +178,27 @@ MI_DEV float wave_sum_strided(float v, int width) {
   return v;
 }
 
+// Kernel-argument prefetch: one vector load touches every 64-byte line of the first BYTES of the
+// argument segment (lane l reads a dword of line l), so the segment is in the L2 after one memory
+// round trip. The descriptor-driven kernels read their arguments through the scalar cache in
+// dependent chains (a job index from one field selects the next fields); each miss there cost a
+// memory round trip at the start of every workgroup (k_elbo_forward's reducing blocks: 2.4-3 us
+// from entry to their first data load, tools/elbo_timing.py), an L2 hit a fraction of one. (Scalar
+// loads of every line would need one wait per 15: the counter's limit.)
+template <int BYTES>
+MI_DEV void kernarg_prefetch() {
+  static_assert(BYTES > 0 && BYTES <= 64 * 64, "argument segment");
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t base = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  const int lane = (int)(threadIdx.x & 63);
+  if (threadIdx.x < 64 && lane * 64 < BYTES) {
+    typedef const __attribute__((address_space(1))) uint32_t gword;
+    const uint32_t x = *(gword*)(base + (uint64_t)lane * 64);
+    asm volatile("" : : "v"(x));
+  }
+#endif
+}
+
 // Kernel span stamps (bench.py's timing of a replayed kernel): every workgroup of a launch folds
 // its start and end times on the device's constant-rate clock (s_memrealtime, 100 MHz) into
 // stamps[0] (minimum) and stamps[1] (maximum), so the launch's span is stamps[1] - stamps[0] --

@@ -19,7 +19,6 @@
 #include "entropy.hpp"
 
 #include <algorithm>
-#include <type_traits>
 #include <cstdlib>
 
 namespace mi {
@@ -509,6 +508,22 @@ MI_DEV void absorbed_block(const mi_elbo& E, const AbsorbPlan& P, int bid, float
   if (counter != nullptr && threadIdx.x == 0) *counter = 0u;
 }
 
+// Phase timestamps (MI_ELBO_TIMING builds only, tools/elbo_timing.py): wall clock at up to 16
+// points of every block of k_elbo_forward (thread 0), into a buffer the timing build allocates.
+#ifndef MI_ELBO_TIMING
+#define MI_ELBO_TIMING 0
+#endif
+#if MI_ELBO_TIMING
+__device__ unsigned long long* mi_elbo_tbuf;
+__shared__ unsigned long long mi_ets[16];
+#define MI_ELBO_STAMP(i) do { if (threadIdx.x == 0) mi_ets[i] = wall_clock64(); } while (0)
+#define MI_ELBO_FLUSH() do { if (threadIdx.x == 0) { unsigned long long* o = mi_elbo_tbuf + (int64_t)blockIdx.x * 16; \
+    for (int q = 0; q < 16; ++q) o[q] = mi_ets[q]; } } while (0)
+#else
+#define MI_ELBO_STAMP(i) do { } while (0)
+#define MI_ELBO_FLUSH() do { } while (0)
+#endif
+
 // ---- deferred site finalize reductions (mi_elbo.reduce) ---------------------------------------
 // Block (job a, particle block kb, value v) sums part[v][seg][k] over the job's segments for 64
 // particles: 4 segment groups of 64 lanes, up to sixteen loads in flight per lane, partial sums in fp64
@@ -663,37 +678,30 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
       r1f = q[kc];
       r1e = q[K + kc];
     }
+    MI_ELBO_STAMP(8);   // (descriptor decoded: the segment loads go out next)
     double acc = 0.0;
     int64_t g = gl;
-    // NL loads in flight per lane, the last round padded with clamped loads whose values are
-    // dropped (a remainder loop waited one round trip per segment). Each round is one memory
-    // latency: 32 per lane when the list is longer than 16 per lane (C2's ~250 segments over 8
-    // groups, C4's 513 over 16: one round instead of two), else 16. The sum runs in segment order
-    // either way.
-    auto rounds = [&](auto nl) {
-      constexpr int NL = decltype(nl)::value;
-      for (; g + (NL - 1) * kRedG < J.nseg; g += NL * kRedG) {
-        float x[NL];
+    // sixteen loads in flight per lane (a C2-sized list, ~250 segments over 8 groups, is two
+    // rounds of memory latency instead of four), the last round padded with clamped loads whose
+    // values are dropped: a remainder loop waited one round trip per segment
+    for (; g + 15 * kRedG < J.nseg; g += 16 * kRedG) {
+      float x[16];
 #pragma unroll
-        for (int j = 0; j < NL; ++j) x[j] = p[(g + j * kRedG) * stride];
+      for (int j = 0; j < 16; ++j) x[j] = p[(g + j * kRedG) * stride];
 #pragma unroll
-        for (int j = 0; j < NL; ++j) acc += (double)x[j];
+      for (int j = 0; j < 16; ++j) acc += (double)x[j];
+    }
+    if (g < J.nseg) {
+      float x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int64_t gj = g + j * kRedG;
+        x[j] = keep_if(p[(gj < J.nseg ? gj : J.nseg - 1) * stride], gj < J.nseg);
       }
-      if (g < J.nseg) {
-        float x[NL];
 #pragma unroll
-        for (int j = 0; j < NL; ++j) {
-          const int64_t gj = g + j * kRedG;
-          x[j] = keep_if(p[(gj < J.nseg ? gj : J.nseg - 1) * stride], gj < J.nseg);
-        }
-#pragma unroll
-        for (int j = 0; j < NL; ++j) acc += (double)x[j];
-      }
-    };
-    if (J.nseg > 16 * kRedG)
-      rounds(std::integral_constant<int, 32>{});
-    else
-      rounds(std::integral_constant<int, 16>{});
+      for (int j = 0; j < 16; ++j) acc += (double)x[j];
+    }
+    MI_ELBO_STAMP(9);   // (the lane's segments summed)
     __syncthreads();
     lds[gl * kRedK + kl] = acc;
     __syncthreads();
@@ -762,20 +770,7 @@ MI_DEV double reduce_block(const mi_elbo& E, const ReducePlan& R, int bid,
   return share;
 }
 
-// Phase timestamps (MI_ELBO_TIMING builds only, tools/elbo_timing.py): wall clock at 6 points of
-// every block of k_elbo_forward (thread 0), into a buffer the timing build allocates.
-#ifndef MI_ELBO_TIMING
-#define MI_ELBO_TIMING 0
-#endif
-#if MI_ELBO_TIMING
-__device__ unsigned long long* mi_elbo_tbuf;
-#define MI_ELBO_STAMP(i) do { if (threadIdx.x == 0) ets_[i] = wall_clock64(); } while (0)
-#define MI_ELBO_FLUSH() do { if (threadIdx.x == 0) { unsigned long long* o = mi_elbo_tbuf + (int64_t)blockIdx.x * 8; \
-    for (int q = 0; q < 8; ++q) o[q] = ets_[q]; } } while (0)
-#else
-#define MI_ELBO_STAMP(i) do { } while (0)
-#define MI_ELBO_FLUSH() do { } while (0)
-#endif
+
 
 // ---- what the last block needs that is known at the launch's start ---------------------------
 // Block 0 computes, while its own reduction's loads are in flight, the values the last block's
@@ -835,9 +830,10 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   __shared__ double red[kElboThreads][2];
   __shared__ bool last;
 #if MI_ELBO_TIMING
-  unsigned long long ets_[8] = {};
+  if (threadIdx.x < 16) mi_ets[threadIdx.x] = 0;
 #endif
   MI_ELBO_STAMP(0);
+  kernarg_prefetch<(int)(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan))>();
   const int nred = R.first[R.num];
   const int nloss = P.lead_blocks;
   const int nshare = nred + nloss;   // blocks that write a loss share
@@ -1057,38 +1053,15 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                         __HIP_MEMORY_SCOPE_AGENT);
   double t = 0.0;
   double acc[kMaxTails][2] = {};
-  // kSU shares per lane per round, all loads issued before the first add (a loop of one share per
-  // iteration waited a memory round trip per iteration: C2's 257 shares are two); the adds run in
-  // share order, as before
-  constexpr int kSU = 4;
-  auto ld = [](const double* a) {
-    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  for (int b0 = threadIdx.x; b0 < nshare; b0 += kSU * kElboThreads) {
-    double x[kSU], y[kMaxTails][2][kSU];
-#pragma unroll
-    for (int u = 0; u < kSU; ++u) {
-      const int b = b0 + u * kElboThreads;
-      const bool on = b < nshare;
-      const int bc = on ? b : b0;
-      x[u] = keep_if_d(ld(&work[bc]), on);
+  for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
+    t += __hip_atomic_load(&work[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ABSORB) {
 #pragma unroll
       for (int q = 0; q < kMaxTails; ++q) {
-        y[q][0][u] = y[q][1][u] = 0.0;
-        if (!ABSORB && q < R.tails) {
-          const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + bc) * 2];
-          y[q][0][u] = keep_if_d(ld(w2), on);
-          y[q][1][u] = keep_if_d(ld(w2 + 1), on);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kSU; ++u) {
-      t += x[u];
-#pragma unroll
-      for (int q = 0; q < kMaxTails; ++q) {
-        acc[q][0] += y[q][0][u];
-        acc[q][1] += y[q][1][u];
+        if (q >= R.tails) break;
+        const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
+        acc[q][0] += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[q][1] += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -1116,40 +1089,19 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     const int64_t i = threadIdx.x;
     nt_p0 = F.param[0][i * F.stride[0]];
     nt_p1 = F.param[1][i * F.stride[1]];
-    if (!nt_wide)   // (its particle blocks' partials, kSU loads in flight, added in order)
-      for (int kb0 = 0; kb0 < R.nt_nkb; kb0 += kSU) {
-        double x0[kSU], x1[kSU];
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-          const bool on = kb0 + u < R.nt_nkb;
-          const double* w2 = &work[R.nt_part + (i * R.nt_nkb + (on ? kb0 + u : kb0)) * 2];
-          x0[u] = keep_if_d(ld(w2), on);
-          x1[u] = keep_if_d(ld(w2 + 1), on);
-        }
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-          nt_s0 += x0[u];
-          nt_s1 += x1[u];
-        }
+    if (!nt_wide)
+      for (int kb = 0; kb < R.nt_nkb; ++kb) {
+        const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
+        nt_s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nt_s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
   }
   if (nt_wide) {   // (element 0 of factor 0; the whole block, uniform branch)
     double q0 = 0.0, q1 = 0.0;
-    for (int kb0 = threadIdx.x; kb0 < R.nt_nkb; kb0 += kSU * kElboThreads) {
-      double x0[kSU], x1[kSU];
-#pragma unroll
-      for (int u = 0; u < kSU; ++u) {
-        const int kb = kb0 + u * kElboThreads;
-        const bool on = kb < R.nt_nkb;
-        const double* w2 = &work[R.nt_part + (int64_t)(on ? kb : kb0) * 2];
-        x0[u] = keep_if_d(ld(w2), on);
-        x1[u] = keep_if_d(ld(w2 + 1), on);
-      }
-#pragma unroll
-      for (int u = 0; u < kSU; ++u) {
-        q0 += x0[u];
-        q1 += x1[u];
-      }
+    for (int kb = threadIdx.x; kb < R.nt_nkb; kb += kElboThreads) {
+      const double* w2 = &work[R.nt_part + (int64_t)kb * 2];
+      q0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     q0 = wave_sum(q0);
     q1 = wave_sum(q1);
@@ -1680,7 +1632,7 @@ static unsigned long long* mi_elbo_timing_last = nullptr;
 extern "C" {
 
 #if MI_ELBO_TIMING
-// Copy the stamps of the last k_elbo_forward (8 per block) to the host (timing builds only).
+// Copy the stamps of the last k_elbo_forward (16 per block) to the host (timing builds only).
 int mi_elbo_timing_read(void* host, size_t bytes) {
   if (mi_elbo_timing_last == nullptr) return MI_EINVAL;
   return hipMemcpy(host, mi_elbo_timing_last, bytes < (8u << 20) ? bytes : (8u << 20),

@@ -1,9 +1,8 @@
 """
 Time mininf_amd.optim.Adam alone on C5's guide parameters (z loc and scale, 1e6 floats each):
-HIP events around graph replays of 50 steps each. Launch-shape knobs are read once per process
-(MININF_AMD_ADAM_CHUNK, MININF_AMD_ADAM_NT, MININF_AMD_ADAM_UNROLL), so run one process per setting:
+HIP events around graph replays of 50 steps each (MININF_AMD_LIB selects a variant build):
 
-    MININF_AMD_ADAM_CHUNK=4096 python tools/adam_probe.py
+    python tools/adam_probe.py [elements per tensor]
 """
 import json
 import os
@@ -51,11 +50,7 @@ def main():
     torch.cuda.synchronize()
     us = start.elapsed_time(stop) * 1e3 / steps
     moved = 28.0 * 2 * n   # read param, grad, m, v; write param, m, v (fp32)
-    print(json.dumps({"chunk": os.environ.get("MININF_AMD_ADAM_CHUNK", "default"),
-                      "blocks": os.environ.get("MININF_AMD_ADAM_BLOCKS", "256"),
-                      "count": os.environ.get("MININF_AMD_ADAM_COUNT", "1"),
-                      "nt": os.environ.get("MININF_AMD_ADAM_NT", "0"),
-                      "unroll": os.environ.get("MININF_AMD_ADAM_UNROLL", "2"), "n": n,
+    print(json.dumps({"lib": os.environ.get("MININF_AMD_LIB", "default"), "n": n,
                       "us_per_step": round(us, 2), "TB_s": round(moved / us / 1e6, 3)}),
           flush=True)
 

@@ -5,10 +5,11 @@ build of the library with -DMI_ELBO_TIMING=1, over eager steps of a bench config
     python tools/elbo_timing.py build          (on the CPU: tools/_timing/libmininf_amd.so)
     python tools/elbo_timing.py run [c2|c4|c5] (on the GPU)
 
-Stamps per block (thread 0): 0 entry, 1 the block's own work done (reduction or lead terms),
+Stamps per block (thread 0; 16 slots): 0 entry, 1 the block's own work done (reduction or lead terms),
 2 tail partials and the block sum, 3 the completion count (the last block known); the last block
 only: 4 final loads and the loss sum, 6 the Beta tails (with their Adam updates), 7 the Normal
-tail (with its Adam updates), 5 end (flag mirror, generator and optimizer step counts).
+tail (with its Adam updates), 5 end (flag mirror, generator and optimizer step counts); reducing
+blocks also 8 descriptor decoded (segment loads next) and 9 their segments summed.
 """
 import ctypes
 import os
@@ -52,7 +53,7 @@ def run(config="c2"):
         buf = np.zeros(1 << 20, dtype=np.uint64)
         lib.mi_elbo_timing_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
         if step >= 4:
-            rows = buf.reshape(-1, 8)
+            rows = buf.reshape(-1, 16)
             rows = rows[rows[:, 0] > 0].astype(np.float64) / 100.0   # microseconds
             rows_all.append(rows)
     torch.cuda.synchronize()
@@ -66,6 +67,12 @@ def run(config="c2"):
               f"loads+sum {last[0, 4] - last[0, 3]:.2f}, tails {last[0, 6] - last[0, 4]:.2f}, "
               f"normal tail {last[0, 7] - last[0, 6]:.2f}, mirror+step {last[0, 5] - last[0, 7]:.2f}, "
               f"end {last[0, 5] - base:.2f} us", flush=True)
+        red = rows[rows[:, 8] > 0]   # reducing blocks: descriptor decoded (8), segments summed (9)
+        if red.shape[0]:
+            print(f"  reducing blocks {red.shape[0]}: entry -> loads issued {np.mean(red[:, 8] - red[:, 0]):.2f} "
+                  f"(max {np.max(red[:, 8] - red[:, 0]):.2f}), loads -> summed {np.mean(red[:, 9] - red[:, 8]):.2f} "
+                  f"(max {np.max(red[:, 9] - red[:, 8]):.2f}), summed -> work done {np.mean(red[:, 1] - red[:, 9]):.2f} us",
+                  flush=True)
 
 
 if __name__ == "__main__":
