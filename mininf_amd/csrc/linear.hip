@@ -290,6 +290,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   unsigned long long ts_[8] = {};
 #endif
   MI_LIN_STAMP(0);
+  // one-stage launches (C4's minibatch) run each wave through a short body once: the argument
+  // chain at their start is on the critical path (C4 37.5 -> 36.5 us per step); the multi-stage
+  // launches (C3) lose more to the prefetch's wait in wave 0 than they gain (300.5 -> 308 us)
+  if (ONESTAGE) kernarg_prefetch<(int)sizeof(mi_linear)>();
   const unsigned long long span_t0 = span_begin(L.stamps);
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;

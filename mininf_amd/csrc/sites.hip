@@ -593,6 +593,7 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
                                                                    int mode,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
+  kernarg_prefetch<(int)sizeof(mi_group)>();
   // mode bit 0: rank-one slot layout; bit 1: progress-balanced wave priority (below)
   const int rank1 = mode & 1;
   const bool balance = (mode & 2) != 0;
