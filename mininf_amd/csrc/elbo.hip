@@ -540,6 +540,7 @@ constexpr int kRedKWide = 64;
 #define MI_ELBO_RELEASE_FENCE 0
 #endif
 constexpr int kGroupBlocks = 32;
+constexpr int kSingleCount = 160;
 constexpr int kGroupCounters = 64;        // groups: at most kGroupCounters * kGroupBlocks blocks
 constexpr int kGroupCounterWord = 16;     // first group counter (uint32 word)
 constexpr int kGroupCounterStride = 16;   // words between group counters (64 bytes)
@@ -653,6 +654,9 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
     if (j >= 0 && i >= 0 && i < E.factors[0].n) nt_slot = i;
   }
   const int nt_mask = nt_fin && R.nt_single ? pick(R.nt_mask, a) : 0;
+  // the Normal tail's generator step, read before the segment loads (its use follows them: read
+  // there, it was one more memory round trip after them)
+  const uint64_t nt_step = nt_slot >= 0 ? forward_step0(E) : 0ull;
   const int kl = threadIdx.x % kRedK, gl = threadIdx.x / kRedK;
   const int64_t K = J.K;
   const int64_t k = kb * kRedK + kl;
@@ -720,7 +724,7 @@ MI_DEV double reduce_job(const mi_elbo& E, float g0, const mi_reduce& J, int loc
         if (nt_slot >= 0 && (!R.nt_single || ((nt_mask >> j) & 1))) {
           // d z[k, i] for the Normal tail, against its regenerated eps
           const mi_factor& F = E.factors[0];
-          const uint64_t step = forward_step0(E);
+          const uint64_t step = nt_step;
           const int64_t i = nt_slot;
           float q[4];
           guide_normals(F.seed, step, F.stream_id, (uint64_t)((F.element_offset + i) >> 2),
@@ -999,7 +1003,9 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     if (MI_ELBO_RELEASE_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_s_waitcnt(0);
     const int group = (int)blockIdx.x / kGroupBlocks;
-    const int ngroups = (nshare + kGroupBlocks - 1) / kGroupBlocks;
+    // (one level up to kSingleCount blocks: their arrivals at one address cost less than the
+    // second level's round trip)
+    const int ngroups = nshare <= kSingleCount ? 1 : (nshare + kGroupBlocks - 1) / kGroupBlocks;
     const unsigned in_group = (unsigned)min(kGroupBlocks, nshare - group * kGroupBlocks);
     unsigned* gc = counters + kGroupCounterWord + group * kGroupCounterStride;
     bool done = true;
@@ -1020,6 +1026,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   // the tails' partials and concentrations, the validation words, the generator step) is issued
   // before the first sum: one memory round trip instead of one per stage.
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  MI_ELBO_STAMP(10);
   // the optimised tensors' elements this thread updates (element threadIdx.x of every slot) and
   // their moments: loaded now, used when the gradient is written below. Lane q computes slot q's
   // bias corrections (fp64 pow: a long dependent chain) meanwhile, into LDS.
@@ -1053,15 +1060,41 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
                                         __HIP_MEMORY_SCOPE_AGENT);
   double t = 0.0;
   double acc[kMaxTails][2] = {};
-  for (int b = threadIdx.x; b < nshare; b += kElboThreads) {
-    t += __hip_atomic_load(&work[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!ABSORB) {
+  auto ld = [](const double* w) {
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // kSU shares per lane per round, each load under its own (uniform per round) guard and all of
+  // them issued before the first add: a loop of one share per iteration waited a memory round trip
+  // per iteration (C2's 257 shares are two); the adds run in share order, as before
+  constexpr int kSU = 2;
+  for (int b0 = threadIdx.x; b0 < nshare; b0 += kSU * kElboThreads) {
+    double x[kSU], y[kMaxTails][2][kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int b = b0 + u * kElboThreads;
+      x[u] = 0.0;
+#pragma unroll
+      for (int q = 0; q < kMaxTails; ++q) y[q][0][u] = y[q][1][u] = 0.0;
+      if (b < nshare) {
+        x[u] = ld(&work[b]);
+        if (!ABSORB) {
+#pragma unroll
+          for (int q = 0; q < kMaxTails; ++q)
+            if (q < R.tails) {
+              const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
+              y[q][0][u] = ld(w2);
+              y[q][1][u] = ld(w2 + 1);
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      t += x[u];
 #pragma unroll
       for (int q = 0; q < kMaxTails; ++q) {
-        if (q >= R.tails) break;
-        const double* w2 = &work[R.tail_part + ((int64_t)q * nshare + b) * 2];
-        acc[q][0] += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        acc[q][1] += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        acc[q][0] += y[q][0][u];
+        acc[q][1] += y[q][1][u];
       }
     }
   }
@@ -1089,11 +1122,23 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     const int64_t i = threadIdx.x;
     nt_p0 = F.param[0][i * F.stride[0]];
     nt_p1 = F.param[1][i * F.stride[1]];
-    if (!nt_wide)
-      for (int kb = 0; kb < R.nt_nkb; ++kb) {
-        const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb) * 2];
-        nt_s0 += __hip_atomic_load(w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        nt_s1 += __hip_atomic_load(w2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!nt_wide)   // (the particle blocks' partials: four per round, guarded, added in order)
+      for (int kb0 = 0; kb0 < R.nt_nkb; kb0 += 4) {
+        double x0[4], x1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          x0[u] = x1[u] = 0.0;
+          if (kb0 + u < R.nt_nkb) {
+            const double* w2 = &work[R.nt_part + (i * R.nt_nkb + kb0 + u) * 2];
+            x0[u] = ld(w2);
+            x1[u] = ld(w2 + 1);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          nt_s0 += x0[u];
+          nt_s1 += x1[u];
+        }
       }
   }
   if (nt_wide) {   // (element 0 of factor 0; the whole block, uniform branch)

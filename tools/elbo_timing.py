@@ -67,6 +67,9 @@ def run(config="c2"):
               f"loads+sum {last[0, 4] - last[0, 3]:.2f}, tails {last[0, 6] - last[0, 4]:.2f}, "
               f"normal tail {last[0, 7] - last[0, 6]:.2f}, mirror+step {last[0, 5] - last[0, 7]:.2f}, "
               f"end {last[0, 5] - base:.2f} us", flush=True)
+        if last[0, 10] > 0:
+            print(f"  last block: count -> acquire fence done {last[0, 10] - last[0, 3]:.2f}, "
+                  f"fence -> loads summed {last[0, 4] - last[0, 10]:.2f} us", flush=True)
         red = rows[rows[:, 8] > 0]   # reducing blocks: descriptor decoded (8), segments summed (9)
         if red.shape[0]:
             print(f"  reducing blocks {red.shape[0]}: entry -> loads issued {np.mean(red[:, 8] - red[:, 0]):.2f} "
