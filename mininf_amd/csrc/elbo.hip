@@ -888,7 +888,16 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
           const int64_t nq = F.n >> 2;
           const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
           int64_t q = first;
-          // four quads' loads in flight per round (a lead block covers ~16 elements per lane)
+          // eight quads' loads in flight per round, then four (a lead block covers ~32 elements
+          // per lane: one memory round trip, not two); quads summed in order either way
+          for (; q + 7 * stride < nq; q += 8 * stride) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sq[q + u * stride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
+          }
           for (; q + 3 * stride < nq; q += 4 * stride) {
             float4 v[4];
 #pragma unroll
