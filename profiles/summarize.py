@@ -83,7 +83,12 @@ def counters(raw: str, kind: str, cfg: str):
 
 
 def per_launch(values):
-    return sum(values) / len(values) if values else None
+    """Mean over the replayed launches: the second half of a run's launches (the first are the
+    eager warm-up steps and the capture's)."""
+    if not values:
+        return None
+    tail = values[len(values) // 2:] if len(values) >= 4 else values
+    return sum(tail) / len(tail)
 
 
 def c5_calibration(raw: str):
@@ -119,8 +124,9 @@ def replay_durations(raw: str, round_tag: str) -> None:
         src = os.path.join(raw, f"stats_{cfg}", "run_kernel_trace.csv")
         if not os.path.exists(src):
             continue
+        # (C2: not the reducible-floor variant of the site kernel, SUFF = true)
         rows = [r for r in csv.DictReader(open(src)) if re.search(pattern, r["Kernel_Name"]) and
-                "true>" not in short(r["Kernel_Name"])[-8:]]
+                not (cfg == "c2" and "true>" in short(r["Kernel_Name"])[-8:])]
         if not rows:
             continue
         grid = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
@@ -211,7 +217,7 @@ def valu(raw: str, round_tag: str) -> None:
         if "SQ_INSTS_VALU" not in per or "GRBM_GUI_ACTIVE" not in per:
             continue
         cycles = per["GRBM_GUI_ACTIVE"] / XCDS
-        us = per.get("vtype_us", per.get("valu_us"))
+        us = per.get("vtype_us") or per.get("valu_us") or per.get("wait_us")
         per["clock_ghz"] = cycles / (us * 1e3)
         if "SQ_INSTS_VALU_TRANS_F32" in per:
             trans = per["SQ_INSTS_VALU_TRANS_F32"]
