@@ -453,12 +453,17 @@ def check_launch(args, world, rank):
 _COMMUNICATOR = None
 
 
-def communicator(group, device):
-    """The run's one RCCL communicator (mininf_amd.rccl), shared by every config: graphs of an
-    earlier config may still hold its captured collective."""
+def communicator(group, device, kind="rccl"):
+    """The run's one communicator, shared by every config (graphs of an earlier config may still
+    hold its captured collective): RCCL called directly (mininf_amd.rccl), or with
+    ``--allreduce peer`` the one-shot peer-write all-reduce (mininf_amd.peer, opt-in)."""
     global _COMMUNICATOR
     if _COMMUNICATOR is None:
-        _COMMUNICATOR = rccl.Communicator(group, device)
+        if kind == "peer":
+            from mininf_amd.peer import PeerCommunicator
+            _COMMUNICATOR = PeerCommunicator(group, device)
+        else:
+            _COMMUNICATOR = rccl.Communicator(group, device)
     return _COMMUNICATOR
 
 
@@ -487,10 +492,11 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
     # (several steps per replay, like N = 1); gloo cannot be captured, so there the step is split
     # around the host-issued all-reduce (two graphs).
     sharded = group is not None
-    collective_in_graph = sharded and args.dist_backend == "nccl"
+    collective_in_graph = sharded and (args.dist_backend == "nccl" or args.allreduce == "peer")
     # over RCCL the all-reduce runs on a communicator of our own (mininf_amd.rccl: RCCL called
-    # directly, no process-group watchdog polling events of the captured collective)
-    comm = communicator(group, device) if collective_in_graph else None
+    # directly, no process-group watchdog polling events of the captured collective); the peer
+    # all-reduce is one kernel of ours, captured the same way whatever the process group's backend
+    comm = communicator(group, device, args.allreduce) if collective_in_graph else None
     # data sharding reduces only the replicated (shared) parameters' gradients; every rank
     # updates its own slice of the rest
     bucket = GradientBucket(w.get("reduce_params") or module.parameters(), group, with_loss=True,
@@ -655,9 +661,12 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         elapsed, loss = timed(graph_step, steps // repeat)
         loss = loss.detach().clone()   # (see above; the graph's own output is static as well)
         captured.check()
+        if comm is not None and hasattr(comm, "check"):
+            comm.check()   # (the peer all-reduce's timeout word)
         mode = "hipGraph replay" + (f" ({repeat} steps per replay)" if repeat > 1 else "")
         if sharded:
-            mode += (" with the RCCL all-reduce captured in the graph" if collective_in_graph
+            what = "peer-write" if args.allreduce == "peer" else "RCCL"
+            mode += (f" with the {what} all-reduce captured in the graph" if collective_in_graph
                      else f" split around the host-issued {args.dist_backend} all-reduce")
         floor_ms = None
         if config == "c2" and not sharded:
@@ -739,7 +748,8 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                    "evals_per_step_per_gpu": w["evals"],
                    "parallelism": (f"particle-sharded x{world}" if shard is None else
                                    f"data-sharded x{shard.world} (element slices)") + (
-                       (" + RCCL grad all-reduce" if args.dist_backend == "nccl" else
+                       (" + peer-write grad all-reduce" if args.allreduce == "peer" else
+                        " + RCCL grad all-reduce" if args.dist_backend == "nccl" else
                         f" + {args.dist_backend} grad all-reduce") if sharded else ""),
                    "validate": not args.no_validate, "final_loss": float(loss.detach()),
                    "step_mode": mode, "eager_ms_per_step": eager_ms,
@@ -783,6 +793,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo lets "
                          "several ranks share one GPU to exercise the sharded path)")
+    ap.add_argument("--allreduce", choices=("rccl", "peer"), default="rccl",
+                    help="N > 1: the gradient bucket's all-reduce -- RCCL (nccl backend) or the "
+                         "one-shot peer-write kernel (mininf_amd.peer, any backend; opt-in, "
+                         "unmeasured on multi-GPU hardware)")
     ap.add_argument("--optimizer", choices=("mi", "torch"), default="mi",
                     help="Adam implementation: mininf_amd.optim.Adam (one HIP launch, default) or "
                          "torch.optim.Adam(fused=True, capturable=True)")

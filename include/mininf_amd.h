@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 16
+#define MI_ABI_VERSION 17
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -609,6 +609,34 @@ typedef struct mi_adam {
   mi_adam_tensor tensors[MI_ADAM_MAX_TENSORS];
 } mi_adam;
 int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream);
+
+/* ---- one-shot peer-write all-reduce (replaces the sharded step's small-bucket
+ * dist.all_reduce / ncclAllReduce, distributed.GradientBucket) -------------------------------------
+ * Each rank allocates one region (mi_peer_region_bytes for the largest bucket, mi_peer_alloc:
+ * fine-grained device memory, zeroed, and its IPC handle, MI_PEER_HANDLE_BYTES), exchanges the
+ * handles over its process group and maps the peers' regions (mi_peer_open). mi_peer_allreduce
+ * then sums a float bucket over the ranks in ONE kernel on the caller's stream (capturable): the
+ * bucket is written into a slot of every peer's region with system-scope stores, a flag carrying
+ * the call number follows, the caller waits for every peer's flag in its own region and adds the
+ * slots in rank order (two ranks: the same sum as any SUM all-reduce). A peer that never arrives
+ * ends the wait after about a second and sets bit 0 of *error (device memory, never cleared by the
+ * library). Every rank must call it the same number of times, with buckets of the same length. */
+#define MI_PEER_MAX_RANKS 8
+#define MI_PEER_MAX_FLOATS 4096
+#define MI_PEER_HANDLE_BYTES 64
+typedef struct mi_peer {
+  int32_t rank;
+  int32_t world;
+  int64_t max_floats;                    /* the regions' slot length */
+  void* regions[MI_PEER_MAX_RANKS];      /* [rank]: this rank's region; others: the mapped peers' */
+} mi_peer;
+int mi_peer_region_bytes(int64_t max_floats, size_t* bytes);
+int mi_peer_alloc(size_t bytes, void** region, void* handle);
+int mi_peer_open(const void* handle, void** region);
+int mi_peer_close(void* region);
+int mi_peer_free(void* region);
+int mi_peer_allreduce(const mi_peer* peer, const float* in, float* out, int64_t n,
+                      uint32_t* error, void* stream);
 
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 

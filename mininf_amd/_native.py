@@ -40,7 +40,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 16   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 17   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -178,6 +178,17 @@ class AdamTensor(ctypes.Structure):
                 ("step", c_vp), ("numel", c_i64)]
 
 
+PEER_MAX_RANKS = 8
+PEER_MAX_FLOATS = 4096
+PEER_HANDLE_BYTES = 64
+
+
+class Peer(ctypes.Structure):
+    """mi_peer (include/mininf_amd.h)."""
+    _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32), ("max_floats", c_i64),
+                ("regions", c_vp * PEER_MAX_RANKS)]
+
+
 class Adam(ctypes.Structure):
     _fields_ = [("num", ctypes.c_int32), ("maximize", ctypes.c_int32), ("lr", ctypes.c_double),
                 ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
@@ -289,6 +300,12 @@ _SIGNATURES = {
                                          ctypes.c_uint64, c_vp, c_i64, c_vp]),
     "mi_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mi_adam_step": (ctypes.c_int, [ctypes.POINTER(Adam), c_vp, c_vp]),
+    "mi_peer_region_bytes": (ctypes.c_int, [c_i64, ctypes.POINTER(ctypes.c_size_t)]),
+    "mi_peer_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(c_vp), c_vp]),
+    "mi_peer_open": (ctypes.c_int, [c_vp, ctypes.POINTER(c_vp)]),
+    "mi_peer_close": (ctypes.c_int, [c_vp]),
+    "mi_peer_free": (ctypes.c_int, [c_vp]),
+    "mi_peer_allreduce": (ctypes.c_int, [ctypes.POINTER(Peer), c_vp, c_vp, c_i64, c_vp, c_vp]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

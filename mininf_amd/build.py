@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = [os.path.join(CSRC, name)
            for name in ("sites.hip", "guide.hip", "elbo.hip", "linear.hip", "minibatch.hip",
-                        "adam.hip", "mvn.hip", "jit.cpp")]
+                        "adam.hip", "mvn.hip", "peer.hip", "jit.cpp")]
 HEADERS = [os.path.join(CSRC, name) for name in ("common.hpp", "device_math.hpp", "beta_grad.hpp", "jit.hpp",
                                                  "internal.hpp", "entropy.hpp", "adam_math.hpp")] + \
     [os.path.join(INCLUDE, "mininf_amd.h")]
