@@ -60,11 +60,6 @@ MI_DEV T pick_adam(const T (&arr)[N], int a) {
 // of the block's tensor runs on registers. Left to itself the compiler turned the selects into
 // indexed loads of the argument segment -- two more dependent round trips before the block's first
 // data loads (the C5 update: ~3 us of a 12 us launch).
-template <typename V>
-MI_DEV V pin(V v) {
-  asm("" : "+s"(v));
-  return v;
-}
 // (a pointer through its address, handed back in the global address space: global, not flat,
 // accesses)
 template <typename V>

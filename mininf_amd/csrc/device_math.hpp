@@ -178,6 +178,14 @@ MI_DEV float wave_sum_strided(float v, int width) {
   return v;
 }
 
+// A uniform value pinned to a scalar register at this point of the program (an empty asm): its load
+// cannot be sunk to a later use, nor a select over several such values turned back into an indexed
+// load of the argument segment.
+template <typename V>
+MI_DEV V pin(V v) {
+  asm("" : "+s"(v));
+  return v;
+}
 // Kernel-argument prefetch: one vector load touches every 64-byte line of the first BYTES of the
 // argument segment (lane l reads a dword of line l), so the segment is in the L2 after one memory
 // round trip. The descriptor-driven kernels read their arguments through the scalar cache in
