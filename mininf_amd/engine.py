@@ -1987,8 +1987,18 @@ class PendingGrad(torch.Tensor):
                                      torch_function_flush(func, types, args, kwargs))
 
 
+def grad_meta(g: torch.Tensor):
+    """(address, dtype, device, contiguous) of a gradient: a PendingGrad's recorded values (no
+    flush hook), any other tensor's own."""
+    meta = g.__dict__.get("_mi_meta") if type(g) is PendingGrad else None
+    return meta if meta is not None else (g.data_ptr(), g.dtype, g.device, g.is_contiguous())
+
+
 def _current_stream(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    index = getattr(device, "index", None)
+    if index is None:
+        return torch.cuda.current_stream(device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(index)   # (no torch.cuda.Stream object)
 
 
 class _PendingStep:
@@ -2012,8 +2022,12 @@ class _PendingStep:
         return self.stream is not None and _current_stream(self.stream[0]) != self.stream[1]
 
     def hold(self, var: torch.Tensor, grad: torch.Tensor) -> torch.Tensor:
-        """``grad`` as the PendingGrad to assign to ``var.grad``."""
+        """``grad`` as the PendingGrad to assign to ``var.grad``. Its address and layout ride along
+        as plain attributes (``_mi_meta``: address, dtype, device, contiguous), so the package's
+        own checks (the optimizer's plan, the launch descriptors) read them without a torch call
+        -- each torch call on a PendingGrad goes through its flush hook."""
         held = grad.as_subclass(PendingGrad)
+        held._mi_meta = (grad.data_ptr(), grad.dtype, grad.device, grad.is_contiguous())
         self.held.append((var, held))
         return held
 
@@ -2062,7 +2076,8 @@ def attach_optimizer(adam, grads: Sequence[torch.Tensor]) -> bool:
     """
     global _PENDING, LAST_FUSIONS
     step = _PENDING
-    if step is None or adam.num < 1 or not any(g.data_ptr() in step.grad_ptrs for g in grads):
+    if step is None or adam.num < 1 or \
+            not any(grad_meta(g)[0] in step.grad_ptrs for g in grads):
         return False
     if step.other_stream():
         # an optimizer stepping on another stream than the forward's: the launch runs first (the

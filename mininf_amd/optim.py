@@ -170,8 +170,12 @@ class _Plan:
             g = p.grad
             if p is not q or p.data_ptr() != ptr or state.get(p) is not s or \
                     s.get("step") is not step or s.get("exp_avg") is not m or \
-                    s.get("exp_avg_sq") is not v or g.is_sparse or \
-                    g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device:
+                    s.get("exp_avg_sq") is not v:
+                return False
+            # (a held gradient's recorded layout: no torch call through its flush hook)
+            _, dtype, device, contiguous = engine.grad_meta(g)
+            if type(g) is not engine.PendingGrad and g.is_sparse or dtype != torch.float32 or \
+                    not contiguous or device != p.device:
                 return False
         return True
 
@@ -180,7 +184,7 @@ class _Plan:
         for desc, device in self.descs:
             if not fresh:
                 for j in range(desc.num):
-                    desc.tensors[j].grad = active[cursor + j].grad.data_ptr()
+                    desc.tensors[j].grad = engine.grad_meta(active[cursor + j].grad)[0]
             grads = [p.grad for p in active[cursor:cursor + desc.num]]
             cursor += desc.num
             # the step's held finishing launch writes these gradients: the update runs in its
