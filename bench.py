@@ -634,7 +634,11 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
         # idle ~13 us, which a launch-bound step amortises (mininf_amd.graph.StepGraph)
         repeat = 1
         if not sharded or collective_in_graph:
-            repeat = args.graph_repeat or next(r for r in (8, 6, 5, 4, 3, 2, 1) if steps % r == 0)
+            # the largest divisor of --steps up to 24: the driver's 20-step run is one replay
+            # (tools/gpurun_r05/t19.sh: 5 steps per replay 94.7-98.1 us per C2 step, 20 per
+            # replay 94.5-95.9)
+            repeat = args.graph_repeat or next(r for r in range(min(24, steps), 0, -1)
+                                               if steps % r == 0)
             if steps % repeat:
                 raise SystemExit(f"--graph-repeat {repeat} does not divide --steps {steps}")
         arm(f"{config}: graph capture")
@@ -777,8 +781,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--graph-repeat", type=int, default=0,
-                    help="steps captured per graph replay at N = 1 (0: the largest of 8, 6, 5, 4, 3, 2, 1 that "
-                         "divides --steps)")
+                    help="steps captured per graph replay (0: the largest divisor of --steps up to 24)")
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--warm-ms", type=float, default=50.0,
