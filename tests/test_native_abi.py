@@ -59,6 +59,22 @@ def test_invalid_arguments_are_rejected():
     assert lib.mi_normal_rsample(ctypes.byref(buf), 0, ctypes.byref(buf), 0, 1, 1, 0, 0, None, 0,
                                  0, 6, None, ctypes.byref(buf), None) == -1
     assert lib.mi_categorical_workspace_bytes(0, 1, ctypes.byref(size)) == -1
+    # the peer all-reduce: slot lengths and descriptors are checked before anything is launched
+    assert lib.mi_peer_region_bytes(0, ctypes.byref(size)) == -1
+    assert lib.mi_peer_region_bytes(nat.PEER_MAX_FLOATS + 1, ctypes.byref(size)) == -1
+    assert lib.mi_peer_region_bytes(256, ctypes.byref(size)) == 0
+    assert size.value == 2 * nat.PEER_MAX_RANKS * 8 + 2 * nat.PEER_MAX_RANKS * 256 * 4 + 8
+    peer = nat.Peer()
+    peer.world, peer.rank, peer.max_floats = 2, 0, 256
+    word = ctypes.c_uint32(0)
+    assert lib.mi_peer_allreduce(ctypes.byref(peer), ctypes.byref(buf), ctypes.byref(buf), 1,
+                                 ctypes.byref(word), None) == -1   # (no mapped regions)
+    peer.regions[0] = peer.regions[1] = ctypes.addressof(buf)
+    assert lib.mi_peer_allreduce(ctypes.byref(peer), ctypes.byref(buf), ctypes.byref(buf), 257,
+                                 ctypes.byref(word), None) == -1   # longer than the slots
+    peer.rank = 2
+    assert lib.mi_peer_allreduce(ctypes.byref(peer), ctypes.byref(buf), ctypes.byref(buf), 1,
+                                 ctypes.byref(word), None) == -1   # rank outside the world
 
 
 def hierarchical(n):
