@@ -103,6 +103,21 @@ def c5_calibration(raw: str):
     return C5_CAL_BYTES / (1024.0 * kb), kb
 
 
+C4_CAL_BYTES = 65536 * (32 * 4 + 4)
+
+
+def c4_calibration(raw: str):
+    """(scale, raw KB) of the one-stage linear kernel's FETCH_SIZE from C4's own run, or None."""
+    fetch = counters(raw, "fetch", "c4")
+    if not fetch:
+        return None
+    keys = [k for k in fetch if re.search(DOMINANT["c4"], k[0])]
+    if not keys:
+        return None
+    kb = per_launch(fetch[max(keys, key=lambda k: k[1])])
+    return C4_CAL_BYTES / (1024.0 * kb), kb
+
+
 def c3_calibration(raw: str):
     """(scale, raw KB) of the linear kernel's FETCH_SIZE from C3's K = 32 run, or None."""
     fetch = counters(raw, "fetch", "c3cal")
@@ -145,12 +160,20 @@ def pmc(raw: str, round_tag: str) -> None:
     result = {}
     cal3 = c3_calibration(raw)
     if cal3 is not None:
-        FETCH_SCALE["c3"] = FETCH_SCALE["c4"] = cal3[0]
+        FETCH_SCALE["c3"] = cal3[0]
         result["c3_calibration"] = {
             "known_input_bytes": C3_CAL_BYTES, "raw_fetch_size_kb_at_k32": cal3[1],
             "fetch_scale": cal3[0],
-            "note": "C3 at K = 32: one particle tile, X and y read once; the same scale is applied "
-                    "to C4 (the same kernel, its rows gathered through the minibatch index)"}
+            "note": "C3 at K = 32: one particle tile, X and y read once (contiguous rows)"}
+    cal4 = c4_calibration(raw)
+    if cal4 is not None:
+        FETCH_SCALE["c4"] = cal4[0]
+        result["c4_calibration"] = {
+            "known_input_bytes": C4_CAL_BYTES, "raw_fetch_size_kb": cal4[1], "fetch_scale": cal4[0],
+            "note": "C4 as benched (K = 32, one particle group): every gathered row of X and y is "
+                    "read by exactly one workgroup, so the known input is the batch's 65536 rows; "
+                    "the raw count is about that (random 128-byte row gathers are counted in full, "
+                    "unlike C3's streamed rows), hence a scale near 1 -- C3's 1.79 does not apply"}
     cal = c5_calibration(raw)
     if cal is not None:
         FETCH_SCALE["c5"] = cal[0]
