@@ -192,11 +192,15 @@ def arm(phase: str) -> None:
 
 def wait_device(device) -> None:
     """torch.cuda.synchronize() as an event poll: the host keeps running Python (and the
-    watchdog its deadline) while the device drains."""
+    watchdog its deadline) while the device drains. The first 20 ms poll without sleeping: a
+    sleep of 20 us lasts ~60-80 us on this host (timer slack), which the end of a short timed
+    region (the driver's 20-step run: ~1.8 ms) would count as step time."""
     event = torch.cuda.Event()
     event.record(torch.cuda.current_stream(device))
+    t0 = time.perf_counter()
     while not event.query():
-        time.sleep(20e-6)
+        if time.perf_counter() - t0 > 0.02:
+            time.sleep(20e-6)
 
 
 # ------------------------------------------------------------------------------------------------
