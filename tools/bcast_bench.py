@@ -3,7 +3,8 @@ Microbenchmark of the Bernoulli BCAST site kernel (C2's k_site_bcast_smem / k_si
 the engine's group launcher, over particle and element counts: mean kernel time (HIP events
 recorded by mi_group_forward_deferred around the site kernel) and packed-FMA rate.
 
-    python tools/bcast_bench.py           (MININF_AMD_BCAST_SMEM / _TUNE select the kernel)
+    python tools/bcast_bench.py           (MININF_AMD_LIB=<variant build> compares launch shapes,
+                                           tools/variant_build.py)
 """
 import os
 import sys

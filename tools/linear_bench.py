@@ -1,8 +1,8 @@
 """
 Microbenchmark of mi_linear_forward (the linear-predictor site kernel) at the C3 / C4 shapes.
 
-    python tools/linear_bench.py [--valu]      (MININF_AMD_LINEAR_TUNE=<variant> selects the
-                                               matrix-core launch variant, see linear.hip)
+    python tools/linear_bench.py [--valu]      (MININF_AMD_LIB=<variant build> compares launch
+                                               shapes, tools/variant_build.py)
 Prints one line per shape: mean kernel+finalize time and achieved TFLOP/s (4 P FLOP per eval).
 """
 import argparse
