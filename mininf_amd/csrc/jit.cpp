@@ -320,6 +320,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
+  // the descriptor's lines into L2 with one vector load (device_math.hpp kernarg_prefetch): the
+  // program's draw and prior prologue reads it in dependent chains
+  o << "  mi::kernarg_prefetch<(int)sizeof(mi_group)>();\n";
   o << "  const unsigned long long span_t0 = mi::span_begin(G.stamps);\n";
   o << "  const int lane = threadIdx.x & 63;\n";
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
