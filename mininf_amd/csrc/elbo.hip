@@ -1531,7 +1531,11 @@ Layout make_layout(const mi_elbo* e) {
     L.red.vblocks[r] = J.num_sites == 1 ? J.num_sites + J.num_slots : 1;
     // long lists over few particles (a fused draw's block rows: ~1000 segments, K = 128): 16
     // particles x 16 segment groups per block, for more blocks and fewer serial loads per lane
-    L.red.kred[r] = (J.nseg >= 512 && J.K < 2048)                       ? kKredLong
+    // (very long lists, C5's 977 block rows: 8 particles per block, two rounds of loads per lane
+    // instead of four -- 0.3 us per C5 step, tools/gpurun_r05/t29.sh; C4's 513 keep 16: 8 was
+    // 1.1 us slower there in r04)
+    L.red.kred[r] = (J.nseg >= 768 && J.K < 2048)                       ? 8
+                    : (J.nseg >= 512 && J.K < 2048)                     ? kKredLong
                     : (J.nseg >= 64 && kKred != mi::kRedKWide) ? kKred
                                                                      : mi::kRedKWide;
     nred += (int)ceil_div(J.K, L.red.kred[r]) * L.red.vblocks[r];
