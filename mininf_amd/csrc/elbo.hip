@@ -1067,6 +1067,24 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   if (!ABSORB && (int)threadIdx.x < 3 * R.tails)
     tg_early = (float)__hip_atomic_load(work + R.early + threadIdx.x, __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_AGENT);
+  // the Beta tails' argument words, read here and pinned after the share loads below: lanes 0 / 1
+  // read them after the tails' barrier otherwise, a dependent chain of scalar-cache misses there
+  double hw[kMaxTails] = {};
+  float* hout[kMaxTails][2] = {};
+  int hexp[kMaxTails] = {};
+  double* hpre[kMaxTails] = {};
+  if (!ABSORB) {
+#pragma unroll
+    for (int q = 0; q < kMaxTails; ++q)
+      if (q < R.tails) {
+        const int f = R.tail_factor[q];
+        hw[q] = -(double)1.0f * E.entropy_scale * factor_weight(E, f);
+        hout[q][0] = factor_grad(E, f, 0);
+        hout[q][1] = factor_grad(E, f, 1);
+        hexp[q] = (factor_exp(E, f, 0) ? 1 : 0) | (factor_exp(E, f, 1) ? 2 : 0);
+        hpre[q] = R.tail_saved[q];
+      }
+  }
   double t = 0.0;
   double acc[kMaxTails][2] = {};
   auto ld = [](const double* w) {
@@ -1109,6 +1127,16 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   }
   float tc1[kMaxTails] = {}, tc0[kMaxTails] = {};
   if (!ABSORB) {
+    // (in vector registers: the values come out of selects and fp64 arithmetic)
+    auto vpin = [](auto& v) { asm("" : "+v"(v)); };
+#pragma unroll
+    for (int q = 0; q < kMaxTails; ++q) {
+      vpin(hw[q]);
+      vpin(hout[q][0]);
+      vpin(hout[q][1]);
+      vpin(hexp[q]);
+      vpin(hpre[q]);
+    }
 #pragma unroll
     for (int q = 0; q < kMaxTails; ++q)
       if (q < R.tails) {
@@ -1176,12 +1204,15 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   const double total = block_sum(t, rsum + kElboThreads / kWave);
   MI_ELBO_STAMP(4);
   // the Adam update of element i of the tensor behind (factor f, parameter j), gradient g
-  auto adam_step = [&](int f, int j, int64_t i, float g) {
+  // (xv / xm / xq: the element's value and moments, av / am / aq unless a lane updates another
+  // lane's element)
+  auto adam_step_of = [&](int f, int j, int64_t i, float g, const float* xv, const float* xm,
+                          const float* xq) {
     if (!has_adam) return;
 #pragma unroll
     for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
       if (q >= sad.num || sad.slots[q].factor != f || sad.slots[q].param != j) continue;
-      float pv = av[q], mv = am[q], vv = aq[q];
+      float pv = xv[q], mv = xm[q], vv = xq[q];
       adam_update(sad, sco[q], pv, g, mv, vv);
       const mi_elbo_adam_slot& A = sad.slots[q];
       A.value[i] = pv;
@@ -1213,38 +1244,49 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         tws[0][wave] = w0;
         tws[1][wave] = w1;
       }
+      // element 0's value and moments on lane 1 too (lane j writes parameter j's gradient)
+      float zv[MI_ELBO_ADAM_SLOTS], zm[MI_ELBO_ADAM_SLOTS], zq[MI_ELBO_ADAM_SLOTS];
+#pragma unroll
+      for (int s = 0; s < MI_ELBO_ADAM_SLOTS; ++s) {
+        zv[s] = __shfl(av[s], 0);
+        zm[s] = __shfl(am[s], 0);
+        zq[s] = __shfl(aq[s], 0);
+      }
       __syncthreads();
-      if (threadIdx.x == 0) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
+      MI_ELBO_STAMP(11);
+      if (threadIdx.x < 2) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
+        const int j = threadIdx.x;
         double s0 = 0.0, s1 = 0.0;
         for (int w = 0; w < kElboThreads / kWave; ++w) {
           s0 += tws[0][w];
           s1 += tws[1][w];
         }
         const float tt = (tsum - 2.0f) * tgs[0];
-        double* pre = R.tail_saved[q];
         const double h0 = (double)(tt - (a - 1.0f) * tgs[1]);
         const double h1 = (double)(tt - (b - 1.0f) * tgs[2]);
-        pre[0] = s0;
-        pre[1] = s1;
-        pre[2] = h0;
-        pre[3] = h1;
+        if (j == 0) {
+          double* pre = hpre[q];
+          pre[0] = s0;
+          pre[1] = s1;
+          pre[2] = h0;
+          pre[3] = h1;
+        }
         if (E.options & MI_ELBO_FINAL_GRADS) {
           // the gradients k_elbo_backward writes from `pre` for an upstream of 1 (same
           // arithmetic as write_grad: u * pre + w * dH with u = 1, w = -entropy_scale * weight,
           // times the parameter under an exp transform)
           const int f = R.tail_factor[q];
-          const double w = -(double)1.0f * E.entropy_scale * factor_weight(E, f);
-          double g[2] = {(double)1.0f * s0 + w * h0, (double)1.0f * s1 + w * h1};
-          const float pv[2] = {a, b};
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            float* out = factor_grad(E, f, j);
-            if (out == nullptr) continue;
-            if (factor_exp(E, f, j)) g[j] *= (double)pv[j];
-            out[0] = (float)g[j];
-            adam_step(f, j, 0, (float)g[j]);
+          const double w = hw[q];
+          double g = j == 0 ? (double)1.0f * s0 + w * h0 : (double)1.0f * s1 + w * h1;
+          // (j differs between the lanes: both parameters' words picked)
+          float* out = j == 0 ? hout[q][0] : hout[q][1];
+          if (out != nullptr) {
+            if (hexp[q] & (1 << j)) g *= (double)(j == 0 ? a : b);
+            out[0] = (float)g;
+            adam_step_of(f, j, 0, (float)g, zv, zm, zq);
           }
         }
+        MI_ELBO_STAMP(12);
       }
       __syncthreads();
     }
@@ -1254,22 +1296,51 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     // the Normal tail's gradients for an upstream of 1: its blocks' sums in a fixed order, then
     // what k_elbo_backward's absorbed blocks write (u * s + w * dH, the exp chain rule)
     const mi_factor& F = E.factors[0];
-    const int64_t i = threadIdx.x;
-    if (nt_fin) {
-      const float p0 = nt_p0, p1 = nt_p1;
-      const double s0 = nt_s0, s1 = nt_s1;
-      // entropy_grad_of / write_grad_of of a Normal factor: dH = (0, 1 / scale)
-      const double d0 = 0.0, d1 = (double)(1.0f / p1);
-      const double w = -(double)1.0f * E.entropy_scale * F.weight;
-      double g[2] = {(double)1.0f * s0 + w * d0, (double)1.0f * s1 + w * d1};
-      const float pv[2] = {p0, p1};
+    // up to 32 elements: lane i (parameter 0) and lane 32 + i (parameter 1) of wave 0 each write
+    // one gradient and its Adam update, lane 32 + i with lane i's sums, parameters and moments
+    // (shuffled while the whole wave is here); more elements: one thread each, both parameters
+    const bool split = F.n <= kWave / 2;
+    const int src = split ? (int)(threadIdx.x & (kWave / 2 - 1)) : (int)(threadIdx.x & (kWave - 1));
+    float p0 = nt_p0, p1 = nt_p1;
+    double s0 = nt_s0, s1 = nt_s1;
+    float xv[MI_ELBO_ADAM_SLOTS], xm[MI_ELBO_ADAM_SLOTS], xq[MI_ELBO_ADAM_SLOTS];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (F.grad[j] == nullptr) continue;
-        if (F.transform[j] == MI_TRANSFORM_EXP) g[j] *= (double)pv[j];
-        F.grad[j][i * F.grad_stride[j]] = (float)g[j];
-        adam_step(0, j, i, (float)g[j]);
+    for (int s = 0; s < MI_ELBO_ADAM_SLOTS; ++s) {
+      xv[s] = av[s];
+      xm[s] = am[s];
+      xq[s] = aq[s];
+    }
+    if (split) {
+      p0 = __shfl(p0, src);
+      p1 = __shfl(p1, src);
+      s0 = __shfl(s0, src);
+      s1 = __shfl(s1, src);
+#pragma unroll
+      for (int s = 0; s < MI_ELBO_ADAM_SLOTS; ++s) {
+        xv[s] = __shfl(xv[s], src);
+        xm[s] = __shfl(xm[s], src);
+        xq[s] = __shfl(xq[s], src);
       }
+    }
+    const int64_t i = split ? src : (int64_t)threadIdx.x;
+    // entropy_grad_of / write_grad_of of a Normal factor: dH = (0, 1 / scale)
+    auto write = [&](int j, double g, float pv) {
+      if (F.grad[j] == nullptr) return;
+      if (F.transform[j] == MI_TRANSFORM_EXP) g *= (double)pv;
+      F.grad[j][i * F.grad_stride[j]] = (float)g;
+      adam_step_of(0, j, i, (float)g, xv, xm, xq);
+    };
+    const double w = -(double)1.0f * E.entropy_scale * F.weight;
+    if (split) {
+      if (threadIdx.x < kWave && i < F.n) {
+        if (threadIdx.x < kWave / 2)
+          write(0, (double)1.0f * s0 + w * 0.0, p0);
+        else
+          write(1, (double)1.0f * s1 + w * (double)(1.0f / p1), p1);
+      }
+    } else if (nt_fin) {
+      write(0, (double)1.0f * s0 + w * 0.0, p0);
+      write(1, (double)1.0f * s1 + w * (double)(1.0f / p1), p1);
     }
   }
   MI_ELBO_STAMP(7);

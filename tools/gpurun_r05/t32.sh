@@ -1,0 +1,18 @@
+#!/bin/bash
+# Lane-split ELBO tails (tree) vs HEAD (head variant): the ELBO GPU tests, the timing stamps of C2,
+# then C2 / C4 / C5 bench A/B
+set -u
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+fatal() { [ "$1" -eq 124 ] || [ "$1" -eq 137 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fused_reduce.py tests/test_gpu_final_grads.py tests/test_gpu_fused_step.py tests/test_gpu_parity.py tests/test_gpu_linear_draw.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t32_tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -1 gpurun_out/t32_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 python3 -u tools/elbo_timing.py run c2 > gpurun_out/etime32_c2.log 2>&1; rc=$?; echo "etime rc=$rc"; tail -4 gpurun_out/etime32_c2.log; fatal $rc && exit $rc
+for rep in 1 2; do for v in tree head; do
+  L=""; [ $v != tree ] && L=$GRAFT_REPO_ROOT/tools/_timing/$v/libmininf_amd.so
+  for c in c2 c4 c5; do
+    MININF_AMD_LIB=$L timeout -k 10 120 python3 -u bench.py --config $c --steps 480 --no-cpu-baseline --no-other-configs > gpurun_out/t32.json 2> gpurun_out/t32.err; rc=$?
+    [ $rc -ne 0 ] && { tail -5 gpurun_out/t32.err; exit $rc; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/t32.json').read().strip().splitlines()[-1]); print('$rep $v $c', round(d['ms_per_step']*1e3,2))"
+  done
+done; done
