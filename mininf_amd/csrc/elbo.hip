@@ -1085,6 +1085,12 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         hpre[q] = R.tail_saved[q];
       }
   }
+  // the same for the Normal tail (factor 0)
+  float* ngrad[2] = {E.factors[0].grad[0], E.factors[0].grad[1]};
+  int64_t nstride[2] = {E.factors[0].grad_stride[0], E.factors[0].grad_stride[1]};
+  int nexp = (E.factors[0].transform[0] == MI_TRANSFORM_EXP ? 1 : 0) |
+             (E.factors[0].transform[1] == MI_TRANSFORM_EXP ? 2 : 0);
+  double nw = -(double)1.0f * E.entropy_scale * E.factors[0].weight;
   double t = 0.0;
   double acc[kMaxTails][2] = {};
   auto ld = [](const double* w) {
@@ -1129,6 +1135,20 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   if (!ABSORB) {
     // (in vector registers: the values come out of selects and fp64 arithmetic)
     auto vpin = [](auto& v) { asm("" : "+v"(v)); };
+#pragma unroll
+    for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {   // (the optimised elements' loads, too)
+      vpin(av[q]);
+      vpin(am[q]);
+      vpin(aq[q]);
+    }
+    if (R.nt_job >= 0) {
+      vpin(ngrad[0]);
+      vpin(ngrad[1]);
+      vpin(nstride[0]);
+      vpin(nstride[1]);
+      vpin(nexp);
+      vpin(nw);
+    }
 #pragma unroll
     for (int q = 0; q < kMaxTails; ++q) {
       vpin(hw[q]);
@@ -1209,16 +1229,24 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   auto adam_step_of = [&](int f, int j, int64_t i, float g, const float* xv, const float* xm,
                           const float* xq) {
     if (!has_adam) return;
+    // the slot of (f, j) picked first, then one update: lanes of one wave with different (f, j)
+    // (the split tails below) share the update's instructions instead of running one per slot
+    int qs = -1;
+    float pv = 0.0f, mv = 0.0f, vv = 0.0f;
 #pragma unroll
-    for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q) {
-      if (q >= sad.num || sad.slots[q].factor != f || sad.slots[q].param != j) continue;
-      float pv = xv[q], mv = xm[q], vv = xq[q];
-      adam_update(sad, sco[q], pv, g, mv, vv);
-      const mi_elbo_adam_slot& A = sad.slots[q];
-      A.value[i] = pv;
-      A.exp_avg[i] = mv;
-      A.exp_avg_sq[i] = vv;
-    }
+    for (int q = 0; q < MI_ELBO_ADAM_SLOTS; ++q)
+      if (q < sad.num && sad.slots[q].factor == f && sad.slots[q].param == j) {
+        qs = q;
+        pv = xv[q];
+        mv = xm[q];
+        vv = xq[q];
+      }
+    if (qs < 0) return;
+    adam_update(sad, sco[qs], pv, g, mv, vv);
+    const mi_elbo_adam_slot& A = sad.slots[qs];
+    A.value[i] = pv;
+    A.exp_avg[i] = mv;
+    A.exp_avg_sq[i] = vv;
   };
   if (threadIdx.x == 0) {
     *loss = (float)total;
@@ -1325,18 +1353,18 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
     const int64_t i = split ? src : (int64_t)threadIdx.x;
     // entropy_grad_of / write_grad_of of a Normal factor: dH = (0, 1 / scale)
     auto write = [&](int j, double g, float pv) {
-      if (F.grad[j] == nullptr) return;
-      if (F.transform[j] == MI_TRANSFORM_EXP) g *= (double)pv;
-      F.grad[j][i * F.grad_stride[j]] = (float)g;
+      float* out = j == 0 ? ngrad[0] : ngrad[1];
+      if (out == nullptr) return;
+      if (nexp & (1 << j)) g *= (double)pv;
+      out[i * (j == 0 ? nstride[0] : nstride[1])] = (float)g;
       adam_step_of(0, j, i, (float)g, xv, xm, xq);
     };
-    const double w = -(double)1.0f * E.entropy_scale * F.weight;
+    const double w = nw;
     if (split) {
-      if (threadIdx.x < kWave && i < F.n) {
-        if (threadIdx.x < kWave / 2)
-          write(0, (double)1.0f * s0 + w * 0.0, p0);
-        else
-          write(1, (double)1.0f * s1 + w * (double)(1.0f / p1), p1);
+      if (threadIdx.x < kWave && i < F.n) {   // (one path for both halves: selects, not branches)
+        const int j = threadIdx.x < kWave / 2 ? 0 : 1;
+        const double g0 = (double)1.0f * s0 + w * 0.0, g1 = (double)1.0f * s1 + w * (double)(1.0f / p1);
+        write(j, j == 0 ? g0 : g1, j == 0 ? p0 : p1);
       }
     } else if (nt_fin) {
       write(0, (double)1.0f * s0 + w * 0.0, p0);

@@ -18,7 +18,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "_timing", "libmininf_amd.so")
+# (MI_ELBO_TIMING_LIB: another timing build, e.g. a copy kept for an A/B run)
+OUT = os.environ.get("MI_ELBO_TIMING_LIB") or os.path.join(ROOT, "tools", "_timing", "libmininf_amd.so")
 
 
 def build():
