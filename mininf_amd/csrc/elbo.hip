@@ -105,17 +105,6 @@ MI_DEV void entropy_grad(const mi_factor& f, int64_t i, double& d0, double& d1) 
   d1 = (double)(tt - (b - 1.0f) * trigammaf(b));
 }
 
-MI_DEV double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x == 0)
-    for (int w = 0; w < kElboThreads / kWave; ++w) s += red[w];
-  return s;
-}
-
 // ---- absorbed guide draws -------------------------------------------------------------------
 // Blocks [lead_blocks, lead_blocks + first[num]) of a launch work on absorbed factors: factor a
 // gets a [slices x gx] grid (gx columns of ti elements, slices of the particle rows), whose
@@ -1053,7 +1042,7 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
       aq[q] = A.exp_avg_sq[threadIdx.x];
     }
   }
-  if (has_adam && (int)threadIdx.x < sad.num) {   // block 0's (visible after block_sum's barrier)
+  if (has_adam && (int)threadIdx.x < sad.num) {   // block 0's (visible after the sums' barrier below)
     const double* o = work + R.early + 3 * kMaxTails + 2 * threadIdx.x;
     const double d[2] = {__hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                          __hip_atomic_load(o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
@@ -1221,7 +1210,33 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
   }
   const uint32_t fw0 = (int64_t)threadIdx.x < E.nflags ? E.flags[threadIdx.x] : 0u;
   const uint64_t step0 = (threadIdx.x == 0 && E.step_counter != nullptr) ? *E.step_counter : 0ull;
-  const double total = block_sum(t, rsum + kElboThreads / kWave);
+  // the loss sum and the Beta tails' two sums through one barrier: wave sums, then the waves in a
+  // fixed order (the loss's tree as before: each wave's lane-0 sum, waves 0..3 on thread 0); the tails' trigammas (block 0's, lanes 3 q .. 3 q + 2)
+  // into LDS before it too
+  __shared__ double tws[kMaxTails][2][kElboThreads / kWave];
+  __shared__ float tg_all[3 * kMaxTails];
+  double total = 0.0;
+  {
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    double* lred = rsum + kElboThreads / kWave;
+    const double tw = wave_sum(t);
+    if (lane == 0) lred[wave] = tw;
+    if (!ABSORB) {
+#pragma unroll
+      for (int q = 0; q < kMaxTails; ++q) {
+        if (q >= R.tails) break;
+        const double w0 = wave_sum(acc[q][0]), w1 = wave_sum(acc[q][1]);
+        if (lane == 0) {
+          tws[q][0][wave] = w0;
+          tws[q][1][wave] = w1;
+        }
+      }
+      if ((int)threadIdx.x < 3 * R.tails) tg_all[threadIdx.x] = tg_early;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int w = 0; w < kElboThreads / kWave; ++w) total += lred[w];
+  }
   MI_ELBO_STAMP(4);
   // the Adam update of element i of the tensor behind (factor f, parameter j), gradient g
   // (xv / xm / xq: the element's value and moments, av / am / aq unless a lane updates another
@@ -1256,22 +1271,11 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
 #pragma unroll
     for (int q = 0; q < kMaxTails; ++q) {
       if (q >= R.tails) break;
-      // both sums through one fixed-order tree (red[][0] and red[][1]); the three trigammas of the
-      // entropy derivatives on lanes 0-2 meanwhile
+      // (the sums and trigammas are in LDS, above; no barrier between the tails: each has its own
+      // words)
       const float a = tc1[q], b = tc0[q];
       const float tsum = a + b;
-      // the trigammas of (a + b, a, b): block 0's (early_tail), on lanes 3 q .. 3 q + 2
-      __shared__ float tg_all[3 * kMaxTails];
-      if ((int)threadIdx.x < 3 * R.tails) tg_all[threadIdx.x] = tg_early;
-      // wave sums, then the waves in order (fixed order, one barrier)
-      const double w0 = wave_sum(acc[q][0]), w1 = wave_sum(acc[q][1]);
-      __shared__ double tws[2][kElboThreads / kWave];
       const float* tgs = tg_all + 3 * q;
-      const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-      if (lane == 0) {
-        tws[0][wave] = w0;
-        tws[1][wave] = w1;
-      }
       // element 0's value and moments on lane 1 too (lane j writes parameter j's gradient)
       float zv[MI_ELBO_ADAM_SLOTS], zm[MI_ELBO_ADAM_SLOTS], zq[MI_ELBO_ADAM_SLOTS];
 #pragma unroll
@@ -1280,14 +1284,13 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         zm[s] = __shfl(am[s], 0);
         zq[s] = __shfl(aq[s], 0);
       }
-      __syncthreads();
       MI_ELBO_STAMP(11);
       if (threadIdx.x < 2) {   // pre = {sum dz dgrad0, sum dz dgrad1, dH/da, dH/db} (n = 1)
         const int j = threadIdx.x;
         double s0 = 0.0, s1 = 0.0;
         for (int w = 0; w < kElboThreads / kWave; ++w) {
-          s0 += tws[0][w];
-          s1 += tws[1][w];
+          s0 += tws[q][0][w];
+          s1 += tws[q][1][w];
         }
         const float tt = (tsum - 2.0f) * tgs[0];
         const double h0 = (double)(tt - (a - 1.0f) * tgs[1]);
@@ -1316,7 +1319,6 @@ __global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
         }
         MI_ELBO_STAMP(12);
       }
-      __syncthreads();
     }
   }
   MI_ELBO_STAMP(6);

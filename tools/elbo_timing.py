@@ -72,8 +72,8 @@ def run(config="c2"):
             print(f"  last block: count -> acquire fence done {last[0, 10] - last[0, 3]:.2f}, "
                   f"fence -> loads summed {last[0, 4] - last[0, 10]:.2f} us", flush=True)
         if last[0, 11] > 0:
-            print(f"  beta tail: sums -> barrier {last[0, 11] - last[0, 4]:.2f}, thread 0's tail "
-                  f"(grads, Adam) {last[0, 12] - last[0, 11]:.2f}, -> next barrier "
+            print(f"  beta tail: sums' barrier -> lanes' start {last[0, 11] - last[0, 4]:.2f}, lanes 0 / 1's "
+                  f"tail (grads, Adam) {last[0, 12] - last[0, 11]:.2f}, -> tails done "
                   f"{last[0, 6] - last[0, 12]:.2f} us", flush=True)
         red = rows[rows[:, 8] > 0]   # reducing blocks: descriptor decoded (8), segments summed (9)
         if red.shape[0]:
