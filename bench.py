@@ -9,9 +9,11 @@ The default workload is C2 (BASELINE.json configs[1]): the README biased-coin mo
 observations and 4096 Monte-Carlo particles per GPU (particles are sharded across GPUs: weak
 scaling). One site-log_prob eval = one (particle, site, observed element) triple.
 
-Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (timed with HIP
-event nodes around exactly that kernel in replays of the captured step, after the timed region) and the CPU baseline (the reference's
-torch-CPU semantics, oracle/cpu_port.py, on a bounded sample, N = 1 only).
+Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel (timed by span
+stamps -- every workgroup of exactly that kernel folds its start and end device clock into a slot
+-- in replays of a capture of the same step, after the timed region; HIP events around the kernel
+only for eager runs) and the CPU baseline (the reference's torch-CPU semantics, oracle/cpu_port.py,
+on a bounded sample, N = 1 only).
 """
 from __future__ import annotations
 
@@ -349,6 +351,23 @@ def data_shard(n, world, rank):
     if world == 1 and DATA_SHARD_WORLD > 1:
         return element_shard(n, shared=("mu",), world=DATA_SHARD_WORLD, rank=DATA_SHARD_RANK)
     return element_shard(n, shared=("mu",), world=world, rank=rank)
+
+
+def measured_issue(name):
+    """
+    The VALU pipe's busy fraction of the dominant kernel by the issue-cost model (profiles/
+    summarize.py: SQ instruction counts by type weighted by their measured issue cycles, over the
+    kernel's cycles on all SIMDs), from the newest committed profiles/rNN_valu_pmc.json that has
+    it for this config; None otherwise.
+    """
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_valu_pmc.json")),
+                       reverse=True):
+        with open(path) as fh:
+            entry = json.load(fh).get(name) or {}
+        if "valu_busy" in entry:
+            return entry["valu_busy"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def measured_traffic(name):
@@ -743,6 +762,18 @@ def run_config(config, args, world, rank, device, group, steps, warmup, cpu_budg
                 "kernel_ms": kernel_ms, "launches_timed": launches,
                 "kernel_timing": kernel_source,
                 "algorithmic_per_launch": f"{nbytes:.4g} B"}
+    if config == "c5":
+        # the FLOP count prices transcendentals at 1 and omits the Philox integer work, so it is
+        # not the issue-bound resource: the issue model's busy fraction is the bound's fraction
+        busy, busy_source = measured_issue(config)
+        if busy is not None:
+            roof["valu_busy"] = busy
+            roof["valu_busy_source"] = (f"{busy_source} (rocprofv3 --pmc SQ_INSTS_VALU by type x "
+                                        "measured issue cycles / kernel SIMD cycles)")
+    if config == "c4":
+        roof["kernel_timing"] += ("; the stamps span first workgroup start to last workgroup end "
+                                  "and exclude the dispatch (rocprofv3's trace includes it: "
+                                  "~2 us more for this ~24 us launch)")
     traffic, source = measured_traffic(config)
     roof["traffic"] = traffic
     if traffic is not None:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 17
+#define MI_ABI_VERSION 18
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -267,9 +267,10 @@ typedef struct mi_reduce {
 
 /* mi_group_forward with the finalize handed to the caller through *reduce (see above). When
  * non-NULL, the hipEvent_t `start_event` / `stop_event` are recorded on `stream` immediately before
- * and after the main site kernel (not the flag reset or the finalize reduction), as external event
- * nodes under stream capture (hipEventRecordExternal), so the caller can time exactly the
- * roofline-bound kernel -- also inside a replayed graph. */
+ * and after the main site kernel (not the flag reset or the finalize reduction), so the caller can
+ * time exactly the roofline-bound kernel of an eager launch. Events are eager-only: while `stream`
+ * is capturing, a call with either event returns MI_EUNSUPPORTED before enqueuing anything (the
+ * capture stays valid); a replayed kernel is timed by `mi_group.stamps` instead. */
 int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t workspace_bytes,
                               float* total, double* site_lp, float* slot_grad, uint32_t* flags,
                               void* start_event, void* stop_event, void* stream, mi_reduce* reduce);
@@ -619,8 +620,11 @@ int mi_adam_step(const mi_adam* adam, uint32_t* counters, void* stream);
  * bucket is written into a slot of every peer's region with system-scope stores, a flag carrying
  * the call number follows, the caller waits for every peer's flag in its own region and adds the
  * slots in rank order (two ranks: the same sum as any SUM all-reduce). A peer that never arrives
- * ends the wait after about a second and sets bit 0 of *error (device memory, never cleared by the
- * library). Every rank must call it the same number of times, with buckets of the same length. */
+ * ends the wait after about a second: the call sets bit 0 of *error (device-visible memory, e.g.
+ * pinned host memory the host can poll; never cleared by the library), fills `out` with NaN and
+ * does not advance the call counter. A call that finds *error set at entry does the same without
+ * writing into any peer's region (sticky failure: the communicator is unusable afterwards). Every
+ * rank must call it the same number of times, with buckets of the same length. */
 #define MI_PEER_MAX_RANKS 8
 #define MI_PEER_MAX_FLOATS 4096
 #define MI_PEER_HANDLE_BYTES 64
@@ -637,6 +641,8 @@ int mi_peer_close(void* region);
 int mi_peer_free(void* region);
 int mi_peer_allreduce(const mi_peer* peer, const float* in, float* out, int64_t n,
                       uint32_t* error, void* stream);
+/* Diagnostics (synchronous): the number of calls this rank's region has completed. */
+int mi_peer_call_count(const mi_peer* peer, uint64_t* count);
 
 /* ---- ELBO tail (replaces nn.py:224-228 + FactorizedDistribution.entropy, nn.py:121-131) -------- */
 

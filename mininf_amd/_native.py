@@ -40,7 +40,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 17   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 18   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -306,6 +306,7 @@ _SIGNATURES = {
     "mi_peer_close": (ctypes.c_int, [c_vp]),
     "mi_peer_free": (ctypes.c_int, [c_vp]),
     "mi_peer_allreduce": (ctypes.c_int, [ctypes.POINTER(Peer), c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "mi_peer_call_count": (ctypes.c_int, [ctypes.POINTER(Peer), ctypes.POINTER(ctypes.c_uint64)]),
     "mi_elbo_workspace_bytes": (ctypes.c_int, [ctypes.POINTER(Elbo),
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "mi_elbo_workspace_init": (ctypes.c_int, [c_vp, ctypes.c_size_t, c_vp]),

@@ -192,6 +192,10 @@ __global__ __launch_bounds__(kAdamBlock) void k_adam_step(const mi_adam A, const
   // complete (lgkmcnt(0) only: the first pass's loads stay in flight), the barrier, then the
   // bookkeeping wave counts the workgroup (two levels: groups of kAdamGroup, then the tensor); the
   // tensor's last workgroup to count stores s + 1 (every workgroup has read s by then).
+  // The empty asm consumes s1, so the compiler itself waits for the step read's result before the
+  // barrier whatever kind of load it emits (today a scalar load, covered by lgkmcnt; a vector
+  // load would get its vmcnt wait here) -- the explicit waitcnt alone only covers scalar loads.
+  __asm__ volatile("" ::"v"(s1));
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   if (books) {

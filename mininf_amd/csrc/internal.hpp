@@ -18,20 +18,21 @@ int mi_launch_finalize(const float* part, int64_t nseg, int64_t K, int num_sites
                        const double* scale, double slot_scale, float* total, double* site_lp,
                        float* slot_grad, double* scratch, hipStream_t stream, int rank1 = 0);
 
-// Record a caller's timing event on `stream`. Under stream capture the record becomes an event
-// record node of the graph, appended after the capture's current dependencies (every replay of
-// the graph then records it, so a replayed kernel can be timed); otherwise a plain record.
-inline hipError_t mi_record_event(void* event, hipStream_t stream) {
+// Timing events around a site kernel (the `start_event` / `stop_event` arguments) are for eager
+// launches only. Round 5 first recorded them under capture with hipEventRecordWithFlags(...,
+// hipEventRecordExternal) (commit c13b392): on this stack that call returns hipErrorInvalidValue
+// inside a capture, which invalidates the whole capture sequence, so the draw launched next
+// (mi_normal_rsample_exp) failed with the same code (gpurun_out/dbg1_one.err). Replayed kernels
+// are timed by span stamps instead (mi_group.stamps / mi_linear.stamps). An entry point given
+// events while `stream` is capturing returns MI_EUNSUPPORTED before it enqueues anything, so the
+// capture stays valid.
+inline hipError_t mi_stream_capturing(hipStream_t stream, bool* capturing) {
   hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
-  hipGraph_t graph = nullptr;
-  const hipGraphNode_t* deps = nullptr;
-  size_t ndeps = 0;
-  hipError_t e = hipStreamGetCaptureInfo_v2(stream, &status, nullptr, &graph, &deps, &ndeps);
-  if (e != hipSuccess) return e;
-  if (status != hipStreamCaptureStatusActive)
-    return hipEventRecord(static_cast<hipEvent_t>(event), stream);
-  hipGraphNode_t node = nullptr;
-  e = hipGraphAddEventRecordNode(&node, graph, deps, ndeps, static_cast<hipEvent_t>(event));
-  if (e != hipSuccess) return e;
-  return hipStreamUpdateCaptureDependencies(stream, &node, 1, hipStreamSetCaptureDependencies);
+  const hipError_t e = hipStreamIsCapturing(stream, &status);
+  *capturing = status != hipStreamCaptureStatusNone;
+  return e;
+}
+
+inline hipError_t mi_record_event(void* event, hipStream_t stream) {
+  return hipEventRecord(static_cast<hipEvent_t>(event), stream);
 }

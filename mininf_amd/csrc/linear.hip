@@ -919,6 +919,12 @@ int mi_linear_forward_deferred(const mi_linear* site, void* workspace, size_t wo
   if (!valid(site) || total == nullptr || flags == nullptr ||
       (site->compute_grads && dslots == nullptr))
     return MI_EINVAL;
+  if (start_event != nullptr || stop_event != nullptr) {   // eager timing only (internal.hpp)
+    bool capturing = false;
+    const hipError_t ce = mi_stream_capturing(static_cast<hipStream_t>(stream), &capturing);
+    if (ce != hipSuccess) return to_code(ce);
+    if (capturing) return MI_EUNSUPPORTED;
+  }
   size_t need = 0;
   mi_linear_workspace_bytes(site, &need);
   if (workspace == nullptr || workspace_bytes < need) return MI_EWORKSPACE;

@@ -14,8 +14,15 @@
 //
 // Coherence: the regions are fine-grained device memory; the data and flag stores and the flag
 // and slot loads are system-scope (they bypass the non-coherent caches), the data stores are
-// fenced before the flag store. A missing peer ends the wait after a bounded number of polls and
-// sets the caller's error word instead of hanging the device.
+// fenced before the flag store.
+//
+// Failure is loud and sticky. A missing peer ends the wait after a bounded number of polls; the
+// kernel then ORs 1 into the caller's error word (pinned host memory: the host reads it without a
+// synchronisation), writes NaN into `out` instead of a sum over stale slots, and does NOT advance
+// the call counter. Every later call sees the error word at entry and does the same without
+// touching any peer's region, so a failed rank never overwrites slots a late peer may still read;
+// its peers in turn time out on their next call and fail the same way. The host raises at its next
+// read of the word (PeerCommunicator.all_reduce before enqueuing, StepGraph's replay checks).
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -37,11 +44,22 @@ MI_DEV uint64_t* peer_counter(unsigned char* region, int64_t max_floats) {
   return reinterpret_cast<uint64_t*>(peer_slot(region, max_floats, 2, 0));
 }
 
+MI_DEV void peer_poison(float* out, int64_t n) {
+  for (int64_t i = threadIdx.x; i < n; i += kPeerThreads) out[i] = __builtin_nanf("");
+}
+
 __global__ __launch_bounds__(kPeerThreads) void k_peer_allreduce(const mi_peer P,
                                                                  const float* in,   // (may be out)
                                                                  float* out,
                                                                  int64_t n,
                                                                  uint32_t* __restrict__ error) {
+  __shared__ int failed;
+  // a failed communicator stays failed: no peer writes, no counter advance, a poisoned result
+  if (__hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+    peer_poison(out, n);
+    return;
+  }
+  if (threadIdx.x == 0) failed = 0;
   unsigned char* own = static_cast<unsigned char*>(P.regions[P.rank]);
   uint64_t* counter = peer_counter(own, P.max_floats);
   const uint64_t call = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
@@ -66,13 +84,19 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_allreduce(const mi_peer P
     uint32_t polls = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != call) {
       if (++polls == kPeerPolls) {
-        __hip_atomic_fetch_or(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        failed = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
+  if (failed) {   // (uniform after the barrier)
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_or(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    peer_poison(out, n);
+    return;
+  }
   // the sum in rank order (the caller's own bucket read from `in`)
   for (int64_t i = threadIdx.x; i < n; i += kPeerThreads) {
     float acc = 0.0f;
@@ -131,6 +155,17 @@ int mi_peer_allreduce(const mi_peer* peer, const float* in, float* out, int64_t 
   hipLaunchKernelGGL(mi::k_peer_allreduce, dim3(1), dim3(mi::kPeerThreads), 0,
                      static_cast<hipStream_t>(stream), *peer, in, out, n, error);
   return to_code(hipGetLastError());
+}
+
+int mi_peer_call_count(const mi_peer* peer, uint64_t* count) {
+  if (peer == nullptr || count == nullptr || peer->rank < 0 || peer->rank >= MI_PEER_MAX_RANKS ||
+      peer->regions[peer->rank] == nullptr || peer->max_floats < 1)
+    return MI_EINVAL;
+  const uint64_t* counter = reinterpret_cast<const uint64_t*>(
+      static_cast<const unsigned char*>(peer->regions[peer->rank]) +
+      2 * MI_PEER_MAX_RANKS * sizeof(uint64_t) +
+      (size_t)2 * MI_PEER_MAX_RANKS * (size_t)peer->max_floats * sizeof(float));
+  return to_code(hipMemcpy(count, counter, sizeof(uint64_t), hipMemcpyDeviceToHost));
 }
 
 }  // extern "C"

@@ -1373,6 +1373,12 @@ int mi_group_forward_deferred(const mi_group* group, void* workspace, size_t wor
   if (reduce != nullptr) *reduce = mi_reduce{};
   if (!validate_group(group) || total == nullptr || flags == nullptr) return MI_EINVAL;
   if (group->num_slots > 0 && slot_grad == nullptr) return MI_EINVAL;
+  if (start_event != nullptr || stop_event != nullptr) {   // eager timing only (internal.hpp)
+    bool capturing = false;
+    const hipError_t ce = mi_stream_capturing(static_cast<hipStream_t>(stream), &capturing);
+    if (ce != hipSuccess) return to_code(ce);
+    if (capturing) return MI_EUNSUPPORTED;
+  }
   const Plan p = make_plan(group);
   if (workspace_bytes < ::workspace_bytes(group, p) || workspace == nullptr) return MI_EWORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -191,6 +191,7 @@ class _GroupLauncher:
         # a deferred one-element Normal guide draw this launch makes itself (mi_group.pdraw,
         # claim_group_draws): (the draw, the operand index that reads it)
         self.pdraw: Optional[Tuple[guide.PendingDraw, int]] = None
+        self.made_pdraw = False   # the last launch made that draw (EvidenceLowerBoundLoss.last_fusions)
 
     @property
     def flag_sites(self) -> List[SiteRecord]:
@@ -368,6 +369,10 @@ class _GroupLauncher:
             pr.scale = self.prior[0].scale
         if self.pdraw is not None and not self.pdraw[0].done:
             rec, index = self.pdraw
+            if rec.source is None and not query:
+                # no fused exp for this scale: a deferred transform runs before the program reads
+                # it (as for the operand draw above)
+                guide.fill_exp(rec.scale)
             rec.describe(group.pdraw)
             group.pdraw.operand = index + 1
         return group, grads
@@ -465,6 +470,7 @@ class _GroupLauncher:
             group.pdraw = nat.Draw()
             code = launch()
         nat.check(code, "mi_group_forward_deferred")
+        self.made_pdraw = bool(group.pdraw.operand)
         if group.pdraw.operand:
             guide.take_draw(self.pdraw[0])
         if self.exp_pending is not None:
@@ -1785,7 +1791,9 @@ class _ElboPlan:
         folded_priors: prior sites evaluated by the launch of the site that reads their value
         (mi_prior); linear_theta_draws / linear_rows: linear launches that drew the guide's theta
         (mi_linear.draw) / their minibatch rows (mi_rows) themselves; fused_draws: Normal guide
-        factors drawn in registers by the site programs (mi_draw); deferred_reductions: site
+        factors drawn in registers by the site programs (mi_draw); program_draws: one-element
+        Normal guide factors drawn per particle by the site program that reads them (mi_group.pdraw,
+        no draw launch); deferred_reductions: site
         reductions finished by the ELBO forward; final_grads: the forward wrote the guide
         gradients (no backward launch for loss.backward()); optimizer_step: the Adam step ran in the held launch's last block (no launch of its own).
         """
@@ -1795,6 +1803,7 @@ class _ElboPlan:
             "linear_theta_draws": sum(l.drew_theta for l in self.linears),
             "linear_rows": sum(l.drew_rows for l in self.linears),
             "fused_draws": sum(p.kind == nat.DRAW_PARTIALS for p in self.absorbed.values()),
+            "program_draws": sum(l.made_pdraw for l in self.launchers),
             "deferred_reductions": self.deferred_count,
             "final_grads": int(getattr(self, "final", None) is not None),
             "optimizer_step": 0,   # set when the optimizer step joins the held launch

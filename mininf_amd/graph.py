@@ -103,6 +103,18 @@ def _capture_safe_distributions():
             module.broadcast_all = _ORIGINAL_BROADCAST_ALL
 
 
+def register_host_check(check: Callable[[], None]) -> None:
+    """
+    Called by an operation being captured into a :class:`StepGraph` whose failures surface in
+    host-visible memory (the peer all-reduce's error word): the graph calls ``check()`` before
+    each replay and in :meth:`StepGraph.check`, so the error is raised at the next host read.
+    Outside a capture, a no-op.
+    """
+    checks = getattr(_STATE, "host_checks", None)
+    if checks is not None and check not in checks:
+        checks.append(check)
+
+
 def deferred() -> Optional[list]:
     """
     The collector of deferred validations while a step is being warmed up or captured.
@@ -299,8 +311,10 @@ class StepGraph:
         gc_was_enabled = gc.isenabled()
         gc.disable()
         from . import particles
+        self._host_checks: List[Callable[[], None]] = []
         with torch.cuda.stream(capture_stream):
             self.graph.capture_begin(capture_error_mode=capture_error_mode)
+            _STATE.host_checks = self._host_checks
             try:
                 # the cached device copies of host constants the captured step reads live as long
                 # as the graph (particles.device_copy's cache may evict them)
@@ -326,6 +340,7 @@ class StepGraph:
                                    f"{_failing_op(error)}: {type(error).__name__}: {error}") \
                     from error
             finally:
+                _STATE.host_checks = None
                 if gc_was_enabled:
                     gc.enable()
         torch.cuda.current_stream().wait_stream(capture_stream)
@@ -405,11 +420,13 @@ class StepGraph:
         self._check(block=True)
 
     def _check(self, block: bool) -> None:
-        if not self._pending:
-            return
         if block:
             self._done.synchronize()
-        elif not self._done.query():
+        for check in self._host_checks:   # (host-visible words: read without a wait)
+            check()
+        if not self._pending:
+            return
+        if not block and not self._done.query():
             return
         self._pending = False
         values = self._flags_host.tolist()

@@ -109,12 +109,19 @@ def test_c5_fused_draw_full_size_against_oracle(device):
         return out
     engine.plan_absorption = spy
     try:
-        loss = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed)(cond, approx())
+        loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed)
+        loss = loss_fn(cond, approx())
         loss.backward()
     finally:
         engine.plan_absorption = original
     from mininf_amd import _native as nat
     assert ("z", nat.DRAW_PARTIALS) in seen[0], "z should be drawn inside the site kernel"
+    # the bench configuration's fusions were all active, so the oracle below checks them: z drawn
+    # in registers, mu drawn per particle by the same program (mi_group.pdraw), mu's prior folded
+    # into it (mi_group.prior)
+    assert loss_fn.last_fusions["fused_draws"] == 1, loss_fn.last_fusions
+    assert loss_fn.last_fusions["program_draws"] == 1, loss_fn.last_fusions
+    assert loss_fn.last_fusions["folded_priors"] == 1, loss_fn.last_fusions
 
     lib = oracle_build.load()
     eps_mu = np.empty((K, 1), np.float32)

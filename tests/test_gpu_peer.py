@@ -1,8 +1,10 @@
 """
 The one-shot peer-write all-reduce (mininf_amd.peer, VERDICT r04 "Next round" 6), run by two
-processes sharing the one GPU (the IPC handles exchanged over a gloo group, each rank mapping the
-other's region): the kernel's sums equal gloo's all_reduce of the same buckets bit for bit (two
-ranks: one addition), eagerly and replayed from a captured graph; and bench.py's sharded C4 step
+and three processes sharing the one GPU (the IPC handles exchanged over a gloo group, each rank
+mapping the others' regions): the kernel's sums equal gloo's all_reduce of the same buckets (bit for
+bit with two ranks: one addition), eagerly and replayed from a captured graph; a rank that never
+calls makes every other rank's call fail loudly and bounded (NaN bucket, sticky error word,
+PeerTimeout at the next host read, call counter kept); and bench.py's sharded C4 step
 with the peer all-reduce captured in its graph ends on the same loss as the step split around
 gloo's all-reduce. Unmeasured on multi-GPU hardware. Each check runs in child processes with
 their own time limits.
@@ -31,15 +33,38 @@ def _last_json(out):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
-def test_peer_all_reduce_matches_gloo(device):
-    out = subprocess.run([sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1",
-                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                          "--master-port", "29561",
-                          os.path.join(ROOT, "tests", "peer_check.py")],
-                         env=_env(), capture_output=True, text=True, timeout=240)
-    line = _last_json(out)
-    assert line["eager_equal"] and line["graph_equal"], line
-    assert line["error_word"] == 0, line
+def _ranks(n, mode, port, timeout=240):
+    return subprocess.run([sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1",
+                           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+                           "--master-port", str(port),
+                           os.path.join(ROOT, "tests", "peer_check.py"), mode],
+                          env=_env(), capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world,port", [(2, 29561), (3, 29563)])
+def test_peer_all_reduce_matches_gloo(device, world, port):
+    line = _last_json(_ranks(world, "sum", port))
+    assert line["world"] == world
+    for rank in line["ranks"]:
+        assert rank["eager_equal"] and rank["graph_equal"], line
+        assert rank["error_word"] == 0, line
+
+
+@pytest.mark.parametrize("world,port", [(2, 29565), (3, 29567)])
+def test_peer_all_reduce_missing_rank_fails_loudly(device, world, port):
+    """The last rank never calls: the others time out within the bounded wait (seconds, not the
+    test's limit), poison their buckets, raise PeerTimeout at the next host read (the StepGraph's
+    check, the next eager call -- which enqueues nothing) and keep their call counters."""
+    line = _last_json(_ranks(world, "missing", port, timeout=180))
+    callers = line["ranks"][:-1]
+    assert len(callers) == world - 1
+    for rank in callers:
+        assert rank["wait_s"] < 30, line
+        assert rank["graph_nan"] and rank["graph_raised"], line
+        assert rank["eager_raised"] and rank["eager_untouched"], line
+        assert rank["sticky_nan"], line
+        assert rank["counter"] == [0, 0], line
+        assert rank["error_word"] == 1, line
 
 
 def _bench(*argv):

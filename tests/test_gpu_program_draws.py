@@ -4,11 +4,15 @@ The masked hierarchical model's global parameter (examples/missing-observations.
 
 * mu's prior site is evaluated by the program's block-row flush (mi_group.prior on site 0's
   per-particle parameter) instead of a launch of its own: loss and gradients equal the unfolded
-  path (MININF_AMD_FOLD_PRIOR=0) at 1e-6 and the oracle at 1e-5;
+  path (MININF_AMD_FOLD_PRIOR=0) at 1e-6;
 * mu's K draws are made by the program (mi_group.pdraw: the mi_normal_rsample normals and fmaf,
   bit-identical) instead of a mi_normal_rsample launch before it: the same loss, gradients and
   written draws as the separate launch (MININF_AMD_DRAW_IN_LINEAR=0 keeps every draw its own
   launch), eager and under graph replay.
+
+Both fusions are checked against the oracle (not only against the unfused path) at full size by
+test_gpu_fullsize.py::test_c5_fused_draw_full_size_against_oracle, which asserts that both were
+active (last_fusions: program_draws, folded_priors) in the evaluation it compares at 1e-5.
 """
 import numpy as np
 import pytest
@@ -86,6 +90,7 @@ def test_program_makes_the_global_draw(device, monkeypatch):
     losses, grads, params, fusions = _steps(device)
     assert calls == [] and plain == [], "mu's draw ran in the site program"
     assert fusions["fused_draws"] == 1 and fusions["folded_priors"] == 1
+    assert fusions["program_draws"] == 1
     ref_losses, ref_grads, ref_params, _ = _steps(device, MININF_AMD_DRAW_IN_LINEAR="0")
     assert losses == ref_losses
     for a, b in zip(grads, ref_grads):

@@ -31,7 +31,7 @@ def test_library_loads_and_exports_header():
         assert hasattr(lib, name), name
     assert set(names) == set(nat.EXPORTED_SYMBOLS)
     target = ctypes.create_string_buffer(16)
-    assert lib.mi_abi_version(target, 16) == nat.ABI_VERSION == 17
+    assert lib.mi_abi_version(target, 16) == nat.ABI_VERSION == 18
     assert target.value == b"gfx950"
 
 
@@ -75,6 +75,10 @@ def test_invalid_arguments_are_rejected():
     peer.rank = 2
     assert lib.mi_peer_allreduce(ctypes.byref(peer), ctypes.byref(buf), ctypes.byref(buf), 1,
                                  ctypes.byref(word), None) == -1   # rank outside the world
+    count = ctypes.c_uint64()
+    assert lib.mi_peer_call_count(None, ctypes.byref(count)) == -1
+    assert lib.mi_peer_call_count(ctypes.byref(peer), None) == -1
+    assert lib.mi_peer_call_count(ctypes.byref(peer), ctypes.byref(count)) == -1  # (no region)
 
 
 def hierarchical(n):
