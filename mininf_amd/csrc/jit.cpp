@@ -112,6 +112,18 @@ std::string mask_kind_tag(const mi_site& st) {
   return std::to_string((int)kind_of(st.mask_stride_k, st.mask_stride_i));
 }
 
+// Fused-draw row loop shape (round 6 A/B; read per compile, part of the signature):
+//   pairs: two particles per iteration as two independent Philox -> Box-Muller -> density chains
+//   (accumulator form only), tile rows of the per-wave particle-sum LDS tile, and an explicit
+//   waves-per-EU occupancy target for the program (0: the compiler's choice).
+int env_int(const char* name, int fallback) {
+  const char* v = std::getenv(name);
+  return v != nullptr && *v != 0 ? std::atoi(v) : fallback;
+}
+bool draw_pairs() { return env_int("MININF_AMD_DRAW_PAIRS", 1) != 0; }
+int draw_tile_rows(int nv) { return env_int("MININF_AMD_TILE_ROWS", nv <= 2 ? 16 : 8); }
+int draw_waves_per_eu() { return env_int("MININF_AMD_WAVES_PER_EU", 0); }
+
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
   s << (plan.row ? "R" : "C") << plan.elems << "/" << plan.kw << (plan.combined ? "c" : "s")
@@ -135,6 +147,9 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
     << (g.draw.scale_exp != nullptr ? "x" : "")
     << (g.prior.present != 0 ? "|prior" + std::to_string(g.prior.family) : "")
     << (g.pdraw.operand != 0 ? "|pdraw" + std::to_string(g.pdraw.operand) : "");
+  if (g.draw.operand != 0)
+    s << "|pairs" << draw_pairs() << "|t" << draw_tile_rows(g.num_sites + g.num_slots) << "|w"
+      << draw_waves_per_eu();
   return Signature{s.str()};
 }
 
@@ -316,8 +331,12 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   };
   auto dense_grad = [&](int op) { return g.compute_grads && g.operands[op].grad_mode == MI_GRAD_DENSE; };
 
+  const int draw = g.draw.operand - 1;
   o << "#include \"device_math.hpp\"\n";
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
+  if (row && draw >= 0 && draw_waves_per_eu() > 0)
+    o << "__attribute__((amdgpu_waves_per_eu(" << draw_waves_per_eu() << ", "
+      << draw_waves_per_eu() << "))) ";
   o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
   // the descriptor's lines into L2 with one vector load (device_math.hpp kernarg_prefetch): the
@@ -328,7 +347,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
   // LDS of the row loops' particle sums: nv tiles of [tile_rows][65] floats per wave
-  const int tile_rows = nv <= 2 ? 16 : 8;
+  const int tile_rows = (row && draw >= 0) ? draw_tile_rows(nv) : (nv <= 2 ? 16 : 8);
   if (row)
     o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
       << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";
@@ -425,9 +444,11 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   // block_rows: the block's four waves combine their row sums in LDS (fixed wave order) and write
   // one partial row per block (gridDim.x rows) -- a quarter of the partials, short enough for the
   // ELBO forward's fused reduction; every wave then runs the loop (see emit_draw_loop).
-  auto emit_particle_sums = [&](const char* in, bool block_rows) {
-    for (int v = 0; v < nv; ++v)
-      o << in << "tile[" << v * tile_rows * 65 << " + r * 65 + lane] = " << value_expr(v) << ";\n";
+  // write = false: the caller wrote the tile rows (the paired fused-draw loop)
+  auto emit_particle_sums = [&](const char* in, bool block_rows, bool write = true) {
+    if (write)
+      for (int v = 0; v < nv; ++v)
+        o << in << "tile[" << v * tile_rows * 65 << " + r * 65 + lane] = " << value_expr(v) << ";\n";
     o << in << "if (r == " << tile_rows - 1 << " || k + 1 == k_end) {\n";
     o << in << "  mi::wave_lds_sync();\n";
     if (!block_rows) {
@@ -735,7 +756,6 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   // Philox call yields the lane's four normals of a quad -- exactly the eps of mi_normal_rsample for
   // (quad, particle). z = loc + eps * scale is formed in registers and d/dz is reduced over the
   // block's particles into dloc / dscale, so neither z nor dz touches memory.
-  const int draw = g.draw.operand - 1;
   auto emit_draw_loop = [&]() {
     const char* in = "    ";
     auto elem = [&](const char* e) {
@@ -804,10 +824,39 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     // Two copies of the particle loop: a segment that is neither ragged nor past the end has
     // every element valid, and its unmasked sites need no per-element select.
     const bool acc = packed && acc_form(g, draw);
+    // Two particles per iteration (accumulator form): the loop body below is emitted twice, for
+    // particles k0 and k0 + 1, each in its own scope with `k` bound to its particle, so the two
+    // Philox -> Box-Muller -> density chains are independent and the compiler interleaves them
+    // (one chain per wave left half the issue cycles stalled at 4 waves per SIMD). An odd last
+    // particle is evaluated twice and its second copy masked out of every sum (its tile row is
+    // past the flush bound, its d loc / d scale terms are zeroed). Sums keep the sequential order:
+    // dal / das add particle k0's terms, then k0 + 1's.
+    const bool pairs = acc && draw_pairs() && tile_rows % 2 == 0;
     auto emit_k_loop = [&](const std::string& valid) {
     if (acc) emit_acc_prologue(valid);
+    if (pairs) {
+      for (int op = 0; op < g.num_operands; ++op)
+        if (is(op, kParticle) && op != pdraw)
+          o << in << "float pm" << op << " = k_begin + 1 < k_end ? x" << op << "[(k_begin + 1) * sk"
+            << op << "] : pn" << op << ";\n";
+      o << in << "for (long k0 = k_begin; k0 < k_end; k0 += 2) {\n";
+      o << in << "  const bool two = k0 + 1 < k_end;\n";
+      o << in << "  const int r0 = (int)((k0 - k_begin) & " << tile_rows - 1 << ");\n";
+      for (int op = 0; op < g.num_operands; ++op)
+        if (is(op, kParticle) && op != pdraw) {
+          o << in << "  const float pa" << op << " = pn" << op << ", pb" << op << " = pm" << op << ";\n";
+          o << in << "  if (k0 + 2 < k_end) { pn" << op << " = x" << op << "[(k0 + 2) * sk" << op
+            << "]; pm" << op << " = x" << op << "[min(k0 + 3, k_end - 1) * sk" << op << "]; }\n";
+        }
+      for (int v = 0; v < nv; ++v) o << in << "  float va" << v << ", vb" << v << ";\n";
+    } else {
     o << in << "for (long k = k_begin; k < k_end; ++k) {\n";
     o << in << "  const int r = (int)((k - k_begin) & " << tile_rows - 1 << ");\n";
+    }
+    for (int copy = 0; copy < (pairs ? 2 : 1); ++copy) {
+    if (pairs)
+      o << in << "  {\n" << in << "  const long k = " << (copy == 0 ? "k0" : "two ? k0 + 1 : k0")
+        << ";\n";
     if (packed) {   // pairs: eps and z = loc + eps * scale on packed instructions
       o << in << "  mi::f2 ep2[" << E / 2 << "];\n#pragma unroll\n" << in << "  for (int qq = 0; qq < "
         << E / 4 << "; ++qq) mi::guide_normals2(dseed, dstep, dstream, (unsigned long long)((base >> 2) "
@@ -835,6 +884,8 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     for (int op = 0; op < g.num_operands; ++op)
       if (is(op, kParticle) && op == pdraw)
         o << in << "  const float p" << op << " = pdv[k - k_begin];\n";
+      else if (is(op, kParticle) && pairs)
+        o << in << "  const float p" << op << " = " << (copy == 0 ? "pa" : "pb") << op << ";\n";
       else if (is(op, kParticle))
         o << in << "  const float p" << op << " = pn" << op << ";\n" << in << "  if (k + 1 < k_end) pn"
           << op << " = x" << op << "[(k + 1) * sk" << op << "];\n";
@@ -871,6 +922,11 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       return packed ? "g" + std::to_string(op) + "[(" + e + ") >> 1][(" + e + ") & 1]"
                          : "g" + std::to_string(op) + "[" + e + "]";
     };
+    if (pairs && copy == 1)   // (an odd last particle's second copy adds nothing)
+      for (int op = 0; op < g.num_operands; ++op)
+        if (dense_grad(op))
+          o << in2 << "#pragma unroll\n" << in2 << "for (int h = 0; h < " << E / 2 << "; ++h) g" << op
+            << "[h] = two ? g" << op << "[h] : mi::splat2(0.0f);\n";
     for (int op = 0; op < g.num_operands; ++op) {
       if (!dense_grad(op)) continue;
       if (op == draw && packed)
@@ -888,7 +944,25 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
           << "; ++e) if (ok[e]) r[(e >> 2) * 256 + (e & 3)] = G.grad_scale * " << gel(op, "e")
           << "; }\n";
     }
-    emit_particle_sums(in2, plan.block_rows);
+    if (!pairs) {
+      emit_particle_sums(in2, plan.block_rows);
+    } else {
+      for (int v = 0; v < nv; ++v)
+        o << in2 << (copy == 0 ? "va" : "vb") << v << " = " << value_expr(v) << ";\n";
+      o << in << "  }\n";
+    }
+    }   // copies
+    if (pairs) {
+      // particle k0's row r0, k0 + 1's row r0 + 1; the flush sees the last particle written
+      const char* in2 = "      ";
+      for (int v = 0; v < nv; ++v)
+        o << in2 << "tile[" << v * tile_rows * 65 << " + r0 * 65 + lane] = va" << v << ";\n" << in2
+          << "tile[" << v * tile_rows * 65 << " + (r0 + 1) * 65 + lane] = vb" << v << ";\n";
+      o << in2 << "{\n" << in2 << "const int r = two ? r0 + 1 : r0;\n" << in2
+        << "const long k = two ? k0 + 1 : k0;\n";
+      emit_particle_sums(in2, plan.block_rows, false);
+      o << in2 << "}\n";
+    }
     o << in << "}\n";
     };
     o << in << "if (" << (plan.block_rows ? "live && " : "") << "shift == 0) {\n";

@@ -18,16 +18,23 @@ pytestmark = pytest.mark.gpu
 
 
 class AlwaysEvents:
-    """engine.KERNEL_TIMER that hands out an event pair for every launch, captured or not."""
-    def __init__(self):
+    """engine.KERNEL_TIMER that hands out an event pair for every launch, captured or not. torch
+    creates an event's hipEvent_t at its first record, so the pool's events are recorded once here,
+    outside any capture (as bench.py's EventTimer does)."""
+    def __init__(self, count=16):
+        self.pool = []
+        for _ in range(count):
+            start = torch.cuda.Event(enable_timing=True)
+            stop = torch.cuda.Event(enable_timing=True)
+            start.record()
+            stop.record()
+            self.pool.append((start, stop))
+        torch.cuda.synchronize()
         self.pairs = []
 
     def pair(self, launcher):
-        start = torch.cuda.Event(enable_timing=True)
-        stop = torch.cuda.Event(enable_timing=True)
-        if not torch.cuda.is_current_stream_capturing():
-            start.record()
-            stop.record()
+        start, stop = self.pool[len(self.pairs) % len(self.pool)]
+        assert start.cuda_event and stop.cuda_event
         self.pairs.append((start, stop))
         return start, stop
 
