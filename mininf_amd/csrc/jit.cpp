@@ -829,7 +829,9 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     // Philox -> Box-Muller -> density chains are independent and the compiler interleaves them
     // (one chain per wave left half the issue cycles stalled at 4 waves per SIMD). An odd last
     // particle is evaluated twice and its second copy masked out of every sum (its tile row is
-    // past the flush bound, its d loc / d scale terms are zeroed). Sums keep the sequential order:
+    // past the flush bound, its d loc / d scale terms are zeroed through an opaque lane mask: a
+    // select on the uniform `two` became a branch around the gradient terms, which split the loop
+    // body and kept the two chains from interleaving). Sums keep the sequential order:
     // dal / das add particle k0's terms, then k0 + 1's.
     const bool pairs = acc && draw_pairs() && tile_rows % 2 == 0;
     auto emit_k_loop = [&](const std::string& valid) {
@@ -926,7 +928,8 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       for (int op = 0; op < g.num_operands; ++op)
         if (dense_grad(op))
           o << in2 << "#pragma unroll\n" << in2 << "for (int h = 0; h < " << E / 2 << "; ++h) g" << op
-            << "[h] = two ? g" << op << "[h] : mi::splat2(0.0f);\n";
+            << "[h] = mi::f2{mi::keep_if(g" << op << "[h].x, two), mi::keep_if(g" << op
+            << "[h].y, two)};\n";
     for (int op = 0; op < g.num_operands; ++op) {
       if (!dense_grad(op)) continue;
       if (op == draw && packed)

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 from mininf_amd import _native as nat  # noqa: E402
 
 
-def c5_group(K: int, N: int, grads: bool = True) -> nat.Group:
+def c5_group(K: int, N: int, grads: bool = True, bench: bool = True) -> nat.Group:
     dummy = 1 << 20   # any aligned non-null address: only the signature matters here
     g = nat.Group()
     g.K, g.N = K, N
@@ -49,6 +49,15 @@ def c5_group(K: int, N: int, grads: bool = True) -> nat.Group:
         if masked:
             s.mask, s.mask_stride_k, s.mask_stride_i = dummy, 0, 1
         s.scale = 1.0
+    if bench:   # as benched: mu's prior folded in (mi_group.prior), mu drawn by the program (pdraw)
+        g.prior.present, g.prior.family = 1, nat.NORMAL
+        g.prior.constant[0], g.prior.constant[1] = 0.0, 1.0
+        g.prior.scale, g.prior.flags = 1.0, dummy
+        p = g.pdraw
+        p.operand, p.stream_id = 2, 0
+        p.loc, p.loc_stride, p.scale, p.scale_stride = dummy, 0, dummy, 0
+        p.scale_exp = dummy
+        p.seed, p.step, p.step_device = 1, 0, dummy
     return g
 
 
