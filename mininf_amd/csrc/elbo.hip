@@ -807,21 +807,223 @@ MI_DEV void early_tail(const mi_elbo& E, const ReducePlan& R, const AbsorbPlan& 
   }
 }
 
-// ---- the forward's finish -------------------------------------------------------------------
-// The last share-writing block of k_elbo_forward (or k_elbo_tail's one block) adds the shares in a
-// fixed order and runs the tails: the one-element Beta factors' sums and final gradients, the
-// Normal tail, the optimizer step of the optimised elements, the flag mirror and the generator
-// step. `sad`: the optimizer descriptor in LDS; `rsum`: 2 * kElboThreads doubles of LDS.
-template <bool ABSORB>
-MI_DEV void elbo_finish(const mi_elbo& E, const AbsorbPlan& P, const ReducePlan& R,
-                        double* __restrict__ work, unsigned* __restrict__ counters,
-                        float* __restrict__ loss, const mi_elbo_adam* __restrict__ adam,
-                        const mi_elbo_adam& sad, double* rsum, const int nshare) {
+// ---- forward --------------------------------------------------------------------------------
+// HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
+// of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
+// ABSORB: the launch has forward-absorbed Beta blocks (absorbed_block<true>, inline fp64 implicit
+// gradients: a large register footprint the other variants do not pay for).
+template <bool HAS_BETA, bool ABSORB>
+__global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
+                                                               const AbsorbPlan P,
+                                                               const ReducePlan R,
+                                                               double* __restrict__ work,
+                                                               unsigned* __restrict__ counters,
+                                                               float* __restrict__ loss,
+                                                               const mi_elbo_adam* __restrict__ adam) {
+  __shared__ double red[kElboThreads][2];
+  __shared__ bool last;
+#if MI_ELBO_TIMING
+  if (threadIdx.x < 16) mi_ets[threadIdx.x] = 0;
+#endif
+  MI_ELBO_STAMP(0);
+  kernarg_prefetch<(int)(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan))>();
+  const int nred = R.first[R.num];
+  const int nloss = P.lead_blocks;
+  const int nshare = nred + nloss;   // blocks that write a loss share
+  if (ABSORB && (int)blockIdx.x >= nshare) {
+    absorbed_block<true>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
+    return;
+  }
+  if (!ABSORB && (int)blockIdx.x >= nshare) {
+    // MI_ELBO_FINAL_GRADS: the gradients of the fused-draw factors (MI_DRAW_PARTIALS) for an
+    // upstream of 1 -- k_elbo_backward's absorbed blocks, run here (P: their plan); they read only
+    // the site launches' partial rows, so they run beside the reductions
+    absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
+    return;
+  }
+  if (!ABSORB && blockIdx.x == 0 && (R.tails > 0 || adam != nullptr))
+    early_tail(E, R, P, adam, work);
+  double* rsum = &red[0][0];
+  double share;
+  double c[kMaxTails][2] = {};   // this lane's tail contributions
+  double nt[2] = {0.0, 0.0};     // this lane's Normal-tail sums (R.nt_job), element nt_slot
+  int nt_slot = -1, nt_kb = 0;
+  if (!ABSORB && (int)blockIdx.x < nred) {   // (ABSORB launches have no deferred reductions)
+    share = reduce_block(E, R, (int)blockIdx.x, c, red, nt, nt_slot, nt_kb);
+    __syncthreads();
+  } else {
+    const int64_t lead = (int64_t)blockIdx.x - nred;
+    const int64_t stride = (int64_t)nloss * kElboThreads;
+    const int64_t first = lead * kElboThreads + threadIdx.x;
+    double lp = 0.0, h = 0.0;
+    for (int t = 0; t < E.num_terms; ++t)
+      for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
+    if (R.external) {
+#pragma unroll
+      for (int a = 0; a < MI_MAX_REDUCE; ++a)
+        if (a < R.num)
+          for (int64_t k = first; k < E.K; k += stride) lp += (double)E.reduce[a].total[k];
+    }
+    for (int f = 0; f < E.num_factors; ++f) {
+      const mi_factor& F = E.factors[f];
+      if (!HAS_BETA || F.family == MI_NORMAL) {
+        // sum_i (0.5 + 0.5 log(2 pi) + log scale_i): the constant once, the logs per element
+        const float* __restrict__ sc = F.param[1];
+        const int64_t ss = F.stride[1];
+        float hf = 0.0f;   // per-thread partial of a few terms, then fp64
+        int64_t head = 0;
+        if (ss == 1 && (reinterpret_cast<uintptr_t>(sc) & 15) == 0) {
+          // 16-byte loads, all issued before the logs
+          const int64_t nq = F.n >> 2;
+          const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
+          int64_t q = first;
+          // eight quads' loads in flight per round, then four (a lead block covers ~32 elements
+          // per lane: one memory round trip, not two); quads summed in order either way
+          for (; q + 7 * stride < nq; q += 8 * stride) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = sq[q + u * stride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
+          }
+          for (; q + 3 * stride < nq; q += 4 * stride) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sq[q + u * stride];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
+          }
+          for (; q < nq; q += stride) {
+            const float4 v = sq[q];
+            hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
+          }
+          head = nq << 2;
+        }
+        for (int64_t i = head + first; i < F.n; i += stride) hf += logf(sc[i * ss]);
+        double hn = (double)hf;
+        if (first == 0) hn += 1.4189385332046727 * (double)F.n;
+        h += F.weight * hn;
+      } else {
+        double hb = 0.0;
+        for (int64_t i = first; i < F.n; i += stride) hb += factor_entropy(F, i);
+        h += F.weight * hb;
+      }
+    }
+    share = (double)E.g0 * lp - E.entropy_scale * h;
+    if (!ABSORB) {   // tail sources written by earlier launches
+#pragma unroll
+      for (int q = 0; q < kMaxTails; ++q) {
+        const int mask = q < R.tails ? R.tail_ext[q] : 0;
+        if (mask == 0) continue;
+        // every source slot and the factor read unconditionally (an unused slot reads the first
+        // used one and adds +0): one memory round trip instead of one per load
+        const int on0 = __builtin_ctz((unsigned)mask);
+        for (int64_t k = first; k < E.K; k += stride) {
+          float g = 0.0f;
+#pragma unroll
+          for (int src = 0; src < MI_MAX_SOURCES; ++src) {
+            const bool on = (mask >> src) & 1;
+            const int sc = on ? src : on0;
+            g += keep_if(R.tail_src[q][sc][k * R.tail_src_stride[q][sc]], on);
+          }
+          const double2 d = *reinterpret_cast<const double2*>(R.tail_dgrad[q] + 2 * k);
+          if (g == 0.0f) continue;   // a zero upstream never meets the factor
+          c[q][0] += (double)g * d.x;
+          c[q][1] += (double)g * d.y;
+        }
+      }
+    }
+  }
+  MI_ELBO_STAMP(1);
+  // the block's share and its tail partials in one pass: wave sums, then the waves in order
+  // through LDS, one barrier (thread 0 stores the tail partials and returns the share)
+  double s;
+  {
+    constexpr int kWaves = kElboThreads / kWave;
+    constexpr int kVals = 1 + 2 * kMaxTails;
+    __shared__ double wsum[kVals][kWaves];
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+    const double v0 = wave_sum(share);
+    if (lane == 0) wsum[0][wave] = v0;
+    const int tails = ABSORB ? 0 : R.tails;
+    // the Normal tail's sums live on the particle lanes (the first kRedK <= 64 threads: wave 0)
+    double nts0 = 0.0, nts1 = 0.0;
+    if (!ABSORB && nt_slot >= 0 && wave == 0) {
+      nts0 = wave_sum(nt[0]);
+      nts1 = wave_sum(nt[1]);
+    }
+#pragma unroll
+    for (int t = 0; t < kMaxTails; ++t)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (t < tails) {
+          const double v = wave_sum(c[t][q]);
+          if (lane == 0) wsum[1 + 2 * t + q][wave] = v;
+        }
+    __syncthreads();
+    s = 0.0;
+    if (threadIdx.x == 0) {
+      for (int w = 0; w < kWaves; ++w) s += wsum[0][w];
+      for (int t = 0; t < tails; ++t)
+        for (int q = 0; q < 2; ++q) {
+          double v = 0.0;
+          for (int w = 0; w < kWaves; ++w) v += wsum[1 + 2 * t + q][w];
+          __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + blockIdx.x) * 2 + q], v,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      if (!ABSORB && nt_slot >= 0) {
+        double* w2 = &work[R.nt_part + ((int64_t)nt_slot * R.nt_nkb + nt_kb) * 2];
+        __hip_atomic_store(w2, nts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w2 + 1, nts1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  MI_ELBO_STAMP(2);
+  // mi_elbo_forward_adam: every share-writing block fetches the optimizer's descriptor (240 B, an
+  // L2 hit after the first) into LDS while its completion count is in flight, so the last block
+  // can issue the optimised tensors' loads with its first loads
+  __shared__ mi_elbo_adam sad;
   const bool has_adam = !ABSORB && adam != nullptr;
+  if (has_adam) {
+    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
+    static_assert(kWords <= kElboThreads, "one descriptor word per thread");
+    if ((int)threadIdx.x < kWords)
+      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
+          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    // The shares (and the slot gradients the tail reads) are device-coherent stores, complete
+    // (s_waitcnt) before the barrier / the counter update: no per-block L2 write-back fence,
+    // which serialises over a few hundred reducing blocks.
+    __hip_atomic_store(&work[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MI_ELBO_RELEASE_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_s_waitcnt(0);
+    const int group = (int)blockIdx.x / kGroupBlocks;
+    // (one level up to kSingleCount blocks: their arrivals at one address cost less than the
+    // second level's round trip)
+    const int ngroups = nshare <= kSingleCount ? 1 : (nshare + kGroupBlocks - 1) / kGroupBlocks;
+    const unsigned in_group = (unsigned)min(kGroupBlocks, nshare - group * kGroupBlocks);
+    unsigned* gc = counters + kGroupCounterWord + group * kGroupCounterStride;
+    bool done = true;
+    if (ngroups > 1) {
+      done = atomicAdd(gc, 1u) == in_group - 1u;
+      if (done) *gc = 0u;   // reset for the next launch (no other block of the group is left)
+    }
+    last = done && atomicAdd(counters, 1u) == (unsigned)(ngroups > 1 ? ngroups : nshare) - 1u;
+  }
+  MI_ELBO_STAMP(3);
+  __syncthreads();
+  if (!last) {
+    MI_ELBO_FLUSH();
+    return;
+  }
   // the last block adds the shares: each thread a fixed strided subset, then a fixed-order block
   // sum -- deterministic, and no serial chain of dependent loads. Every load of this phase (shares,
   // the tails' partials and concentrations, the validation words, the generator step) is issued
   // before the first sum: one memory round trip instead of one per stage.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   MI_ELBO_STAMP(10);
   // the optimised tensors' elements this thread updates (element threadIdx.x of every slot) and
   // their moments: loaded now, used when the gradient is written below. Lane q computes slot q's
@@ -1186,254 +1388,8 @@ MI_DEV void elbo_finish(const mi_elbo& E, const AbsorbPlan& P, const ReducePlan&
   // (lane q alone read slot q's count; a fused-draw factor's last reader advances its own)
   if (has_adam && (int)threadIdx.x < sad.num && !fin_factor(P, sad.slots[threadIdx.x].factor))
     *sad.slots[threadIdx.x].step = sstep1[threadIdx.x];
-}
-
-// ---- forward --------------------------------------------------------------------------------
-// HAS_BETA = false: only Normal factors (log of the scale), which keeps the register footprint
-// of the common large-factor case small; true: any Beta or Gamma factor (generic entropy path).
-// ABSORB: the launch has forward-absorbed Beta blocks (absorbed_block<true>, inline fp64 implicit
-// gradients: a large register footprint the other variants do not pay for).
-// SPLIT: the blocks store their shares and end; k_elbo_tail finishes (see there).
-template <bool HAS_BETA, bool ABSORB, bool SPLIT = false>
-__global__ __launch_bounds__(kElboThreads) void k_elbo_forward(const mi_elbo E,
-                                                               const AbsorbPlan P,
-                                                               const ReducePlan R,
-                                                               double* __restrict__ work,
-                                                               unsigned* __restrict__ counters,
-                                                               float* __restrict__ loss,
-                                                               const mi_elbo_adam* __restrict__ adam) {
-  __shared__ double red[kElboThreads][2];
-  __shared__ bool last;
-#if MI_ELBO_TIMING
-  if (threadIdx.x < 16) mi_ets[threadIdx.x] = 0;
-#endif
-  MI_ELBO_STAMP(0);
-  kernarg_prefetch<(int)(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan))>();
-  const int nred = R.first[R.num];
-  const int nloss = P.lead_blocks;
-  const int nshare = nred + nloss;   // blocks that write a loss share
-  if (ABSORB && (int)blockIdx.x >= nshare) {
-    absorbed_block<true>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
-    return;
-  }
-  if (!ABSORB && (int)blockIdx.x >= nshare) {
-    // MI_ELBO_FINAL_GRADS: the gradients of the fused-draw factors (MI_DRAW_PARTIALS) for an
-    // upstream of 1 -- k_elbo_backward's absorbed blocks, run here (P: their plan); they read only
-    // the site launches' partial rows, so they run beside the reductions
-    absorbed_block<false>(E, P, (int)blockIdx.x - nshare, 1.0f, counters, work, red, &last);
-    return;
-  }
-  if (!ABSORB && blockIdx.x == 0 && (R.tails > 0 || adam != nullptr))
-    early_tail(E, R, P, adam, work);
-  double* rsum = &red[0][0];
-  double share;
-  double c[kMaxTails][2] = {};   // this lane's tail contributions
-  double nt[2] = {0.0, 0.0};     // this lane's Normal-tail sums (R.nt_job), element nt_slot
-  int nt_slot = -1, nt_kb = 0;
-  if (!ABSORB && (int)blockIdx.x < nred) {   // (ABSORB launches have no deferred reductions)
-    share = reduce_block(E, R, (int)blockIdx.x, c, red, nt, nt_slot, nt_kb);
-    __syncthreads();
-  } else {
-    const int64_t lead = (int64_t)blockIdx.x - nred;
-    const int64_t stride = (int64_t)nloss * kElboThreads;
-    const int64_t first = lead * kElboThreads + threadIdx.x;
-    double lp = 0.0, h = 0.0;
-    for (int t = 0; t < E.num_terms; ++t)
-      for (int64_t k = first; k < E.K; k += stride) lp += (double)E.terms[t][k];
-    if (R.external) {
-#pragma unroll
-      for (int a = 0; a < MI_MAX_REDUCE; ++a)
-        if (a < R.num)
-          for (int64_t k = first; k < E.K; k += stride) lp += (double)E.reduce[a].total[k];
-    }
-    for (int f = 0; f < E.num_factors; ++f) {
-      const mi_factor& F = E.factors[f];
-      if (!HAS_BETA || F.family == MI_NORMAL) {
-        // sum_i (0.5 + 0.5 log(2 pi) + log scale_i): the constant once, the logs per element
-        const float* __restrict__ sc = F.param[1];
-        const int64_t ss = F.stride[1];
-        float hf = 0.0f;   // per-thread partial of a few terms, then fp64
-        int64_t head = 0;
-        if (ss == 1 && (reinterpret_cast<uintptr_t>(sc) & 15) == 0) {
-          // 16-byte loads, all issued before the logs
-          const int64_t nq = F.n >> 2;
-          const float4* __restrict__ sq = reinterpret_cast<const float4*>(sc);
-          int64_t q = first;
-          // eight quads' loads in flight per round, then four (a lead block covers ~32 elements
-          // per lane: one memory round trip, not two); quads summed in order either way
-          for (; q + 7 * stride < nq; q += 8 * stride) {
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = sq[q + u * stride];
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
-          }
-          for (; q + 3 * stride < nq; q += 4 * stride) {
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = sq[q + u * stride];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              hf += (logf(v[u].x) + logf(v[u].y)) + (logf(v[u].z) + logf(v[u].w));
-          }
-          for (; q < nq; q += stride) {
-            const float4 v = sq[q];
-            hf += (logf(v.x) + logf(v.y)) + (logf(v.z) + logf(v.w));
-          }
-          head = nq << 2;
-        }
-        for (int64_t i = head + first; i < F.n; i += stride) hf += logf(sc[i * ss]);
-        double hn = (double)hf;
-        if (first == 0) hn += 1.4189385332046727 * (double)F.n;
-        h += F.weight * hn;
-      } else {
-        double hb = 0.0;
-        for (int64_t i = first; i < F.n; i += stride) hb += factor_entropy(F, i);
-        h += F.weight * hb;
-      }
-    }
-    share = (double)E.g0 * lp - E.entropy_scale * h;
-    if (!ABSORB) {   // tail sources written by earlier launches
-#pragma unroll
-      for (int q = 0; q < kMaxTails; ++q) {
-        const int mask = q < R.tails ? R.tail_ext[q] : 0;
-        if (mask == 0) continue;
-        // every source slot and the factor read unconditionally (an unused slot reads the first
-        // used one and adds +0): one memory round trip instead of one per load
-        const int on0 = __builtin_ctz((unsigned)mask);
-        for (int64_t k = first; k < E.K; k += stride) {
-          float g = 0.0f;
-#pragma unroll
-          for (int src = 0; src < MI_MAX_SOURCES; ++src) {
-            const bool on = (mask >> src) & 1;
-            const int sc = on ? src : on0;
-            g += keep_if(R.tail_src[q][sc][k * R.tail_src_stride[q][sc]], on);
-          }
-          const double2 d = *reinterpret_cast<const double2*>(R.tail_dgrad[q] + 2 * k);
-          if (g == 0.0f) continue;   // a zero upstream never meets the factor
-          c[q][0] += (double)g * d.x;
-          c[q][1] += (double)g * d.y;
-        }
-      }
-    }
-  }
-  MI_ELBO_STAMP(1);
-  // the block's share and its tail partials in one pass: wave sums, then the waves in order
-  // through LDS, one barrier (thread 0 stores the tail partials and returns the share)
-  double s;
-  {
-    constexpr int kWaves = kElboThreads / kWave;
-    constexpr int kVals = 1 + 2 * kMaxTails;
-    __shared__ double wsum[kVals][kWaves];
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-    const double v0 = wave_sum(share);
-    if (lane == 0) wsum[0][wave] = v0;
-    const int tails = ABSORB ? 0 : R.tails;
-    // the Normal tail's sums live on the particle lanes (the first kRedK <= 64 threads: wave 0)
-    double nts0 = 0.0, nts1 = 0.0;
-    if (!ABSORB && nt_slot >= 0 && wave == 0) {
-      nts0 = wave_sum(nt[0]);
-      nts1 = wave_sum(nt[1]);
-    }
-#pragma unroll
-    for (int t = 0; t < kMaxTails; ++t)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (t < tails) {
-          const double v = wave_sum(c[t][q]);
-          if (lane == 0) wsum[1 + 2 * t + q][wave] = v;
-        }
-    __syncthreads();
-    s = 0.0;
-    if (threadIdx.x == 0) {
-      for (int w = 0; w < kWaves; ++w) s += wsum[0][w];
-      for (int t = 0; t < tails; ++t)
-        for (int q = 0; q < 2; ++q) {
-          double v = 0.0;
-          for (int w = 0; w < kWaves; ++w) v += wsum[1 + 2 * t + q][w];
-          __hip_atomic_store(&work[R.tail_part + ((int64_t)t * nshare + blockIdx.x) * 2 + q], v,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      if (!ABSORB && nt_slot >= 0) {
-        double* w2 = &work[R.nt_part + ((int64_t)nt_slot * R.nt_nkb + nt_kb) * 2];
-        __hip_atomic_store(w2, nts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(w2 + 1, nts1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  MI_ELBO_STAMP(2);
-  // mi_elbo_forward_adam: every share-writing block fetches the optimizer's descriptor (240 B, an
-  // L2 hit after the first) into LDS while its completion count is in flight, so the last block
-  // can issue the optimised tensors' loads with its first loads
-  if (SPLIT) {   // the finish is k_elbo_tail's, after the kernel boundary: a plain store
-    if (threadIdx.x == 0) work[blockIdx.x] = s;
-    MI_ELBO_FLUSH();
-    return;
-  }
-  __shared__ mi_elbo_adam sad;
-  const bool has_adam = !ABSORB && adam != nullptr;
-  if (has_adam) {
-    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
-    static_assert(kWords <= kElboThreads, "one descriptor word per thread");
-    if ((int)threadIdx.x < kWords)
-      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
-          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
-  }
-  if (threadIdx.x == 0) {
-    // The shares (and the slot gradients the tail reads) are device-coherent stores, complete
-    // (s_waitcnt) before the barrier / the counter update: no per-block L2 write-back fence,
-    // which serialises over a few hundred reducing blocks.
-    __hip_atomic_store(&work[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (MI_ELBO_RELEASE_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_s_waitcnt(0);
-    const int group = (int)blockIdx.x / kGroupBlocks;
-    // (one level up to kSingleCount blocks: their arrivals at one address cost less than the
-    // second level's round trip)
-    const int ngroups = nshare <= kSingleCount ? 1 : (nshare + kGroupBlocks - 1) / kGroupBlocks;
-    const unsigned in_group = (unsigned)min(kGroupBlocks, nshare - group * kGroupBlocks);
-    unsigned* gc = counters + kGroupCounterWord + group * kGroupCounterStride;
-    bool done = true;
-    if (ngroups > 1) {
-      done = atomicAdd(gc, 1u) == in_group - 1u;
-      if (done) *gc = 0u;   // reset for the next launch (no other block of the group is left)
-    }
-    last = done && atomicAdd(counters, 1u) == (unsigned)(ngroups > 1 ? ngroups : nshare) - 1u;
-  }
-  MI_ELBO_STAMP(3);
-  __syncthreads();
-  if (!last) {
-    MI_ELBO_FLUSH();
-    return;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  elbo_finish<ABSORB>(E, P, R, work, counters, loss, adam, sad, rsum, nshare);
   MI_ELBO_STAMP(5);
   MI_ELBO_FLUSH();
-}
-
-// The finish as its own one-workgroup launch (SPLIT forward): the share-writing blocks only store
-// their shares; after the kernel boundary this block reads them (plain loads: the boundary makes
-// the stores visible), with no completion count and no device-scope fence -- a 255 -> 1 fan-in on
-// one counter costs 3.2-4.5 us on MI355X (MI355X_MICROARCH.md "fanin"), a dependent boundary ~1.5.
-__global__ __launch_bounds__(kElboThreads) void k_elbo_tail(const mi_elbo E, const AbsorbPlan P,
-                                                            const ReducePlan R,
-                                                            double* __restrict__ work,
-                                                            unsigned* __restrict__ counters,
-                                                            float* __restrict__ loss,
-                                                            const mi_elbo_adam* __restrict__ adam) {
-  __shared__ double red[kElboThreads][2];
-  __shared__ mi_elbo_adam sad;
-  kernarg_prefetch<(int)(sizeof(mi_elbo) + sizeof(AbsorbPlan) + sizeof(ReducePlan))>();
-  if (adam != nullptr) {
-    constexpr int kWords = (int)(sizeof(mi_elbo_adam) / sizeof(uint32_t));
-    if ((int)threadIdx.x < kWords)
-      reinterpret_cast<uint32_t*>(&sad)[threadIdx.x] =
-          reinterpret_cast<const uint32_t*>(adam)[threadIdx.x];
-  }
-  __syncthreads();
-  elbo_finish<false>(E, P, R, work, counters, loss, adam, sad, &red[0][0],
-                     R.first[R.num] + P.lead_blocks);
 }
 
 // ---- backward -------------------------------------------------------------------------------
@@ -1941,34 +1897,16 @@ int mi_elbo_forward_adam(const mi_elbo* elbo, void* workspace, size_t workspace_
   }
 #endif
   const dim3 block(mi::kElboThreads);
-  // split finish (k_elbo_tail after the share-writing launch; launches without forward-absorbed
-  // Beta blocks): MININF_AMD_ELBO_SPLIT (round-6 A/B)
-  static const bool split = [] {
-    const char* v = std::getenv("MININF_AMD_ELBO_SPLIT");
-    return v != nullptr && std::atoi(v) != 0;
-  }();
   if (L.fwd.num > 0)
     hipLaunchKernelGGL((mi::k_elbo_forward<true, true>), grid, block, 0, s, *elbo, L.fwd, L.red,
                        work, counters, loss, nullptr);
-  else if (has_beta && split)
-    hipLaunchKernelGGL((mi::k_elbo_forward<true, false, true>), grid, block, 0, s, *elbo, plan,
-                       L.red, work, counters, loss, adam);
   else if (has_beta)
     hipLaunchKernelGGL((mi::k_elbo_forward<true, false>), grid, block, 0, s, *elbo, plan, L.red,
                        work, counters, loss, adam);
-  else if (split)
-    hipLaunchKernelGGL((mi::k_elbo_forward<false, false, true>), grid, block, 0, s, *elbo, plan,
-                       L.red, work, counters, loss, adam);
   else
     hipLaunchKernelGGL((mi::k_elbo_forward<false, false>), grid, block, 0, s, *elbo, plan,
                        L.red, work, counters, loss, adam);
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess && split && L.fwd.num == 0) {
-    hipLaunchKernelGGL(mi::k_elbo_tail, dim3(1), block, 0, s, *elbo, plan, L.red, work, counters,
-                       loss, adam);
-    e = hipGetLastError();
-  }
-  return to_code(e);
+  return to_code(hipGetLastError());
 }
 
 int mi_elbo_backward(const mi_elbo* elbo, const float* upstream, float* dterm, void* workspace,

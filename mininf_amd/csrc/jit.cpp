@@ -112,17 +112,14 @@ std::string mask_kind_tag(const mi_site& st) {
   return std::to_string((int)kind_of(st.mask_stride_k, st.mask_stride_i));
 }
 
-// Fused-draw row loop shape (round 6 A/B; read per compile, part of the signature):
-//   pairs: two particles per iteration as two independent Philox -> Box-Muller -> density chains
-//   (accumulator form only), tile rows of the per-wave particle-sum LDS tile, and an explicit
-//   waves-per-EU occupancy target for the program (0: the compiler's choice).
-int env_int(const char* name, int fallback) {
-  const char* v = std::getenv(name);
-  return v != nullptr && *v != 0 ? std::atoi(v) : fallback;
+// MININF_AMD_DRAW_PAIRS=1: the fused-draw accumulator loop takes two particles per iteration as
+// two independent Philox -> Box-Muller -> density chains (opt-in: measured slower on MI355X, round
+// 6 -- C5's program 153.4-154.0 us against 151.7-152.5 with one chain, profiles/r06_c5_ab.json).
+// Read per compile; part of the signature.
+bool draw_pairs() {
+  const char* v = std::getenv("MININF_AMD_DRAW_PAIRS");
+  return v != nullptr && std::atoi(v) != 0;
 }
-bool draw_pairs() { return env_int("MININF_AMD_DRAW_PAIRS", 1) != 0; }
-int draw_tile_rows(int nv) { return env_int("MININF_AMD_TILE_ROWS", nv <= 2 ? 16 : 8); }
-int draw_waves_per_eu() { return env_int("MININF_AMD_WAVES_PER_EU", 0); }
 
 Signature signature(const mi_group& g, const PlanInfo& plan) {
   std::ostringstream s;
@@ -147,9 +144,7 @@ Signature signature(const mi_group& g, const PlanInfo& plan) {
     << (g.draw.scale_exp != nullptr ? "x" : "")
     << (g.prior.present != 0 ? "|prior" + std::to_string(g.prior.family) : "")
     << (g.pdraw.operand != 0 ? "|pdraw" + std::to_string(g.pdraw.operand) : "");
-  if (g.draw.operand != 0)
-    s << "|pairs" << draw_pairs() << "|t" << draw_tile_rows(g.num_sites + g.num_slots) << "|w"
-      << draw_waves_per_eu();
+  if (g.draw.operand != 0) s << "|pairs" << draw_pairs();
   return Signature{s.str()};
 }
 
@@ -334,9 +329,6 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   const int draw = g.draw.operand - 1;
   o << "#include \"device_math.hpp\"\n";
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
-  if (row && draw >= 0 && draw_waves_per_eu() > 0)
-    o << "__attribute__((amdgpu_waves_per_eu(" << draw_waves_per_eu() << ", "
-      << draw_waves_per_eu() << "))) ";
   o << "void mi_site_program(const mi_group G, "
        "float* __restrict__ part, long nseg, long arg, unsigned* __restrict__ flags) {\n";
   // the descriptor's lines into L2 with one vector load (device_math.hpp kernarg_prefetch): the
@@ -347,7 +339,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
   o << "  const long seg = (long)blockIdx.x * 4 + (threadIdx.x >> 6);\n";
   o << "  const long K = G.K, N = G.N;\n";
   // LDS of the row loops' particle sums: nv tiles of [tile_rows][65] floats per wave
-  const int tile_rows = (row && draw >= 0) ? draw_tile_rows(nv) : (nv <= 2 ? 16 : 8);
+  const int tile_rows = nv <= 2 ? 16 : 8;
   if (row)
     o << "  __shared__ float red[" << 4 * nv * tile_rows * 65 << "];\n"
       << "  float* const tile = red + (threadIdx.x >> 6) * " << nv * tile_rows * 65 << ";\n";
@@ -839,16 +831,18 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
     if (pairs) {
       for (int op = 0; op < g.num_operands; ++op)
         if (is(op, kParticle) && op != pdraw)
-          o << in << "float pm" << op << " = k_begin + 1 < k_end ? x" << op << "[(k_begin + 1) * sk"
+          o << in << "float pnn" << op << " = k_begin + 1 < k_end ? x" << op << "[(k_begin + 1) * sk"
             << op << "] : pn" << op << ";\n";
       o << in << "for (long k0 = k_begin; k0 < k_end; k0 += 2) {\n";
       o << in << "  const bool two = k0 + 1 < k_end;\n";
       o << in << "  const int r0 = (int)((k0 - k_begin) & " << tile_rows - 1 << ");\n";
       for (int op = 0; op < g.num_operands; ++op)
         if (is(op, kParticle) && op != pdraw) {
-          o << in << "  const float pa" << op << " = pn" << op << ", pb" << op << " = pm" << op << ";\n";
+          // (pka / pkb: "pb<s>" names the sites' parameter flags)
+          o << in << "  const float pka" << op << " = pn" << op << ", pkb" << op << " = pnn" << op
+            << ";\n";
           o << in << "  if (k0 + 2 < k_end) { pn" << op << " = x" << op << "[(k0 + 2) * sk" << op
-            << "]; pm" << op << " = x" << op << "[min(k0 + 3, k_end - 1) * sk" << op << "]; }\n";
+            << "]; pnn" << op << " = x" << op << "[min(k0 + 3, k_end - 1) * sk" << op << "]; }\n";
         }
       for (int v = 0; v < nv; ++v) o << in << "  float va" << v << ", vb" << v << ";\n";
     } else {
@@ -887,7 +881,7 @@ std::string generate(const mi_group& g, const PlanInfo& plan) {
       if (is(op, kParticle) && op == pdraw)
         o << in << "  const float p" << op << " = pdv[k - k_begin];\n";
       else if (is(op, kParticle) && pairs)
-        o << in << "  const float p" << op << " = " << (copy == 0 ? "pa" : "pb") << op << ";\n";
+        o << in << "  const float p" << op << " = " << (copy == 0 ? "pka" : "pkb") << op << ";\n";
       else if (is(op, kParticle))
         o << in << "  const float p" << op << " = pn" << op << ";\n" << in << "  if (k + 1 < k_end) pn"
           << op << " = x" << op << "[(k + 1) * sk" << op << "];\n";

@@ -761,18 +761,9 @@ struct MfVariant {
   bool flush64;
   int minw;
 };
-constexpr MfVariant kMfVariants[] = {{256, false, 4}, {256, false, 2}, {256, false, 3}};
+constexpr MfVariant kMfVariants[] = {{256, false, 4}, {256, false, 2}};
 
-int mf_variant(int pt) {
-  // MININF_AMD_LINEAR_MINW=3: one feature tile at 3 waves/SIMD (round-6 A/B: the 4-wave launch
-  // spills 16 registers)
-  static const int minw = [] {
-    const char* v = std::getenv("MININF_AMD_LINEAR_MINW");
-    return v != nullptr ? std::atoi(v) : 0;
-  }();
-  if (pt == 1 && minw == 3) return 2;
-  return pt == 1 ? 0 : 1;
-}
+int mf_variant(int pt) { return pt == 1 ? 0 : 1; }
 
 Geometry geometry(const mi_linear* L) {
   Geometry g{};
@@ -867,8 +858,6 @@ void launch_mfma_variant(const mi_linear& L, const Geometry& g, float* part, uin
                          hipStream_t s) {
   if (g.variant == 0)
     launch_mfma<FAMILY, PT, 256, false, 4>(L, g, part, flags, s);
-  else if (g.variant == 2)
-    launch_mfma<FAMILY, PT, 256, false, 3>(L, g, part, flags, s);
   else
     launch_mfma<FAMILY, PT, 256, false, 2>(L, g, part, flags, s);
 }
