@@ -298,8 +298,13 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
-  __shared__ __attribute__((aligned(16))) float xs[S::CH * S::RSTR];
-  __shared__ float2 yms[S::CH];
+  // Multi-stage launches stage X through two LDS buffers: stage st + 1 is stored into the other
+  // buffer right after stage st's tiles, so one barrier per stage separates the two (a single
+  // buffer needed a barrier before its store and one after it).
+  constexpr int kBufs = ONESTAGE ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) float xs[kBufs * S::CH * S::RSTR];
+  __shared__ float2 yms[kBufs * S::CH];
+  int cur = 0;   // the buffer the tiles read
   // rows drawn here (mi_linear.rows, ONESTAGE launches only): the stage's dataset rows
   __shared__ int32_t grows[ONESTAGE ? S::CH : 1];
   const bool gen_rows = ONESTAGE && L.rows.counter != nullptr;
@@ -402,16 +407,16 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       ymr = make_float2(m != 0.0f ? y : 0.0f, m);
     }
   };
-  auto store_stage = [&]() {
+  auto store_stage = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < S::QPT; ++q) {
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
-      float* dst = xs + row * S::RSTR + 2 * c4;
+      float* dst = xs + buf * (S::CH * S::RSTR) + row * S::RSTR + 2 * c4;
       *reinterpret_cast<float2*>(dst) = make_float2(xq[q].x, xq[q].z);           // even features
       *reinterpret_cast<float2*>(dst + S::HS) = make_float2(xq[q].y, xq[q].w);   // odd features
     }
-    if (tid < S::CH) yms[tid] = ymr;
+    if (tid < S::CH) yms[buf * S::CH + tid] = ymr;
   };
 
   // The block's particles' draws through the (still unused) X staging buffer into thf: called by
@@ -439,7 +444,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   // MU = X theta^T for the tile's 32 rows and this wave's 32 particles
   auto gemm1 = [&](int tile) -> f32x16 {
     f32x16 mu = f32x16{};
-    const float* xa = xs + (tile * 32 + c) * S::RSTR + h * S::HS;
+    const float* xa = xs + cur * (S::CH * S::RSTR) + (tile * 32 + c) * S::RSTR + h * S::HS;
 #pragma unroll
     for (int s = 0; s < S::HS; s += 4) {
       const float4 a = *reinterpret_cast<const float4*>(xa + s);
@@ -457,7 +462,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float2 ym = yms[row];
+      const float2 ym = yms[cur * S::CH + row];
       const float loc = mu[r];
       fl |= (loc != loc) ? MI_FLAG_PARAM : 0u;
       if (FAMILY == MI_NORMAL) {
@@ -479,7 +484,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int p = 32 * t + c;
-      const float* xb = xs + (p & 1) * S::HS + (p >> 1);
+      const float* xb = xs + cur * (S::CH * S::RSTR) + (p & 1) * S::HS + (p >> 1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -493,13 +498,28 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       // this batch's rows of the block's stage, from the batch number every block reads before
       // the last one to finish advances it (below). (Issuing the draw's parameter loads before
       // or right after this read measured no faster: tools/linear_timing.py, round 4.)
+      // Both halves of the rows computed one batch ahead (mi_rows.next) are loaded with the
+      // counter -- no load waits on another -- and a row tagged for this batch is taken as is; the
+      // permutation runs only when neither tag matches (the loader's first batch).
+      const int64_t row = st0 * S::CH + tid;
+      const bool mine = tid < S::CH && st0 < st1 && row < N;
+      const int64_t rc = mine ? row : 0;
+      const bool ahead = L.rows.next != nullptr;
+      const uint64_t n0 = ahead ? L.rows.next[rc] : 0ull;
+      const uint64_t n1 = ahead ? L.rows.next[L.rows.batch + rc] : 0ull;
       batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tid < S::CH && st0 < st1) {
-        const int64_t row = st0 * S::CH + tid;
         int32_t r = 0;
-        if (row < N) {
-          const BatchOrder order = batch_order(batch_no, L.rows.batches, L.rows.seed);
-          r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
+        if (mine) {
+          const uint32_t tag = (uint32_t)(batch_no + 1);
+          if ((uint32_t)(n0 >> 32) == tag) {
+            r = (int32_t)(uint32_t)n0;
+          } else if ((uint32_t)(n1 >> 32) == tag) {
+            r = (int32_t)(uint32_t)n1;
+          } else {
+            const BatchOrder order = batch_order(batch_no, L.rows.batches, L.rows.seed);
+            r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
+          }
           if (L.rows.out != nullptr && group == 0) L.rows.out[row] = r;
         }
         grows[tid] = r;
@@ -509,8 +529,19 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     MI_LIN_STAMP(1);
     if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
+    if (gen_rows && L.rows.next != nullptr && group == 0 && tid < S::CH && st0 < st1) {
+      // the next batch's row, while this stage's gathers are in flight (mi_rows.next)
+      const int64_t row = st0 * S::CH + tid;
+      if (row < N) {
+        const uint64_t b1 = batch_no + 1;
+        const BatchOrder order = batch_order(b1, L.rows.batches, L.rows.seed);
+        const int32_t r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
+        L.rows.next[(int64_t)(b1 & 1) * L.rows.batch + row] =
+            ((uint64_t)(uint32_t)(b1 + 1) << 32) | (uint64_t)(uint32_t)r;
+      }
+    }
     if (drawn) draw_here();
-    if (st0 < st1) store_stage();
+    if (st0 < st1) store_stage(0);
     MI_LIN_STAMP(2);
     __syncthreads();
     MI_LIN_STAMP(3);
@@ -539,9 +570,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   if (!ONESTAGE && drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
   if (!ONESTAGE && st0 < st1) load_stage(st0);
   if (!ONESTAGE && drawn) draw_here();
-  if (!ONESTAGE && st0 < st1) store_stage();
+  if (!ONESTAGE && st0 < st1) store_stage(0);
   if (!ONESTAGE) __syncthreads();
   for (int64_t st = st0; !ONESTAGE && st < st1; ++st) {
+    cur = (int)((st - st0) & 1);
     if (st + 1 < st1) load_stage(st + 1);   // in flight during this stage's MFMAs
     // Software pipeline over this wave's tiles: the first product of tile j + 1 is issued before
     // the elementwise step of tile j, so its MFMAs run while the VALU evaluates the densities.
@@ -567,11 +599,10 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
         acc2[t] = f32x16{};
       }
     }
+    // the next stage into the other buffer (no wave reads it: every wave finished the previous
+    // stage at the last barrier), then one barrier before its tiles
+    if (st + 1 < st1) store_stage(cur ^ 1);
     __syncthreads();
-    if (st + 1 < st1) {
-      store_stage();
-      __syncthreads();
-    }
   }
 
   // ---- partials --------------------------------------------------------------------------------

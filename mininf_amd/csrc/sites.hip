@@ -586,11 +586,14 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // SUFF (MININF_AMD_BCAST_SUFFSTAT=1, a measurement of the floor, not the default): the
 // per-(particle, element) FMA loop replaced by its closed form l_k * sum_i x_i -- the same value
 // in exact arithmetic (C2's per-eval arithmetic is reducible).
-template <int FAMILY, int kSmemP, int kSmemChunk, bool SUFF = false>
+// chunk: elements per chunk, a multiple of 32 and at most kSmemMaxChunk (the host sizes it so that
+// chunks x particle blocks fill the chip's workgroup slots: make_plan).
+constexpr int kSmemMaxChunk = 4096;
+template <int FAMILY, int kSmemP, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
-                                                                   int mode,
+                                                                   int mode, int chunk,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
   kernarg_prefetch<(int)sizeof(mi_group)>();
@@ -610,8 +613,8 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const unsigned long long t0 = span_begin(G.stamps);
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
-  const int64_t i0 = c * kSmemChunk;
-  const int len = (int)min((int64_t)kSmemChunk, G.N - i0);
+  const int64_t i0 = c * chunk;
+  const int len = (int)min((int64_t)chunk, G.N - i0);
   uint32_t fl = 0u;
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
@@ -694,6 +697,30 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       flush(in);
     }
   }
+  if (!SUFF && j + kGroup <= len) {   // whole groups of 32 past the last whole block
+    f32x2 in[2][kSmemP];
+#pragma unroll
+    for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
+    float xc[kGroup];
+#pragma unroll
+    for (int e = 0; e < kGroup; ++e) xc[e] = xs[j + e];
+    for (; j + kGroup <= len; j += kGroup) {
+      const int nxt = min(j + kGroup, len - kGroup);   // in bounds; the last is unused
+      float xn[kGroup];
+#pragma unroll
+      for (int e = 0; e < kGroup; ++e) xn[e] = xs[nxt + e];
+#pragma unroll
+      for (int e = 0; e < kGroup; e += 2) {
+        const f32x2 xv = f32x2{xc[e], xc[e + 1]};
+#pragma unroll
+        for (int p = 0; p < kSmemP; ++p)
+          in[(e >> 1) & 1][p] = __builtin_elementwise_fma(xv, ld[p], in[(e >> 1) & 1][p]);
+      }
+#pragma unroll
+      for (int e = 0; e < kGroup; ++e) xc[e] = xn[e];
+    }
+    flush(in);
+  }
   if (!SUFF && j < len) {   // the chunk's tail: element pairs, a zero for an odd last element
     f32x2 in[2][kSmemP];
 #pragma unroll
@@ -708,10 +735,10 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   }
 
   // ---- chunk sum and support flags (vector loads, L2-resident by now) --------------------------
-  // Each lane takes kSmemChunk / kBcastThreads consecutive elements with all its loads in flight
-  // at once (a strided loop waits for one L2 round trip per element group, at the end of every
-  // wave).
-  constexpr int kPerLane = kSmemChunk / kBcastThreads;
+  // Each lane takes kSmemMaxChunk / kBcastThreads consecutive elements (those within the chunk)
+  // with all its loads in flight at once (a strided loop waits for one L2 round trip per element
+  // group, at the end of every wave).
+  constexpr int kPerLane = kSmemMaxChunk / kBcastThreads;
   static_assert(kPerLane % 4 == 0, "whole float4 groups per lane");
   float s_a = 0.0f;
   {
@@ -1118,7 +1145,21 @@ bool bcast_smem(const mi_group* g) {
 // k_site_bcast_smem: particles per lane and chunk length (measured r02: the best of {4, 8} x
 // {2048, 4096, 8192})
 constexpr int kSmemP = 4;
-constexpr int kSmemChunk = 4096;
+// Chunks of at most 4096 elements (measured r02: 4096 against 2048 / 8192), sized so that chunks x
+// particle blocks come close to kSmemSlots workgroups: four 4-wave workgroups per CU on 256 CUs, one
+// round. (r05 used 4096-element chunks throughout: C2's 245 chunks x 4 particle blocks left 44 of
+// the 1024 slots idle.)
+constexpr int64_t kSmemSlots = 1024;
+
+// Grids of 4096-element chunks between half a round and one round of slots are evened out to one
+// round; smaller grids keep 4096 (shorter chunks would only add partials for the reduction).
+int smem_chunk(int64_t N, int64_t gy) {
+  gy = std::max<int64_t>(1, gy);
+  const int64_t blocks = ceil_div(N, mi::kSmemMaxChunk) * gy;
+  if (blocks < kSmemSlots / 2 || blocks > kSmemSlots) return mi::kSmemMaxChunk;
+  const int64_t chunk = (ceil_div(N, kSmemSlots / gy) + 31) / 32 * 32;
+  return (int)std::min<int64_t>(mi::kSmemMaxChunk, std::max<int64_t>(2048, chunk));
+}
 
 struct Plan {
   Shape shape;
@@ -1128,6 +1169,7 @@ struct Plan {
   int64_t rows_per_block;  // ROW
   int64_t seg_len;         // COL
   int kw;                  // COL
+  int chunk = 0;           // BCAST (k_site_bcast_smem): elements per chunk
   dim3 grid;
 };
 
@@ -1138,7 +1180,8 @@ Plan make_plan(const mi_group* g) {
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     const bool smem = bcast_smem(g);
-    const int64_t chunks = ceil_div(g->N, smem ? kSmemChunk : mi::kBcastChunk);
+    if (smem) p.chunk = smem_chunk(g->N, ceil_div(g->K, mi::kBcastThreads * kSmemP));
+    const int64_t chunks = ceil_div(g->N, smem ? p.chunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
     const int64_t side = (smem && g->side.out != nullptr)
                              ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
@@ -1246,11 +1289,11 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   // MININF_AMD_BCAST_SUFFSTAT=1: the reducible-floor measurement of bench.py (sum_i x_i l_k as
   // l_k sum_i x_i), never the default
   if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
-    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, kSmemChunk, true>), grid, block, 0, s,
-                       G, part, p.nseg, gy, rank1, flags);
+    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, true>), grid, block, 0, s,
+                       G, part, p.nseg, gy, rank1, p.chunk, flags);
   else
-    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, kSmemChunk>), grid, block, 0, s, G,
-                       part, p.nseg, gy, rank1, flags);
+    hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP>), grid, block, 0, s, G,
+                       part, p.nseg, gy, rank1, p.chunk, flags);
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {
