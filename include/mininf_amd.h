@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MI_ABI_VERSION 19
+#define MI_ABI_VERSION 18
 
 #define MI_MAX_SITES 4
 #define MI_MAX_OPERANDS 6
@@ -489,12 +489,6 @@ int mi_philox4x32(const uint32_t* ctr, int64_t count, uint32_t key0, uint32_t ke
  * mi_minibatch_rows's meaning; the kernel reads the batch number counter[0], draws its rows, writes
  * them to `out` (when non-NULL, for later readers of the batch) and advances counter[0] once all
  * of its blocks have read it (counter[1]: completion count, zero between launches).
- * next (optional, 2 * batch words, zeroed once, owned by the loader): rows computed one batch
- * ahead -- while its gathers are in flight, the launch for batch b writes the rows of batch b + 1
- * as (tag b + 2) << 32 | row into half (b + 1) & 1, and the launch for batch b takes a row whose
- * tag is b + 1 from either half (both read together with the counter) instead of running the
- * permutation on its critical path; any other tag (the first batch, a counter moved by
- * mi_minibatch_rows) falls back to the permutation.
  * DataLoader(TensorDataset(X, y), batch_size, shuffle=True) of examples/minibatch.md:78. */
 typedef struct mi_rows {
   uint64_t* counter;      /* NULL: no rows drawn here */
@@ -505,7 +499,6 @@ typedef struct mi_rows {
   int32_t shuffle;
   int32_t pad0;
   int32_t* out;
-  uint64_t* next;         /* NULL: no rows carried to the next batch */
 } mi_rows;
 
 typedef struct mi_linear {

@@ -40,7 +40,7 @@ MAX_REDUCE = 4
 REDUCE_MAX_SEG = 1024
 ELBO_COUNTER_BYTES = 16640
 ELBO_FINAL_GRADS = 1   # MI_ELBO_FINAL_GRADS
-ABI_VERSION = 19   # MI_ABI_VERSION of include/mininf_amd.h
+ABI_VERSION = 18   # MI_ABI_VERSION of include/mininf_amd.h
 FLAG_SUPPORT, FLAG_PARAM, FLAG_INTERNAL = 1, 2, 0x40000000
 MI_EINVAL, MI_EWORKSPACE, MI_EUNSUPPORTED = -1, -2, -3
 
@@ -100,7 +100,7 @@ class Group(ctypes.Structure):
 class Rows(ctypes.Structure):
     _fields_ = [("counter", c_vp), ("n", c_i64), ("batch", c_i64), ("batches", c_i64),
                 ("seed", ctypes.c_uint64), ("shuffle", ctypes.c_int32), ("pad0", ctypes.c_int32),
-                ("out", c_vp), ("next", c_vp)]
+                ("out", c_vp)]
 
 
 class Linear(ctypes.Structure):

@@ -498,28 +498,16 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       // this batch's rows of the block's stage, from the batch number every block reads before
       // the last one to finish advances it (below). (Issuing the draw's parameter loads before
       // or right after this read measured no faster: tools/linear_timing.py, round 4.)
-      // Both halves of the rows computed one batch ahead (mi_rows.next) are loaded with the
-      // counter -- no load waits on another -- and a row tagged for this batch is taken as is; the
-      // permutation runs only when neither tag matches (the loader's first batch).
-      const int64_t row = st0 * S::CH + tid;
-      const bool mine = tid < S::CH && st0 < st1 && row < N;
-      const int64_t rc = mine ? row : 0;
-      const bool ahead = L.rows.next != nullptr;
-      const uint64_t n0 = ahead ? L.rows.next[rc] : 0ull;
-      const uint64_t n1 = ahead ? L.rows.next[L.rows.batch + rc] : 0ull;
+      // (Rows computed one batch ahead by the previous launch and read here with the counter were
+      // measured slower, round 6: C4 34.7-35.5 against 33.8-34.8 us per step -- the next batch's
+      // permutation then delays the theta draw that overlaps the gathers; profiles/r06_ab.json.)
       batch_no = __hip_atomic_load(L.rows.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tid < S::CH && st0 < st1) {
+        const int64_t row = st0 * S::CH + tid;
         int32_t r = 0;
-        if (mine) {
-          const uint32_t tag = (uint32_t)(batch_no + 1);
-          if ((uint32_t)(n0 >> 32) == tag) {
-            r = (int32_t)(uint32_t)n0;
-          } else if ((uint32_t)(n1 >> 32) == tag) {
-            r = (int32_t)(uint32_t)n1;
-          } else {
-            const BatchOrder order = batch_order(batch_no, L.rows.batches, L.rows.seed);
-            r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
-          }
+        if (row < N) {
+          const BatchOrder order = batch_order(batch_no, L.rows.batches, L.rows.seed);
+          r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
           if (L.rows.out != nullptr && group == 0) L.rows.out[row] = r;
         }
         grows[tid] = r;
@@ -529,17 +517,6 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     MI_LIN_STAMP(1);
     if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
-    if (gen_rows && L.rows.next != nullptr && group == 0 && tid < S::CH && st0 < st1) {
-      // the next batch's row, while this stage's gathers are in flight (mi_rows.next)
-      const int64_t row = st0 * S::CH + tid;
-      if (row < N) {
-        const uint64_t b1 = batch_no + 1;
-        const BatchOrder order = batch_order(b1, L.rows.batches, L.rows.seed);
-        const int32_t r = batch_row(order, row, L.rows.n, L.rows.batch, L.rows.shuffle, rows_half);
-        L.rows.next[(int64_t)(b1 & 1) * L.rows.batch + row] =
-            ((uint64_t)(uint32_t)(b1 + 1) << 32) | (uint64_t)(uint32_t)r;
-      }
-    }
     if (drawn) draw_here();
     if (st0 < st1) store_stage(0);
     MI_LIN_STAMP(2);

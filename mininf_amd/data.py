@@ -104,7 +104,6 @@ class _Batch:
         R.n, R.batch, R.batches = loader.n, loader.batch_size, loader.batches
         R.seed, R.shuffle = loader.seed, int(loader.shuffle)
         R.out = self._rows.data_ptr()
-        R.next = loader.next_rows.data_ptr()
         return R
 
     def rows_taken(self) -> None:
@@ -255,9 +254,6 @@ class DeviceDataLoader:
         # batch counter (device): epoch = counter[0] // batches, batch = counter[0] % batches;
         # counter[1] is the rows kernel's completion count
         self.counter = torch.zeros(2, dtype=torch.int64, device=self.device)
-        # rows of the next batch, computed one batch ahead by the kernel that draws a batch's rows
-        # (mi_rows.next: two halves of batch_size tagged words)
-        self.next_rows = torch.zeros(2 * self.batch_size, dtype=torch.int64, device=self.device)
         self._position = 0   # host mirror for eager iteration (ragged last batch)
         self._last: Optional[_Batch] = None   # the last drawn batch (rows may be pending)
 

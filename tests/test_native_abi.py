@@ -31,7 +31,7 @@ def test_library_loads_and_exports_header():
         assert hasattr(lib, name), name
     assert set(names) == set(nat.EXPORTED_SYMBOLS)
     target = ctypes.create_string_buffer(16)
-    assert lib.mi_abi_version(target, 16) == nat.ABI_VERSION == 19
+    assert lib.mi_abi_version(target, 16) == nat.ABI_VERSION == 18
     assert target.value == b"gfx950"
 
 
