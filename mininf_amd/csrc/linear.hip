@@ -298,13 +298,8 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   const int64_t bid = blockIdx.x;
   const int64_t row_block = (bid / (8 * gy)) * 8 + bid % 8;
   const int64_t group = (bid / 8) % gy;
-  // Multi-stage launches stage X through two LDS buffers: stage st + 1 is stored into the other
-  // buffer right after stage st's tiles, so one barrier per stage separates the two (a single
-  // buffer needed a barrier before its store and one after it).
-  constexpr int kBufs = ONESTAGE ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) float xs[kBufs * S::CH * S::RSTR];
-  __shared__ float2 yms[kBufs * S::CH];
-  int cur = 0;   // the buffer the tiles read
+  __shared__ __attribute__((aligned(16))) float xs[S::CH * S::RSTR];
+  __shared__ float2 yms[S::CH];
   // rows drawn here (mi_linear.rows, ONESTAGE launches only): the stage's dataset rows
   __shared__ int32_t grows[ONESTAGE ? S::CH : 1];
   const bool gen_rows = ONESTAGE && L.rows.counter != nullptr;
@@ -407,16 +402,16 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
       ymr = make_float2(m != 0.0f ? y : 0.0f, m);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&]() {
 #pragma unroll
     for (int q = 0; q < S::QPT; ++q) {
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
-      float* dst = xs + buf * (S::CH * S::RSTR) + row * S::RSTR + 2 * c4;
+      float* dst = xs + row * S::RSTR + 2 * c4;
       *reinterpret_cast<float2*>(dst) = make_float2(xq[q].x, xq[q].z);           // even features
       *reinterpret_cast<float2*>(dst + S::HS) = make_float2(xq[q].y, xq[q].w);   // odd features
     }
-    if (tid < S::CH) yms[buf * S::CH + tid] = ymr;
+    if (tid < S::CH) yms[tid] = ymr;
   };
 
   // The block's particles' draws through the (still unused) X staging buffer into thf: called by
@@ -444,7 +439,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   // MU = X theta^T for the tile's 32 rows and this wave's 32 particles
   auto gemm1 = [&](int tile) -> f32x16 {
     f32x16 mu = f32x16{};
-    const float* xa = xs + cur * (S::CH * S::RSTR) + (tile * 32 + c) * S::RSTR + h * S::HS;
+    const float* xa = xs + (tile * 32 + c) * S::RSTR + h * S::HS;
 #pragma unroll
     for (int s = 0; s < S::HS; s += 4) {
       const float4 a = *reinterpret_cast<const float4*>(xa + s);
@@ -462,7 +457,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float2 ym = yms[cur * S::CH + row];
+      const float2 ym = yms[row];
       const float loc = mu[r];
       fl |= (loc != loc) ? MI_FLAG_PARAM : 0u;
       if (FAMILY == MI_NORMAL) {
@@ -484,7 +479,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 #pragma unroll
     for (int t = 0; t < PT; ++t) {
       const int p = 32 * t + c;
-      const float* xb = xs + cur * (S::CH * S::RSTR) + (p & 1) * S::HS + (p >> 1);
+      const float* xb = xs + (p & 1) * S::HS + (p >> 1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -518,7 +513,7 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     if (drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
     if (st0 < st1) load_stage(st0);
     if (drawn) draw_here();
-    if (st0 < st1) store_stage(0);
+    if (st0 < st1) store_stage();
     MI_LIN_STAMP(2);
     __syncthreads();
     MI_LIN_STAMP(3);
@@ -547,10 +542,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
   if (!ONESTAGE && drawn) draw_theta_load<kMfThreads>(L, draw_nk, dregs);
   if (!ONESTAGE && st0 < st1) load_stage(st0);
   if (!ONESTAGE && drawn) draw_here();
-  if (!ONESTAGE && st0 < st1) store_stage(0);
+  if (!ONESTAGE && st0 < st1) store_stage();
   if (!ONESTAGE) __syncthreads();
   for (int64_t st = st0; !ONESTAGE && st < st1; ++st) {
-    cur = (int)((st - st0) & 1);
     if (st + 1 < st1) load_stage(st + 1);   // in flight during this stage's MFMAs
     // Software pipeline over this wave's tiles: the first product of tile j + 1 is issued before
     // the elementwise step of tile j, so its MFMAs run while the VALU evaluates the densities.
@@ -576,10 +570,13 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
         acc2[t] = f32x16{};
       }
     }
-    // the next stage into the other buffer (no wave reads it: every wave finished the previous
-    // stage at the last barrier), then one barrier before its tiles
-    if (st + 1 < st1) store_stage(cur ^ 1);
+    // (two LDS buffers with one barrier per stage measured no faster, round 6: C3 313.6-316.1
+    // against 311.9-314.0 us per step, profiles/r06_ab.json)
     __syncthreads();
+    if (st + 1 < st1) {
+      store_stage();
+      __syncthreads();
+    }
   }
 
   // ---- partials --------------------------------------------------------------------------------
