@@ -1152,15 +1152,12 @@ constexpr int kSmemP = 4;
 constexpr int64_t kSmemSlots = 1024;
 
 // Grids of 4096-element chunks between half a round and one round of slots are evened out to one
-// round -- the slots the launch's side-job workgroups (mi_side) take left out, so that no site
-// workgroup shares its SIMDs with one; smaller grids keep 4096 (shorter chunks would only add
-// partials for the reduction).
-int smem_chunk(int64_t N, int64_t gy, int64_t side) {
+// round; smaller grids keep 4096 (shorter chunks would only add partials for the reduction).
+int smem_chunk(int64_t N, int64_t gy) {
   gy = std::max<int64_t>(1, gy);
-  const int64_t slots = kSmemSlots - std::min<int64_t>(side, kSmemSlots / 2);
   const int64_t blocks = ceil_div(N, mi::kSmemMaxChunk) * gy;
-  if (blocks < slots / 2 || blocks > slots) return mi::kSmemMaxChunk;
-  const int64_t chunk = (ceil_div(N, slots / gy) + 31) / 32 * 32;
+  if (blocks < kSmemSlots / 2 || blocks > kSmemSlots) return mi::kSmemMaxChunk;
+  const int64_t chunk = (ceil_div(N, kSmemSlots / gy) + 31) / 32 * 32;
   return (int)std::min<int64_t>(mi::kSmemMaxChunk, std::max<int64_t>(2048, chunk));
 }
 
@@ -1183,11 +1180,11 @@ Plan make_plan(const mi_group* g) {
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     const bool smem = bcast_smem(g);
-    const int64_t side = (smem && g->side.out != nullptr)
-                             ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
-    if (smem) p.chunk = smem_chunk(g->N, ceil_div(g->K, mi::kBcastThreads * kSmemP), side);
+    if (smem) p.chunk = smem_chunk(g->N, ceil_div(g->K, mi::kBcastThreads * kSmemP));
     const int64_t chunks = ceil_div(g->N, smem ? p.chunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
+    const int64_t side = (smem && g->side.out != nullptr)
+                             ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
     p.grid = dim3((unsigned)(chunks + side),
                   (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? kSmemP : mi::kBcastP)));
     return p;
