@@ -658,38 +658,29 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int nfull = SUFF ? 0 : len & ~(kBlock - 1);
   int j = 0;
   if (nfull > 0) {
-    // The block's four waves walk the chunk's whole 256-element blocks from staggered starts
-    // (wave w from block w nb / 4, wrapping), so their scalar-load waits fall at different times
-    // instead of together: the waves of a workgroup read the same x, so walked in step they stalled
-    // on the same round trips and left the SIMDs' VALU idle at once.
-    const int nb = nfull / kBlock;
-    const int b0 = (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * nb) >> 2;   // (uniform)
     float xc[kGroup];
 #pragma unroll
-    for (int e = 0; e < kGroup; ++e) xc[e] = xs[b0 * kBlock + e];
-    // the first block of each later quarter of the walk (no division inside the loop)
-    const int t1 = (nb + 3) / 4, t2 = (nb + 1) / 2, t3 = (3 * nb + 3) / 4;
+    for (int e = 0; e < kGroup; ++e) xc[e] = xs[e];
+    // the first block index of each later quarter of the chunk (no division inside the loop)
+    const int q1 = (nfull / 4 + kBlock - 1) & ~(kBlock - 1), q2 = (nfull / 2 + kBlock - 1) & ~(kBlock - 1),
+              q3 = (3 * nfull / 4 + kBlock - 1) & ~(kBlock - 1);
     if (balance) __builtin_amdgcn_s_setprio(3);
-    int blk = b0;
-    for (int t = 0; t < nb; ++t) {
+    for (; j < nfull; j += kBlock) {
       // Progress-balanced priority: a wave drops one priority level per quarter of its chunk, so
       // the SIMD's arbiter (priority, then age) lets the waves behind it catch up; the waves of a
       // SIMD then finish together instead of the oldest first, which would leave the last one
       // issuing alone (at half the VALU rate) through the kernel's tail.
       if (balance) {
-        if (t == t1) __builtin_amdgcn_s_setprio(2);
-        else if (t == t2) __builtin_amdgcn_s_setprio(1);
-        else if (t == t3) __builtin_amdgcn_s_setprio(0);
+        if (j == q1) __builtin_amdgcn_s_setprio(2);
+        else if (j == q2) __builtin_amdgcn_s_setprio(1);
+        else if (j == q3) __builtin_amdgcn_s_setprio(0);
       }
-      const int jb = blk * kBlock;
-      blk = blk + 1 == nb ? 0 : blk + 1;
-      const int jn = t + 1 < nb ? blk * kBlock : jb;   // the next block's start (the last: unused)
       f32x2 in[2][kSmemP];
 #pragma unroll
       for (int p = 0; p < kSmemP; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
 #pragma unroll
       for (int g = 0; g < kBlock; g += kGroup) {
-        const int nxt = g + kGroup < kBlock ? jb + g + kGroup : jn;
+        const int nxt = min(j + g + kGroup, nfull - kGroup);   // in bounds; the last is unused
         float xn[kGroup];
 #pragma unroll
         for (int e = 0; e < kGroup; ++e) xn[e] = xs[nxt + e];
@@ -705,7 +696,6 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       }
       flush(in);
     }
-    j = nfull;
   }
   if (!SUFF && j + kGroup <= len) {   // whole groups of 32 past the last whole block
     f32x2 in[2][kSmemP];
