@@ -200,3 +200,38 @@ def test_full_size_c2_on_device_draws(device):
         for name in ("concentration1", "concentration0"):
             want = ref[f"grad_u_{name}"]
             assert abs(float(g[name].grad) - want) <= 1e-5 * abs(want), (step, name)
+
+
+@pytest.mark.parametrize("n", [1_000_017, 600_001, 2_100_000])
+def test_c2_chunk_plans_against_the_oracle(device, n):
+    """
+    The C2 site kernel's chunk length follows the grid (r06: chunks evened out to one round of
+    workgroup slots when the 4096-element grid fills between half a round and one round): n =
+    1_000_017 gives 3936-element chunks with a 273-element last chunk (a whole 256-block, then an
+    odd tail of 17 through the pair loop), 600_001 gives 2368-element chunks (groups of 32 past
+    the last whole block), 2_100_000 keeps 4096 (two rounds). Loss and gradients against the oracle
+    at 1e-5, on the device's own Beta draws.
+    """
+    K, seed = 4096, 77
+    gen = torch.Generator().manual_seed(1)
+    x = (torch.rand(n, generator=gen) < 0.3).float()
+
+    def model():
+        theta = mi.sample("theta", Beta(2, 2))
+        mi.sample("x", Bernoulli(theta), sample_shape=[n])
+
+    approx = mi.nn.ParameterizedDistribution(Beta, concentration1=1.7,
+                                             concentration0=3.1).to(device)
+    loss_fn = mi.nn.EvidenceLowerBoundLoss(num_particles=K, seed=seed)
+    q = approx()
+    value = loss_fn(mi.condition(model, x=x.to(device)), {"theta": q})
+    value.backward()
+    c1 = float(q.concentration1.detach().cpu())
+    c0 = float(q.concentration0.detach().cpu())
+    draws = oracle_build.beta_draws([c1], [c0], K, seed, 0, 0, 0)[0][:, 0]
+    ref = oracle.beta_bernoulli_elbo(x.numpy(), 2, 2, c1, c0, draws)
+    assert abs(float(value) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    g = approx.distribution_parameters
+    for name in ("concentration1", "concentration0"):
+        want = ref[f"grad_u_{name}"]
+        assert abs(float(g[name].grad) - want) <= 1e-5 * abs(want), name
