@@ -25,6 +25,8 @@
 #include "entropy.hpp"
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -588,12 +590,19 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // in exact arithmetic (C2's per-eval arithmetic is reducible).
 // chunk: elements per chunk, a multiple of 32 and at most kSmemMaxChunk (the host sizes it so that
 // chunks x particle blocks fill the chip's workgroup slots: make_plan).
-constexpr int kSmemMaxChunk = 4096;
+constexpr int kSmemMaxChunk = 5120;
+// The chunks' element ranges: tier t (chunks [t tier_chunks, (t + 1) tier_chunks), the last tier
+// to the end) holds chunks of len[t] elements from off[t] on.
+struct SmemChunks {
+  int64_t off[4];
+  int len[4];
+  int tier_chunks;
+};
 template <int FAMILY, int kSmemP, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
-                                                                   int mode, int chunk,
+                                                                   int mode, const SmemChunks ch,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
   kernarg_prefetch<(int)sizeof(mi_group)>();
@@ -613,34 +622,38 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const unsigned long long t0 = span_begin(G.stamps);
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
-  const int64_t i0 = c * chunk;
-  const int len = (int)min((int64_t)chunk, G.N - i0);
+  const int tier = (int)min<int64_t>(3, c / ch.tier_chunks);
+  const int64_t i0 = ch.off[tier] + (c - (int64_t)tier * ch.tier_chunks) * ch.len[tier];
+  const int len = (int)min((int64_t)ch.len[tier], G.N - i0);
   uint32_t fl = 0u;
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
+  // Only the logits live through the FMA loop (as the duplicated pairs ld): d l / d theta is
+  // computed again after it, from the same values by the same code (registers: 8 particles per lane
+  // fit 4 waves per SIMD).
   const int64_t K = G.K;
   const int64_t kbase = kblock * (kBcastThreads * kSmemP) + threadIdx.x;
-  float lg[kSmemP], dl[kSmemP];
-#pragma unroll
-  for (int p = 0; p < kSmemP; ++p) {
+  auto logits = [&](int p, float& l, float& d) -> bool {
     const int64_t k = kbase + p * kBcastThreads;
     const float a = role_scalar(G, st, 0, min(k, K - 1));
-    bool bad;
-    dl[p] = 1.0f;
+    d = 1.0f;
     if (FAMILY == MI_BERNOULLI_PROBS) {
-      bad = !(a >= 0.0f && a <= 1.0f);
-      bernoulli_probs_to_logits(a, lg[p], dl[p]);
-    } else {
-      lg[p] = a;
-      bad = a != a;
+      bernoulli_probs_to_logits(a, l, d);
+      return !(a >= 0.0f && a <= 1.0f);
     }
-    fl |= (c == 0 && k < K && bad) ? MI_FLAG_PARAM : 0u;
+    l = a;
+    return a != a;
+  };
+  f32x2 ld[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) {
+    float l, d;
+    const bool bad = logits(p, l, d);
+    ld[p] = f32x2{l, l};
+    fl |= (c == 0 && kbase + p * kBcastThreads < K && bad) ? MI_FLAG_PARAM : 0u;
   }
 
   // ---- sum_i x_i l_k: element pairs from SGPRs against duplicated particle logits --------------
-  f32x2 ld[kSmemP];
-#pragma unroll
-  for (int p = 0; p < kSmemP; ++p) ld[p] = f32x2{lg[p], lg[p]};
   double acc[kSmemP];
 #pragma unroll
   for (int p = 0; p < kSmemP; ++p) acc[p] = 0.0;
@@ -770,10 +783,17 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   s_a = block_sum(s_a, scratch);
   if (SUFF) {
 #pragma unroll
-    for (int p = 0; p < kSmemP; ++p) acc[p] = (double)lg[p] * (double)s_a;
+    for (int p = 0; p < kSmemP; ++p) acc[p] = (double)ld[p].x * (double)s_a;
+  }
+  __asm__ volatile("" ::: "memory");   // (the parameters are read again, not held in registers)
+  float dl[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) {
+    float l;
+    (void)logits(p, l, dl[p]);
   }
 
-  // ---- partials of this chunk, and the particle-constant segment from the chunk-0 blocks -------
+  // ---- partials of this chunk, and the particle-constant segment (below) --------------------
   const int o_a = st.operand[0];
   const int slot_a = (G.compute_grads != 0 && o_a >= 0 && G.operands[o_a].grad_mode == MI_GRAD_PARTICLE)
                          ? G.operands[o_a].slot : -1;
@@ -788,8 +808,19 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
     if (k >= K) continue;
     part[c * K + k] = (float)acc[p];
     if (slot_a >= 0 && !rank1) slot_part[c * K + k] = w * (s_a * dl[p]);
-    if (c == 0) {
-      const float l = lg[p];
+  }
+  // The particle-constant segment: particle slot p of every lane by the chunk-p workgroups (chunk 0
+  // takes all of them when the grid has fewer chunks than particles per lane), one particle at a
+  // time -- the prior's special functions interleaved over the particles held ~40 registers.
+  const bool spread = chunks >= kSmemP;
+  if (spread ? c < kSmemP : c == 0) {
+    const int p0 = spread ? (int)c : 0, p1 = spread ? (int)c + 1 : kSmemP;
+#pragma unroll 1
+    for (int p = p0; p < p1; ++p) {
+      const int64_t k = kbase + p * kBcastThreads;
+      if (k >= K) continue;
+      float l, dlp;
+      (void)logits(p, l, dlp);
       const float t = expf(-fabsf(l));
       const double softplus = (double)(fmaxf(l, 0.0f) + log1pf(t));
       const double sig = (double)(l >= 0.0f ? 1.0f / (1.0f + t) : t / (1.0f + t));
@@ -808,9 +839,9 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
       }
       part[extra * K + k] = (float)(-n * softplus) + prior_lp;
       if (slot_a >= 0) {
-        const float e = w * (float)(-n * sig * (double)dl[p]) + w * prior_d;
+        const float e = w * (float)(-n * sig * (double)dlp) + w * prior_d;
         if (rank1) {
-          slot_part[nseg + k] = w * dl[p];       // f[k]
+          slot_part[nseg + k] = w * dlp;         // f[k]
           slot_part[nseg + K + k] = e;           // e[k]
         } else {
           slot_part[extra * K + k] = e;
@@ -1144,21 +1175,67 @@ bool bcast_smem(const mi_group* g) {
 
 // k_site_bcast_smem: particles per lane and chunk length (measured r02: the best of {4, 8} x
 // {2048, 4096, 8192})
-constexpr int kSmemP = 4;
+// MININF_AMD_BCAST_P=8: eight particles per lane (A/B knob).
+int smem_p() { return env_int("MININF_AMD_BCAST_P", 4) == 8 ? 8 : 4; }
 // Chunks of at most 4096 elements (measured r02: 4096 against 2048 / 8192), sized so that chunks x
-// particle blocks come close to kSmemSlots workgroups: four 4-wave workgroups per CU on 256 CUs, one
+// particle blocks come close to smem_slots() workgroups: four 4-wave workgroups per CU on 256 CUs, one
 // round. (r05 used 4096-element chunks throughout: C2's 245 chunks x 4 particle blocks left 44 of
 // the 1024 slots idle.)
-constexpr int64_t kSmemSlots = 1024;
+constexpr int64_t kSmemSlotsDefault = 1024;
+// MININF_AMD_BCAST_SLOTS: workgroup slots the chunk plan fills (A/B knob)
+int64_t smem_slots() { return std::max(256, env_int("MININF_AMD_BCAST_SLOTS", (int)kSmemSlotsDefault)); }
 
 // Grids of 4096-element chunks between half a round and one round of slots are evened out to one
 // round; smaller grids keep 4096 (shorter chunks would only add partials for the reduction).
+constexpr int kSmemChunk = 4096;
 int smem_chunk(int64_t N, int64_t gy) {
   gy = std::max<int64_t>(1, gy);
-  const int64_t blocks = ceil_div(N, mi::kSmemMaxChunk) * gy;
-  if (blocks < kSmemSlots / 2 || blocks > kSmemSlots) return mi::kSmemMaxChunk;
-  const int64_t chunk = (ceil_div(N, kSmemSlots / gy) + 31) / 32 * 32;
-  return (int)std::min<int64_t>(mi::kSmemMaxChunk, std::max<int64_t>(2048, chunk));
+  const int64_t blocks = ceil_div(N, kSmemChunk) * gy;
+  if (blocks < smem_slots() / 4 || blocks > smem_slots()) return kSmemChunk;
+  const int64_t chunk = (ceil_div(N, smem_slots() / gy) + 31) / 32 * 32;
+  return (int)std::min<int64_t>(kSmemChunk, std::max<int64_t>(1024, chunk));
+}
+
+// The chunks' element ranges (mi::SmemChunks): `chunks` chunks of `chunk` elements, or -- for a
+// one-round grid with MININF_AMD_C2_TAPER="w0,w1,w2,w3" -- four tiers of consecutive chunks whose
+// lengths follow the weights: the workgroups of one round reach their CUs in chunk order (block b
+// is the b / 256-th workgroup of its CU), and the arbiter favours the older waves of a SIMD.
+mi::SmemChunks smem_layout(int64_t N, int chunk, int64_t gy) {
+  mi::SmemChunks L{};
+  const int64_t chunks = ceil_div(N, chunk);
+  L.tier_chunks = (int)std::max<int64_t>(1, chunks);
+  for (int t = 0; t < 4; ++t) L.len[t] = chunk;
+  const char* env = std::getenv("MININF_AMD_C2_TAPER");
+  double w[4];
+  if (env == nullptr || std::sscanf(env, "%lf,%lf,%lf,%lf", &w[0], &w[1], &w[2], &w[3]) != 4)
+    return L;
+  const int64_t blocks = chunks * std::max<int64_t>(1, gy);
+  if (blocks < smem_slots() / 2 || blocks > smem_slots() || chunks < 8) return L;
+  const mi::SmemChunks uniform = L;
+  const int64_t T = ceil_div(chunks, 4);
+  int64_t n[4];
+  double wsum = 0.0;
+  for (int t = 0; t < 4; ++t) {
+    n[t] = std::min<int64_t>(T, std::max<int64_t>(0, chunks - t * T));
+    wsum += (double)n[t] * w[t];
+  }
+  if (n[3] < 1 || !(wsum > 0.0)) return uniform;
+  const double base = (double)N / wsum;
+  int64_t off = 0;
+  for (int t = 0; t < 3; ++t) {
+    const int64_t len = ((int64_t)std::ceil(w[t] * base) + 31) / 32 * 32;
+    if (len < 32 || len > mi::kSmemMaxChunk) return uniform;
+    L.off[t] = off;
+    L.len[t] = (int)len;
+    off += n[t] * len;
+  }
+  const int64_t len3 = (ceil_div(N - off, n[3]) + 31) / 32 * 32;
+  if (off >= N || len3 < 32 || len3 > mi::kSmemMaxChunk || off + (n[3] - 1) * len3 >= N)
+    return uniform;
+  L.off[3] = off;
+  L.len[3] = (int)len3;
+  L.tier_chunks = (int)T;
+  return L;
 }
 
 struct Plan {
@@ -1170,6 +1247,8 @@ struct Plan {
   int64_t seg_len;         // COL
   int kw;                  // COL
   int chunk = 0;           // BCAST (k_site_bcast_smem): elements per chunk
+  mi::SmemChunks layout{}; // BCAST (k_site_bcast_smem): the chunks' element ranges
+  int smem_p = 4;          // BCAST (k_site_bcast_smem): particles per lane
   dim3 grid;
 };
 
@@ -1180,13 +1259,18 @@ Plan make_plan(const mi_group* g) {
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     const bool smem = bcast_smem(g);
-    if (smem) p.chunk = smem_chunk(g->N, ceil_div(g->K, mi::kBcastThreads * kSmemP));
+    if (smem) {
+      p.smem_p = smem_p();
+      const int64_t gy = ceil_div(g->K, mi::kBcastThreads * p.smem_p);
+      p.chunk = smem_chunk(g->N, gy);
+      p.layout = smem_layout(g->N, p.chunk, gy);
+    }
     const int64_t chunks = ceil_div(g->N, smem ? p.chunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
     const int64_t side = (smem && g->side.out != nullptr)
                              ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
     p.grid = dim3((unsigned)(chunks + side),
-                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? kSmemP : mi::kBcastP)));
+                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? p.smem_p : mi::kBcastP)));
     return p;
   }
   int dense = -1;
@@ -1276,8 +1360,8 @@ bool smem_rank1(const mi_group* g, const Plan& p) {
   return g->num_slots == 1 && g->compute_grads && p.nseg >= 3 && p.nseg <= MI_REDUCE_MAX_SEG;
 }
 
-template <int FAM>
-void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
+template <int FAM, int kSmemP>
+void launch_smem_p(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 block(mi::kBcastThreads);
   // p.grid = (chunks + side blocks, particle blocks): the kernel takes them as one XCD-aware
   // dimension (see k_site_bcast_smem)
@@ -1290,10 +1374,18 @@ void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags,
   // l_k sum_i x_i), never the default
   if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
     hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, true>), grid, block, 0, s,
-                       G, part, p.nseg, gy, rank1, p.chunk, flags);
+                       G, part, p.nseg, gy, rank1, p.layout, flags);
   else
     hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP>), grid, block, 0, s, G,
-                       part, p.nseg, gy, rank1, p.chunk, flags);
+                       part, p.nseg, gy, rank1, p.layout, flags);
+}
+
+template <int FAM>
+void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
+  if (p.smem_p == 8)
+    launch_smem_p<FAM, 8>(G, p, part, flags, s);
+  else
+    launch_smem_p<FAM, 4>(G, p, part, flags, s);
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {

@@ -96,17 +96,87 @@ __global__ __launch_bounds__(256) void k_probe(const float* __restrict__ x, cons
   }
 }
 
-template <int P, int CHUNK, bool LOADS, int PREP = 0, bool POST = false>
+// The same sums with the chunk staged in LDS (coalesced float4 loads, one pass) and read back as
+// broadcast ds_read_b128 (every lane the same address) into VGPR pairs: v_pk_fma_f32 with all
+// operands in VGPRs and the data latency decoupled from the scalar unit.
+template <int P, int CHUNK>
+__global__ __launch_bounds__(256) void k_probe_lds(const float* __restrict__ x, const float* __restrict__ logits,
+                                                   int64_t N, int64_t K, float* __restrict__ part,
+                                                   unsigned long long* __restrict__ stamps) {
+  __shared__ float4 xl[CHUNK / 4];
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  const int64_t c = blockIdx.x;
+  const int64_t i0 = c * CHUNK;
+  const int len = (int)min((int64_t)CHUNK, N - i0);
+  const int nq = len / 4;
+  const float4* xg = reinterpret_cast<const float4*>(x + i0);
+  for (int q = threadIdx.x; q < nq; q += 256) xl[q] = xg[q];
+  const int64_t kbase = (int64_t)blockIdx.y * (256 * P) + threadIdx.x;
+  f32x2 ld[P];
+  double acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const float l = logits[min(kbase + p * 256, K - 1)];
+    ld[p] = f32x2{l, l};
+    acc[p] = 0.0;
+  }
+  __syncthreads();
+  constexpr int kQ = 64;   // quads per fp32 partial (256 elements)
+  int q = 0;
+  for (; q + kQ <= nq; q += kQ) {
+    f32x2 in[2][P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
+#pragma unroll 16
+    for (int e = 0; e < kQ; ++e) {
+      const float4 v = xl[q + e];
+      const f32x2 a = f32x2{v.x, v.y}, b = f32x2{v.z, v.w};
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        in[0][p] = __builtin_elementwise_fma(a, ld[p], in[0][p]);
+        in[1][p] = __builtin_elementwise_fma(b, ld[p], in[1][p]);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      acc[p] += (double)((in[0][p].x + in[0][p].y) + (in[1][p].x + in[1][p].y));
+  }
+  for (; q < nq; ++q) {
+    const float4 v = xl[q];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] += (double)(v.x * ld[p].x + v.y * ld[p].x + v.z * ld[p].x + v.w * ld[p].x);
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int64_t k = kbase + p * 256;
+    if (k < K) part[c * K + k] = (float)acc[p];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t b = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    stamps[4 * b + 0] = t0;
+    stamps[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    stamps[4 * b + 2] = __builtin_amdgcn_s_memtime() - c0;
+    stamps[4 * b + 3] = 0;
+  }
+}
+
+template <int P, int CHUNK, bool LOADS, int PREP = 0, bool POST = false, bool LDS = false>
 void run(const char* name, const float* x, const float* lg, int64_t N, int64_t K, float* part,
          unsigned long long* stamps) {
   const dim3 grid((unsigned)((N + CHUNK - 1) / CHUNK), (unsigned)((K + 256 * P - 1) / (256 * P)));
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  for (int w = 0; w < 5; ++w) hipLaunchKernelGGL((k_probe<P, CHUNK, LOADS, PREP, POST>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+  auto launch = [&]() {
+    if (LDS) hipLaunchKernelGGL((k_probe_lds<P, CHUNK>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+    else hipLaunchKernelGGL((k_probe<P, CHUNK, LOADS, PREP, POST>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+  };
+  for (int w = 0; w < 5; ++w) launch();
   (void)hipEventRecord(a);
   const int reps = 20;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_probe<P, CHUNK, LOADS, PREP, POST>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+  for (int r = 0; r < reps; ++r) launch();
   (void)hipEventRecord(b);
   (void)hipEventSynchronize(b);
   float ms;
@@ -149,13 +219,12 @@ int main() {
   for (int64_t k = 0; k < K; ++k) hl[k] = 0.3f + 0.001f * (float)(k % 100);
   (void)hipMemcpy(x, hx.data(), N * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(lg, hl.data(), K * 4, hipMemcpyHostToDevice);
-  run<4, 4096, true>("P4_C4096", x, lg, N, K, part, stamps);
-  run<4, 4096, true, 1>("P4_C4096_prep_libm", x, lg, N, K, part, stamps);
-  run<4, 4096, true, 2>("P4_C4096_prep_hw", x, lg, N, K, part, stamps);
-  run<4, 4096, true, 0, true>("P4_C4096_post", x, lg, N, K, part, stamps);
-  run<4, 4096, true, 1, true>("P4_C4096_prep_libm_post", x, lg, N, K, part, stamps);
-  run<4, 2048, true>("P4_C2048", x, lg, N, K, part, stamps);
-  run<4, 2048, true, 1, true>("P4_C2048_prep_libm_post", x, lg, N, K, part, stamps);
-  run<4, 4096, true>("P4_C4096", x, lg, N, K, part, stamps);
+  run<4, 3936, true>("P4_C3936", x, lg, N, K, part, stamps);
+  run<4, 3936, false>("P4_C3936_noloads", x, lg, N, K, part, stamps);
+  run<4, 3936, true, 0, false, true>("P4_C3936_lds", x, lg, N, K, part, stamps);
+  run<8, 1984, true, 0, false, true>("P8_C1984_lds", x, lg, N, K, part, stamps);
+  run<8, 1984, true>("P8_C1984", x, lg, N, K, part, stamps);
+  run<4, 3936, true>("P4_C3936", x, lg, N, K, part, stamps);
+  run<4, 3936, true, 0, false, true>("P4_C3936_lds", x, lg, N, K, part, stamps);
   return 0;
 }
