@@ -590,19 +590,12 @@ MI_DEV void beta_side_block(const mi_side& S, int64_t b) {
 // in exact arithmetic (C2's per-eval arithmetic is reducible).
 // chunk: elements per chunk, a multiple of 32 and at most kSmemMaxChunk (the host sizes it so that
 // chunks x particle blocks fill the chip's workgroup slots: make_plan).
-constexpr int kSmemMaxChunk = 5120;
-// The chunks' element ranges: tier t (chunks [t tier_chunks, (t + 1) tier_chunks), the last tier
-// to the end) holds chunks of len[t] elements from off[t] on.
-struct SmemChunks {
-  int64_t off[4];
-  int len[4];
-  int tier_chunks;
-};
+constexpr int kSmemMaxChunk = 4096;
 template <int FAMILY, int kSmemP, bool SUFF = false>
 __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_group G,
                                                                    float* __restrict__ part,
                                                                    int64_t nseg, int gy,
-                                                                   int mode, const SmemChunks ch,
+                                                                   int mode, int chunk,
                                                                    uint32_t* __restrict__ flags) {
   __shared__ float scratch[kBcastThreads / 64];
   kernarg_prefetch<(int)sizeof(mi_group)>();
@@ -622,15 +615,14 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const unsigned long long t0 = span_begin(G.stamps);
   const mi_site& st = G.sites[0];
   const float* xg = G.operands[st.operand[2]].data;
-  const int tier = (int)min<int64_t>(3, c / ch.tier_chunks);
-  const int64_t i0 = ch.off[tier] + (c - (int64_t)tier * ch.tier_chunks) * ch.len[tier];
-  const int len = (int)min((int64_t)ch.len[tier], G.N - i0);
+  const int64_t i0 = c * chunk;
+  const int len = (int)min((int64_t)chunk, G.N - i0);
   uint32_t fl = 0u;
 
   // ---- per-particle logits (as k_bcast_prep) ---------------------------------------------------
   // Only the logits live through the FMA loop (as the duplicated pairs ld): d l / d theta is
-  // computed again after it, from the same values by the same code (registers: 8 particles per lane
-  // fit 4 waves per SIMD).
+  // computed again after it, from the same values by the same code (r06: 102 -> 78 VGPR with the
+  // particle-constant segment below; 86.2 vs 87.6 us per C2 step, profiles/r06_ab.json ab14).
   const int64_t K = G.K;
   const int64_t kbase = kblock * (kBcastThreads * kSmemP) + threadIdx.x;
   auto logits = [&](int p, float& l, float& d) -> bool {
@@ -1174,68 +1166,23 @@ bool bcast_smem(const mi_group* g) {
 }
 
 // k_site_bcast_smem: particles per lane and chunk length (measured r02: the best of {4, 8} x
-// {2048, 4096, 8192})
-// MININF_AMD_BCAST_P=8: eight particles per lane (A/B knob).
-int smem_p() { return env_int("MININF_AMD_BCAST_P", 4) == 8 ? 8 : 4; }
+// {2048, 4096, 8192}; r06 at 78 VGPR: 8 particles per lane in 1010 workgroups 91.8 us per C2 step
+// against 86.2, profiles/r06_ab.json ab14)
+constexpr int kSmemP = 4;
 // Chunks of at most 4096 elements (measured r02: 4096 against 2048 / 8192), sized so that chunks x
-// particle blocks come close to smem_slots() workgroups: four 4-wave workgroups per CU on 256 CUs, one
+// particle blocks come close to kSmemSlots workgroups: four 4-wave workgroups per CU on 256 CUs, one
 // round. (r05 used 4096-element chunks throughout: C2's 245 chunks x 4 particle blocks left 44 of
-// the 1024 slots idle.)
-constexpr int64_t kSmemSlotsDefault = 1024;
-// MININF_AMD_BCAST_SLOTS: workgroup slots the chunk plan fills (A/B knob)
-int64_t smem_slots() { return std::max(256, env_int("MININF_AMD_BCAST_SLOTS", (int)kSmemSlotsDefault)); }
+// the 1024 slots idle; r06: 1280 / 1536 slots at 78 VGPR measured slower, ab14.)
+constexpr int64_t kSmemSlots = 1024;
 
 // Grids of 4096-element chunks between half a round and one round of slots are evened out to one
 // round; smaller grids keep 4096 (shorter chunks would only add partials for the reduction).
-constexpr int kSmemChunk = 4096;
 int smem_chunk(int64_t N, int64_t gy) {
   gy = std::max<int64_t>(1, gy);
-  const int64_t blocks = ceil_div(N, kSmemChunk) * gy;
-  if (blocks < smem_slots() / 4 || blocks > smem_slots()) return kSmemChunk;
-  const int64_t chunk = (ceil_div(N, smem_slots() / gy) + 31) / 32 * 32;
-  return (int)std::min<int64_t>(kSmemChunk, std::max<int64_t>(1024, chunk));
-}
-
-// The chunks' element ranges (mi::SmemChunks): `chunks` chunks of `chunk` elements, or -- for a
-// one-round grid with MININF_AMD_C2_TAPER="w0,w1,w2,w3" -- four tiers of consecutive chunks whose
-// lengths follow the weights: the workgroups of one round reach their CUs in chunk order (block b
-// is the b / 256-th workgroup of its CU), and the arbiter favours the older waves of a SIMD.
-mi::SmemChunks smem_layout(int64_t N, int chunk, int64_t gy) {
-  mi::SmemChunks L{};
-  const int64_t chunks = ceil_div(N, chunk);
-  L.tier_chunks = (int)std::max<int64_t>(1, chunks);
-  for (int t = 0; t < 4; ++t) L.len[t] = chunk;
-  const char* env = std::getenv("MININF_AMD_C2_TAPER");
-  double w[4];
-  if (env == nullptr || std::sscanf(env, "%lf,%lf,%lf,%lf", &w[0], &w[1], &w[2], &w[3]) != 4)
-    return L;
-  const int64_t blocks = chunks * std::max<int64_t>(1, gy);
-  if (blocks < smem_slots() / 2 || blocks > smem_slots() || chunks < 8) return L;
-  const mi::SmemChunks uniform = L;
-  const int64_t T = ceil_div(chunks, 4);
-  int64_t n[4];
-  double wsum = 0.0;
-  for (int t = 0; t < 4; ++t) {
-    n[t] = std::min<int64_t>(T, std::max<int64_t>(0, chunks - t * T));
-    wsum += (double)n[t] * w[t];
-  }
-  if (n[3] < 1 || !(wsum > 0.0)) return uniform;
-  const double base = (double)N / wsum;
-  int64_t off = 0;
-  for (int t = 0; t < 3; ++t) {
-    const int64_t len = ((int64_t)std::ceil(w[t] * base) + 31) / 32 * 32;
-    if (len < 32 || len > mi::kSmemMaxChunk) return uniform;
-    L.off[t] = off;
-    L.len[t] = (int)len;
-    off += n[t] * len;
-  }
-  const int64_t len3 = (ceil_div(N - off, n[3]) + 31) / 32 * 32;
-  if (off >= N || len3 < 32 || len3 > mi::kSmemMaxChunk || off + (n[3] - 1) * len3 >= N)
-    return uniform;
-  L.off[3] = off;
-  L.len[3] = (int)len3;
-  L.tier_chunks = (int)T;
-  return L;
+  const int64_t blocks = ceil_div(N, mi::kSmemMaxChunk) * gy;
+  if (blocks < kSmemSlots / 2 || blocks > kSmemSlots) return mi::kSmemMaxChunk;
+  const int64_t chunk = (ceil_div(N, kSmemSlots / gy) + 31) / 32 * 32;
+  return (int)std::min<int64_t>(mi::kSmemMaxChunk, std::max<int64_t>(2048, chunk));
 }
 
 struct Plan {
@@ -1247,8 +1194,6 @@ struct Plan {
   int64_t seg_len;         // COL
   int kw;                  // COL
   int chunk = 0;           // BCAST (k_site_bcast_smem): elements per chunk
-  mi::SmemChunks layout{}; // BCAST (k_site_bcast_smem): the chunks' element ranges
-  int smem_p = 4;          // BCAST (k_site_bcast_smem): particles per lane
   dim3 grid;
 };
 
@@ -1259,18 +1204,13 @@ Plan make_plan(const mi_group* g) {
   if (g->draw.operand == 0 && bcast_eligible(g)) {
     p.shape = kBcast;
     const bool smem = bcast_smem(g);
-    if (smem) {
-      p.smem_p = smem_p();
-      const int64_t gy = ceil_div(g->K, mi::kBcastThreads * p.smem_p);
-      p.chunk = smem_chunk(g->N, gy);
-      p.layout = smem_layout(g->N, p.chunk, gy);
-    }
+    if (smem) p.chunk = smem_chunk(g->N, ceil_div(g->K, mi::kBcastThreads * kSmemP));
     const int64_t chunks = ceil_div(g->N, smem ? p.chunk : mi::kBcastChunk);
     p.nseg = smem ? chunks + 1 : chunks;   // k_site_bcast_smem: + the particle-constant segment
     const int64_t side = (smem && g->side.out != nullptr)
                              ? ceil_div(2 * g->side.K * g->side.N, mi::kBcastThreads) : 0;
     p.grid = dim3((unsigned)(chunks + side),
-                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? p.smem_p : mi::kBcastP)));
+                  (unsigned)ceil_div(g->K, mi::kBcastThreads * (smem ? kSmemP : mi::kBcastP)));
     return p;
   }
   int dense = -1;
@@ -1360,8 +1300,8 @@ bool smem_rank1(const mi_group* g, const Plan& p) {
   return g->num_slots == 1 && g->compute_grads && p.nseg >= 3 && p.nseg <= MI_REDUCE_MAX_SEG;
 }
 
-template <int FAM, int kSmemP>
-void launch_smem_p(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
+template <int FAM>
+void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
   const dim3 block(mi::kBcastThreads);
   // p.grid = (chunks + side blocks, particle blocks): the kernel takes them as one XCD-aware
   // dimension (see k_site_bcast_smem)
@@ -1374,18 +1314,10 @@ void launch_smem_p(const mi_group& G, const Plan& p, float* part, uint32_t* flag
   // l_k sum_i x_i), never the default
   if (env_int("MININF_AMD_BCAST_SUFFSTAT", 0) != 0)
     hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP, true>), grid, block, 0, s,
-                       G, part, p.nseg, gy, rank1, p.layout, flags);
+                       G, part, p.nseg, gy, rank1, p.chunk, flags);
   else
     hipLaunchKernelGGL((mi::k_site_bcast_smem<FAM, kSmemP>), grid, block, 0, s, G,
-                       part, p.nseg, gy, rank1, p.layout, flags);
-}
-
-template <int FAM>
-void launch_smem(const mi_group& G, const Plan& p, float* part, uint32_t* flags, hipStream_t s) {
-  if (p.smem_p == 8)
-    launch_smem_p<FAM, 8>(G, p, part, flags, s);
-  else
-    launch_smem_p<FAM, 4>(G, p, part, flags, s);
+                       part, p.nseg, gy, rank1, p.chunk, flags);
 }
 
 size_t workspace_bytes(const mi_group* g, const Plan& p) {

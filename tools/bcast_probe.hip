@@ -162,7 +162,91 @@ __global__ __launch_bounds__(256) void k_probe_lds(const float* __restrict__ x, 
   }
 }
 
-template <int P, int CHUNK, bool LOADS, int PREP = 0, bool POST = false, bool LDS = false>
+// Half of each chunk through the scalar unit (SGPR pairs), the other half staged in LDS and read
+// as broadcast ds_read_b128 (VGPR pairs), interleaved group by group: twice the FMAs per scalar
+// group of lookahead, the LDS at half the rate of k_probe_lds. Full chunks only (CHUNK | N not
+// required: the partial last chunk is skipped).
+template <int P, int CHUNK>
+__global__ __launch_bounds__(256) void k_probe_hyb(const float* __restrict__ x, const float* __restrict__ logits,
+                                                   int64_t N, int64_t K, float* __restrict__ part,
+                                                   unsigned long long* __restrict__ stamps) {
+  constexpr int kHalf = CHUNK / 2, kGroup = 32, kGroups = kHalf / kGroup;
+  static_assert(kHalf % kGroup == 0, "whole groups");
+  __shared__ float4 xl[kHalf / 4];
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  const int64_t c = blockIdx.x;
+  const int64_t i0 = c * CHUNK;
+  const int64_t kbase = (int64_t)blockIdx.y * (256 * P) + threadIdx.x;
+  double acc[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) acc[p] = 0.0;
+  if (i0 + CHUNK <= N) {
+    const float4* xg = reinterpret_cast<const float4*>(x + i0 + kHalf);
+    for (int q = threadIdx.x; q < kHalf / 4; q += 256) xl[q] = xg[q];
+    f32x2 ld[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const float l = logits[min(kbase + p * 256, K - 1)];
+      ld[p] = f32x2{l, l};
+    }
+    __syncthreads();
+    smem_float* xs = (smem_float*)(x + i0);
+    float xc[kGroup];
+#pragma unroll
+    for (int e = 0; e < kGroup; ++e) xc[e] = xs[e];
+    for (int g = 0; g < kGroups; g += 8) {
+      f32x2 in[2][P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) in[0][p] = in[1][p] = f32x2{0.0f, 0.0f};
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const int nxt = min(g + h + 1, kGroups - 1) * kGroup;
+        float xn[kGroup];
+#pragma unroll
+        for (int e = 0; e < kGroup; ++e) xn[e] = xs[nxt + e];
+        float4 vb[kGroup / 4];
+#pragma unroll
+        for (int q = 0; q < kGroup / 4; ++q) vb[q] = xl[(g + h) * (kGroup / 4) + q];
+#pragma unroll
+        for (int e = 0; e < kGroup; e += 2) {
+          const f32x2 xv = f32x2{xc[e], xc[e + 1]};
+#pragma unroll
+          for (int p = 0; p < P; ++p) in[0][p] = __builtin_elementwise_fma(xv, ld[p], in[0][p]);
+        }
+#pragma unroll
+        for (int q = 0; q < kGroup / 4; ++q) {
+          const f32x2 a = f32x2{vb[q].x, vb[q].y}, b = f32x2{vb[q].z, vb[q].w};
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            in[1][p] = __builtin_elementwise_fma(a, ld[p], in[1][p]);
+            in[1][p] = __builtin_elementwise_fma(b, ld[p], in[1][p]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < kGroup; ++e) xc[e] = xn[e];
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+        acc[p] += (double)((in[0][p].x + in[0][p].y) + (in[1][p].x + in[1][p].y));
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int64_t k = kbase + p * 256;
+    if (k < K) part[c * K + k] = (float)acc[p];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t b = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    stamps[4 * b + 0] = t0;
+    stamps[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    stamps[4 * b + 2] = __builtin_amdgcn_s_memtime() - c0;
+    stamps[4 * b + 3] = 0;
+  }
+}
+
+template <int P, int CHUNK, bool LOADS, int PREP = 0, bool POST = false, bool LDS = false, bool HYB = false>
 void run(const char* name, const float* x, const float* lg, int64_t N, int64_t K, float* part,
          unsigned long long* stamps) {
   const dim3 grid((unsigned)((N + CHUNK - 1) / CHUNK), (unsigned)((K + 256 * P - 1) / (256 * P)));
@@ -170,7 +254,8 @@ void run(const char* name, const float* x, const float* lg, int64_t N, int64_t K
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   auto launch = [&]() {
-    if (LDS) hipLaunchKernelGGL((k_probe_lds<P, CHUNK>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+    if (HYB) hipLaunchKernelGGL((k_probe_hyb<P, CHUNK>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
+    else if (LDS) hipLaunchKernelGGL((k_probe_lds<P, CHUNK>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
     else hipLaunchKernelGGL((k_probe<P, CHUNK, LOADS, PREP, POST>), grid, dim3(256), 0, 0, x, lg, N, K, part, stamps);
   };
   for (int w = 0; w < 5; ++w) launch();
@@ -219,12 +304,13 @@ int main() {
   for (int64_t k = 0; k < K; ++k) hl[k] = 0.3f + 0.001f * (float)(k % 100);
   (void)hipMemcpy(x, hx.data(), N * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(lg, hl.data(), K * 4, hipMemcpyHostToDevice);
-  run<4, 3936, true>("P4_C3936", x, lg, N, K, part, stamps);
-  run<4, 3936, false>("P4_C3936_noloads", x, lg, N, K, part, stamps);
-  run<4, 3936, true, 0, false, true>("P4_C3936_lds", x, lg, N, K, part, stamps);
-  run<8, 1984, true, 0, false, true>("P8_C1984_lds", x, lg, N, K, part, stamps);
-  run<8, 1984, true>("P8_C1984", x, lg, N, K, part, stamps);
-  run<4, 3936, true>("P4_C3936", x, lg, N, K, part, stamps);
-  run<4, 3936, true, 0, false, true>("P4_C3936_lds", x, lg, N, K, part, stamps);
+  run<4, 4096, true>("P4_C4096", x, lg, N, K, part, stamps);
+  run<4, 4096, true, 0, false, false, true>("P4_C4096_hyb", x, lg, N, K, part, stamps);
+  run<4, 3968, true>("P4_C3968", x, lg, N, K, part, stamps);
+  run<4, 3968, true, 0, false, false, true>("P4_C3968_hyb", x, lg, N, K, part, stamps);
+  run<8, 2048, true>("P8_C2048", x, lg, N, K, part, stamps);
+  run<8, 2048, true, 0, false, false, true>("P8_C2048_hyb", x, lg, N, K, part, stamps);
+  run<4, 4096, true>("P4_C4096", x, lg, N, K, part, stamps);
+  run<4, 4096, true, 0, false, false, true>("P4_C4096_hyb", x, lg, N, K, part, stamps);
   return 0;
 }

@@ -49,14 +49,16 @@ def build_variant(name="c2tl"):
     if (threadIdx.x == 0) { g_tl[b * 8] = T0; g_tl[b * 8 + 4] = __builtin_amdgcn_s_memrealtime(); g_tl[b * 8 + 5] = 1; }
     return;
   }""")
-    rep("""  for (int p = 0; p < kSmemP; ++p) ld[p] = f32x2{lg[p], lg[p]};
-  double acc[kSmemP];""", """  for (int p = 0; p < kSmemP; ++p) ld[p] = f32x2{lg[p], lg[p]};
-  if (threadIdx.x == 0) { float z = 0.f;
+    rep("""  double acc[kSmemP];
 #pragma unroll
-    for (int p = 0; p < kSmemP; ++p) z += lg[p];
+  for (int p = 0; p < kSmemP; ++p) acc[p] = 0.0;""", """  if (threadIdx.x == 0) { float z = 0.f;
+#pragma unroll
+    for (int p = 0; p < kSmemP; ++p) z += ld[p].x;
     __asm__ volatile("" :: "v"(z)); }
   const unsigned long long T1 = __builtin_amdgcn_s_memrealtime();
-  double acc[kSmemP];""")
+  double acc[kSmemP];
+#pragma unroll
+  for (int p = 0; p < kSmemP; ++p) acc[p] = 0.0;""")
     rep("""  // ---- chunk sum and support flags (vector loads, L2-resident by now)""",
         """  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();
   // ---- chunk sum and support flags (vector loads, L2-resident by now)""")
