@@ -675,18 +675,47 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     const int64_t ptile = ntile - 1;
     uint32_t pfl = 0u;
     float plp = 0.0f;
+    if (!ONESTAGE) {
 #pragma unroll
-    for (int s = 0; s < S::HS; ++s) {
-      const int p = 2 * s + h;
-      if (kk < K && p < P) {
-        Elem e;
-        if (L.prior.family == MI_BETA) eval_beta(L.prior.constant[0], L.prior.constant[1], thf[s], e);
-        else if (L.prior.family == MI_NORMAL) eval_normal(L.prior.constant[0], L.prior.constant[1], thf[s], e);
-        else eval_gamma(L.prior.constant[0], L.prior.constant[1], thf[s], e);
-        plp += e.lp;
-        pfl |= (e.param_bad ? MI_FLAG_PARAM : 0u) | (e.support_bad ? MI_FLAG_SUPPORT : 0u);
-        if (grads) part[((int64_t)(1 + p) * ntile + ptile) * K + kk] = (float)(L.prior.scale * (double)e.d[2]);
+      for (int s = 0; s < S::HS; ++s) {
+        const int p = 2 * s + h;
+        if (kk < K && p < P) {
+          Elem e;
+          if (L.prior.family == MI_BETA) eval_beta(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+          else if (L.prior.family == MI_NORMAL) eval_normal(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+          else eval_gamma(L.prior.constant[0], L.prior.constant[1], thf[s], e);
+          plp += e.lp;
+          pfl |= (e.param_bad ? MI_FLAG_PARAM : 0u) | (e.support_bad ? MI_FLAG_SUPPORT : 0u);
+          if (grads) part[((int64_t)(1 + p) * ntile + ptile) * K + kk] = (float)(L.prior.scale * (double)e.d[2]);
+        }
       }
+    } else {
+      // One-stage launches choose the family once, outside the unrolled features: this code runs
+      // in one wave of the launch, so its instructions are fetched cold, and the family test inside
+      // the loop (above) lays the three families' code out per feature (r06, tools/linear_timing.py:
+      // the 16 evaluations took 4.6 us in C4's launch, its last wave; 2.6 us hoisted). The
+      // multi-stage kernel keeps the loop above (its code measured 2 us slower hoisted, C3
+      // 313.8-314.2 vs 311.2-312.3 us per step, profiles/r06_ab.json ab17).
+      auto features = [&](auto eval) {
+#pragma unroll
+        for (int s = 0; s < S::HS; ++s) {
+          const int p = 2 * s + h;
+          if (kk < K && p < P) {
+            Elem e;
+            eval(thf[s], e);
+            plp += e.lp;
+            pfl |= (e.param_bad ? MI_FLAG_PARAM : 0u) | (e.support_bad ? MI_FLAG_SUPPORT : 0u);
+            if (grads) part[((int64_t)(1 + p) * ntile + ptile) * K + kk] = (float)(L.prior.scale * (double)e.d[2]);
+          }
+        }
+      };
+      const float pc0 = L.prior.constant[0], pc1 = L.prior.constant[1];
+      if (L.prior.family == MI_NORMAL)
+        features([&](float v, Elem& e) { eval_normal(pc0, pc1, v, e); });
+      else if (L.prior.family == MI_BETA)
+        features([&](float v, Elem& e) { eval_beta(pc0, pc1, v, e); });
+      else
+        features([&](float v, Elem& e) { eval_gamma(pc0, pc1, v, e); });
     }
     plp += __shfl_xor(plp, 32, kWave);   // the particle's two feature parities
     if (h == 0 && kk < K) {

@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "_timing", "libmininf_amd_lin.so")
+OUT = os.path.join(ROOT, "tools", "_variants", "lintiming", "libmininf_amd.so")   # (sent to the GPU box)
 
 
 def build():
@@ -91,8 +91,10 @@ def _phases(raw, label):
     rows = raw[raw.numel() % 8:].reshape(-1, 8)
     ok = (rows[:, 0] > 0) & ((rows[:, 1:] - rows[:, :-1]) >= 0).all(dim=1) & \
         ((rows[:, 7] - rows[:, 0]) < 1_000_000)
+    if not ok.any():
+        return
+    ok &= (rows[:, 0] - rows[ok][:, 0].median()).abs() < 1_000_000
     rows = rows[ok]
-    rows = rows[(rows[:, 0] - rows[:, 0].median()).abs() < 1_000_000]
     t = rows.double() / 100.0
     base = t[:, 0].min()
     names = ["entry->stage", "stage issue", "stage barrier", "tiles", "tile barrier", "combine",
@@ -108,6 +110,21 @@ def _phases(raw, label):
     print(f"  wave lifetime  mean {float(life.mean()):6.2f} us  max {float(life.max()):6.2f} us")
     start = t[:, 0] - base
     print(f"  entry          p50 {float(start.median()):6.2f}  max {float(start.max()):6.2f} us")
+    # the last waves to exit: (block, wave) and their phase durations
+    idx = torch.nonzero(ok).flatten()
+    exit_t = t[:, 7] - base
+    order = torch.argsort(exit_t, descending=True)[:6]
+    for j in order.tolist():
+        w = int(idx[j])
+        ph = " ".join(f"{float(t[j, i + 1] - t[j, i]):5.2f}" for i in range(7))
+        print(f"  late: block {w // 4:4d} wave {w % 4}  entry {float(start[j]):5.2f}  exit "
+              f"{float(exit_t[j]):6.2f}  phases {ph}")
+    blocks = idx // 4
+    for lo, hi in ((0, 1), (1, 16), (16, 256), (256, 512)):
+        sel = (blocks >= lo) & (blocks < hi)
+        if sel.any():
+            print(f"  blocks [{lo},{hi}): exit p50 {float(exit_t[sel].median()):6.2f} max "
+                  f"{float(exit_t[sel].max()):6.2f} us")
 
 
 def run_bench(config="c4"):
@@ -134,6 +151,18 @@ def run_bench(config="c4"):
         optimizer.step()
         if step >= 5:
             _phases(raw, f"{config} step {step}")
+            fn = getattr(nat.lib(), "mi_debug_linear_prior", None)
+            if fn is not None:   # the folded prior's sub-phases (timing builds)
+                import numpy as np
+                buf = np.zeros(64 * 6, dtype=np.uint64)
+                fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+                fn(buf.ctypes.data, buf.nbytes)
+                r = buf.reshape(64, 6).astype(np.int64)
+                r = r[r[:, 1] > 0]
+                for row in r:
+                    d = np.diff(row[:5]) / 100.0
+                    print(f"  prior wave (block {row[5]}): partials-start->prior {d[0]:5.2f}  "
+                          f"kernargs {d[1]:5.2f}  evals {d[2]:5.2f}  stores+flags {d[3]:5.2f} us")
     torch.cuda.synchronize()
 
 
