@@ -606,7 +606,9 @@ __global__ __launch_bounds__(kBcastThreads) void k_site_bcast_smem(const mi_grou
   const int64_t padded = (chunks + 7) / 8 * 8;
   const int64_t b = blockIdx.x;
   if (b >= padded * gy) {   // workgroups past the chunks: the side job (mi_side)
+    const unsigned long long ts = span_begin(G.stamps);   // (the launch's span includes them)
     beta_side_block(G.side, b - padded * gy);
+    span_end(G.stamps, ts);
     return;
   }
   const int64_t c = (b / (8 * gy)) * 8 + b % 8;
