@@ -356,7 +356,9 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
 
   // ---- staging: X quads and (y, mask) of one stage into registers, then into LDS ---------------
   float4 xq[S::QPT];
-  float2 ymr = make_float2(0.0f, 0.0f);
+  float yraw = 0.0f;          // the stage's (y, mask) of row tid, as loaded
+  uint32_t mraw = 1u;
+  int64_t staged_row0 = 0;    // the stage whose loads xq / yraw / mraw hold
   // Source rows first (one uniform branch on how rows are given), then every X quad and the
   // (y, mask) of the stage issued together with no wait in between: a guarded load per quad
   // compiled to a branch and a wait per load, one memory round trip each.
@@ -383,35 +385,41 @@ __global__ __launch_bounds__(NT, MINW) void k_linear_mfma(const mi_linear L, int
     for (int q = 0; q < S::QPT; ++q) {
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
-      const float4 v = *reinterpret_cast<const float4*>(L.x + src[q] * L.x_stride_i +
-                                                        4 * (4 * c4 < P ? c4 : 0));
-      const bool in = row0 + row < N && 4 * c4 < P;
-      xq[q] = make_float4(keep_if(v.x, in), keep_if(v.y, in), keep_if(v.z, in), keep_if(v.w, in));
+      (void)row;
+      xq[q] = *reinterpret_cast<const float4*>(L.x + src[q] * L.x_stride_i +
+                                               4 * (4 * c4 < P ? c4 : 0));
     }
-    const float yv = L.value[src[S::QPT] * L.value_stride_i];
-    const bool mv = L.mask == nullptr ? true : L.mask[src[S::QPT] * L.mask_stride_i] != 0;
-    if (tid < S::CH) {
-      const int64_t row = row0 + tid;
-      float y = 0.0f, m = 0.0f;
-      if (row < N) {
-        y = yv;
-        m = mv ? 1.0f : 0.0f;
-        const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
-        fl |= (m != 0.0f && bad) ? MI_FLAG_SUPPORT : 0u;
-      }
-      ymr = make_float2(m != 0.0f ? y : 0.0f, m);
-    }
+    yraw = L.value[src[S::QPT] * L.value_stride_i];
+    mraw = L.mask == nullptr ? 1u : (uint32_t)L.mask[src[S::QPT] * L.mask_stride_i];
+    staged_row0 = row0;
   };
+  // The loads' values are first used here (rows past N and features past P zeroed, the (y, mask)
+  // checks), so nothing waits for a stage's loads before store time: in one-stage launches the
+  // theta draw runs while the row gathers are in flight (r06: zeroing them in load_stage made the
+  // draw wait for them; C4 32.6 vs 33.9 us per step, profiles/r06_ab.json ab24/ab25).
   auto store_stage = [&]() {
+    const int64_t row0 = staged_row0;
 #pragma unroll
     for (int q = 0; q < S::QPT; ++q) {
       const int e = tid + q * kMfThreads;
       const int row = e / (S::PM / 4), c4 = e % (S::PM / 4);
+      const bool in = row0 + row < N && 4 * c4 < P;
+      const float4 v = xq[q];
       float* dst = xs + row * S::RSTR + 2 * c4;
-      *reinterpret_cast<float2*>(dst) = make_float2(xq[q].x, xq[q].z);           // even features
-      *reinterpret_cast<float2*>(dst + S::HS) = make_float2(xq[q].y, xq[q].w);   // odd features
+      *reinterpret_cast<float2*>(dst) = make_float2(keep_if(v.x, in), keep_if(v.z, in));           // even features
+      *reinterpret_cast<float2*>(dst + S::HS) = make_float2(keep_if(v.y, in), keep_if(v.w, in));   // odd features
     }
-    if (tid < S::CH) yms[tid] = ymr;
+    if (tid < S::CH) {
+      const int64_t row = row0 + tid;
+      float y = 0.0f, m = 0.0f;
+      if (row < N) {
+        y = yraw;
+        m = mraw != 0u ? 1.0f : 0.0f;
+        const bool bad = FAMILY == MI_NORMAL ? (y != y) : !(y == 0.0f || y == 1.0f);
+        fl |= (m != 0.0f && bad) ? MI_FLAG_SUPPORT : 0u;
+      }
+      yms[tid] = make_float2(m != 0.0f ? y : 0.0f, m);
+    }
   };
 
   // The block's particles' draws through the (still unused) X staging buffer into thf: called by

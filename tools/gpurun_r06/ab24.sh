@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 6 A/B 24: multi-stage linear kernel with the theta fragment through LDS and the stage's loads
+# masked at store time (tools/_variants/c3ths) against the tree, C3 and C4.
+set -u
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+fatal() { [ "$1" -eq 124 ] || [ "$1" -eq 137 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+V=$GRAFT_REPO_ROOT/tools/_variants/c3ths/libmininf_amd.so
+MININF_AMD_LIB=$V timeout -k 10 400 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_prior_fold.py tests/test_gpu_linear.py tests/test_gpu_linear_draw.py tests/test_gpu_fullsize.py tests/test_gpu_minibatch.py > gpurun_out/ab24_tests.log 2>&1; rc=$?
+echo "tests rc=$rc $(tail -1 gpurun_out/ab24_tests.log)"; fatal $rc && exit $rc
+run() { local tag=$1; local cfg=$2; shift 2
+  env "$@" timeout -k 10 150 python3 -u bench.py --config $cfg --no-other-configs --no-cpu-baseline --steps 240 > gpurun_out/ab24_$tag.json 2> gpurun_out/ab24_$tag.err; local rc=$?
+  echo "$tag rc=$rc $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab24_$tag.json').read().strip().splitlines()[-1]); print(round(d['ms_per_step']*1e3,2), round(d['roofline']['kernel_ms']*1e3,2), round(d['roofline']['frac'],3))" 2>&1)"
+  if fatal $rc; then exit $rc; fi; }
+for r in 1 2 3; do
+  run c3tree$r c3
+  run c3ths$r c3 MININF_AMD_LIB=$V
+done
+run c4tree1 c4
+run c4ths1 c4 MININF_AMD_LIB=$V
+exit 0
