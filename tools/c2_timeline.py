@@ -39,12 +39,16 @@ def build_variant(name="c2tl"):
     rep("constexpr int kSmemMaxChunk", "__device__ unsigned long long g_tl[8192 * 8];\nconstexpr int kSmemMaxChunk")
     rep("""  const int64_t b = blockIdx.x;
   if (b >= padded * gy) {   // workgroups past the chunks: the side job (mi_side)
+    const unsigned long long ts = span_begin(G.stamps);   // (the launch's span includes them)
     beta_side_block(G.side, b - padded * gy);
+    span_end(G.stamps, ts);
     return;
   }""", """  const int64_t b = blockIdx.x;
   const unsigned long long T0 = __builtin_amdgcn_s_memrealtime();
   if (b >= padded * gy) {   // workgroups past the chunks: the side job (mi_side)
+    const unsigned long long ts = span_begin(G.stamps);
     beta_side_block(G.side, b - padded * gy);
+    span_end(G.stamps, ts);
     __syncthreads();
     if (threadIdx.x == 0) { g_tl[b * 8] = T0; g_tl[b * 8 + 4] = __builtin_amdgcn_s_memrealtime(); g_tl[b * 8 + 5] = 1; }
     return;
